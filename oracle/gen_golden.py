@@ -1,0 +1,333 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE itself.
+
+TEST INFRASTRUCTURE.  Runs only in the build container, where /root/reference exists:
+`make -C oracle ref` compiles the reference's own module/rs.c and system/fec.c (read in
+place, never copied) into oracle/_ref/, and this script drives those libraries through
+ctypes on seeded synthetic inputs (quicknet_amd/synth.py).  The outputs are committed as
+small .npz fixtures; the tests then pin both the CPU restatement (oracle/liboracle.so)
+and the HIP product path against them on the GPU box, where the reference is absent.
+
+    python oracle/gen_golden.py            # rewrites tests/golden/*.npz
+
+Reference entry points driven (file:line in /root/reference):
+  reed_solomon_init/new/encode/reconstruct/error   module/rs.c:382,387,574,598,649
+  fec_new/fec_encode/fec_decode/fec_free           system/fec.c:653,714,821,639
+"""
+import ctypes as C
+import hashlib
+import itertools
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+from quicknet_amd.synth import synth_bytes  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+class RS(C.Structure):  # module/rs.h:7-13
+    _fields_ = [("data_shards", C.c_int), ("parity_shards", C.c_int), ("shards", C.c_int),
+                ("m", C.POINTER(C.c_ubyte)), ("parity", C.POINTER(C.c_ubyte))]
+
+
+class FecParms(C.Structure):  # module/fec.c:633-636
+    _fields_ = [("k", C.c_int), ("n", C.c_int), ("enc_matrix", C.POINTER(C.c_ubyte))]
+
+
+def load_ref():
+    rs = C.CDLL(os.path.join(HERE, "_ref", "libref_rs.so"))
+    fec = C.CDLL(os.path.join(HERE, "_ref", "libref_fec.so"))
+    rs.reed_solomon_new.restype = C.POINTER(RS)
+    rs.reed_solomon_new.argtypes = [C.c_int, C.c_int]
+    rs.reed_solomon_release.argtypes = [C.POINTER(RS)]
+    rs.reed_solomon_encode.argtypes = [C.POINTER(RS), C.POINTER(C.c_void_p), C.c_int, C.c_int]
+    rs.reed_solomon_reconstruct.argtypes = [C.POINTER(RS), C.POINTER(C.c_void_p), C.c_void_p, C.c_int, C.c_int]
+    fec.fec_new.restype = C.POINTER(FecParms)
+    fec.fec_new.argtypes = [C.c_int, C.c_int]
+    fec.fec_free.argtypes = [C.POINTER(FecParms)]
+    fec.fec_encode.argtypes = [C.POINTER(FecParms), C.POINTER(C.c_void_p), C.c_void_p, C.c_int, C.c_int]
+    fec.fec_decode.argtypes = [C.POINTER(FecParms), C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.c_int]
+    rs.reed_solomon_init()
+    return rs, fec
+
+
+def ptr(a, off=0):
+    return a.ctypes.data + off
+
+
+def rs_matrix(rs, k, m):
+    h = rs.reed_solomon_new(k, m)
+    if not h:
+        return None, rs.reed_solomon_error()
+    p = np.ctypeslib.as_array(h.contents.parity, shape=(m * k,)).copy()
+    full = np.ctypeslib.as_array(h.contents.m, shape=((k + m) * k,)).copy()
+    rs.reed_solomon_release(h)
+    return (p.reshape(m, k), full.reshape(k + m, k)), 0
+
+
+def fec_matrix(fec, k, n):
+    h = fec.fec_new(k, n)
+    if not h:
+        return None
+    full = np.ctypeslib.as_array(h.contents.enc_matrix, shape=(n * k,)).copy().reshape(n, k)
+    fec.fec_free(h)
+    return full
+
+
+def gen_matrices(rs, fec):
+    out = {}
+    rs_shapes = [(1, 1), (2, 1), (3, 2), (4, 2), (7, 1), (10, 3), (16, 4), (32, 8), (64, 32),
+                 (128, 127), (200, 55), (254, 1), (1, 254)]
+    for k, m in rs_shapes:
+        (p, full), err = rs_matrix(rs, k, m)
+        assert err == 0
+        out[f"rs_{k}_{m}"] = p
+        out[f"rsfull_{k}_{m}"] = full
+    errs = []
+    for k, m in [(0, 1), (1, 0), (200, 56), (-1, 3), (255, 1)]:
+        res, err = rs_matrix(rs, k, m)
+        assert res is None
+        errs.append((k, m, err))
+    out["rs_errors"] = np.array(errs, dtype=np.int32)
+    fec_shapes = [(1, 1), (1, 2), (2, 4), (3, 5), (5, 8), (4, 6), (3, 4), (4, 5), (5, 6), (7, 8),
+                  (10, 13), (16, 20), (4, 4), (32, 40), (100, 150), (128, 256), (200, 255),
+                  (256, 256), (255, 256), (1, 256), (2, 3)]
+    for k, n in fec_shapes:
+        full = fec_matrix(fec, k, n)
+        assert full is not None
+        out[f"fec_{k}_{n}"] = full
+    bad = []
+    for k, n in [(257, 257), (5, 4), (3, 257)]:
+        bad.append((k, n, 0 if fec_matrix(fec, k, n) is None else 1))
+    out["fec_errors"] = np.array(bad, dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, "matrices.npz"), **out)
+    return out
+
+
+ENC_CASES = [(2, 1), (4, 2), (10, 3), (16, 4), (7, 1), (3, 2)]
+ENC_LENS = [1, 8, 1024, 1400, 37]
+ENC_GROUPS = 4
+
+
+def gen_encode(rs, fec):
+    out = {}
+    seed = 0xE0C0DE00
+    for (k, m), B in itertools.product(ENC_CASES, ENC_LENS):
+        n = k + m
+        seed += 1
+        G = ENC_GROUPS
+        data = synth_bytes(seed, G * k * B).reshape(G * k, B)
+        # rs.c: batched encode over the pointer layout (rs.c:574-588)
+        par = np.full((G * m, B), 0x5A, dtype=np.uint8)
+        h = rs.reed_solomon_new(k, m)
+        ptrs = (C.c_void_p * (G * n))(*([ptr(data, i * B) for i in range(G * k)] +
+                                         [ptr(par, i * B) for i in range(G * m)]))
+        assert rs.reed_solomon_encode(h, ptrs, G * n, B) == 0
+        rs.reed_solomon_release(h)
+        # fec.c: one fec_encode per parity index (the get_fec_encoded_pkt pattern,
+        # network/FecCodecBuf.cpp:151)
+        fpar = np.full((G * m, B), 0xA5, dtype=np.uint8)
+        fh = fec.fec_new(k, n)
+        for g in range(G):
+            src = (C.c_void_p * k)(*[ptr(data, (g * k + i) * B) for i in range(k)])
+            for j in range(m):
+                fec.fec_encode(fh, src, C.c_void_p(ptr(fpar, (g * m + j) * B)), k + j, B)
+        # index < k is a copy; index >= n leaves dst untouched
+        cp = np.zeros(B, dtype=np.uint8)
+        src = (C.c_void_p * k)(*[ptr(data, i * B) for i in range(k)])
+        fec.fec_encode(fh, src, C.c_void_p(ptr(cp)), k - 1, B)
+        untouched = np.full(B, 0x33, dtype=np.uint8)
+        fec.fec_encode(fh, src, C.c_void_p(ptr(untouched)), n, B)
+        fec.fec_free(fh)
+        key = f"{k}_{m}_{B}"
+        out[f"seed_{key}"] = np.array([seed], dtype=np.uint64)
+        out[f"rs_{key}"] = par
+        out[f"fec_{key}"] = fpar
+        out[f"fcopy_{key}"] = cp
+        out[f"fbad_{key}"] = untouched
+    # the rs.c column-0 zero-coefficient quirk: mul() with c == 0 leaves dst stale
+    # (rs.c:116-117).  Poke a zero into the public parity matrix and encode over 0x5A.
+    k, m, B, G = 4, 2, 16, 2
+    data = synth_bytes(0xE0C0DEFF, G * k * B).reshape(G * k, B)
+    par = np.full((G * m, B), 0x5A, dtype=np.uint8)
+    h = rs.reed_solomon_new(k, m)
+    h.contents.parity[0 * k + 0] = 0
+    h.contents.parity[1 * k + 2] = 0
+    pm = np.ctypeslib.as_array(h.contents.parity, shape=(m * k,)).copy()
+    ptrs = (C.c_void_p * (G * (k + m)))(*([ptr(data, i * B) for i in range(G * k)] +
+                                         [ptr(par, i * B) for i in range(G * m)]))
+    rs.reed_solomon_encode(h, ptrs, G * (k + m), B)
+    rs.reed_solomon_release(h)
+    out["quirk_seed"] = np.array([0xE0C0DEFF], dtype=np.uint64)
+    out["quirk_matrix"] = pm.reshape(m, k)
+    out["quirk_parity"] = par
+    # survey KAT: data[i][b] = (8 i + b) & 255, B = 8
+    for k, m in [(10, 3), (4, 2)]:
+        B = 8
+        data = np.array([[(8 * i + b) & 255 for b in range(B)] for i in range(k)], dtype=np.uint8)
+        par = np.zeros((m, B), dtype=np.uint8)
+        h = rs.reed_solomon_new(k, m)
+        ptrs = (C.c_void_p * (k + m))(*([ptr(data, i * B) for i in range(k)] + [ptr(par, i * B) for i in range(m)]))
+        rs.reed_solomon_encode(h, ptrs, k + m, B)
+        rs.reed_solomon_release(h)
+        fh = fec.fec_new(k, k + m)
+        fpar = np.zeros((m, B), dtype=np.uint8)
+        src = (C.c_void_p * k)(*[ptr(data, i * B) for i in range(k)])
+        for j in range(m):
+            fec.fec_encode(fh, src, C.c_void_p(ptr(fpar, j * B)), k + j, B)
+        fec.fec_free(fh)
+        out[f"kat_rs_{k}_{m}"] = par
+        out[f"kat_fec_{k}_{m}"] = fpar
+    np.savez_compressed(os.path.join(OUT, "encode.npz"), **out)
+
+
+def rs_reconstruct_batch(rs, k, m, data, par, marks, B):
+    """Run the reference reconstruct on a contiguous batch (modified in place)."""
+    G = data.shape[0] // k
+    n = k + m
+    h = rs.reed_solomon_new(k, m)
+    ptrs = (C.c_void_p * (G * n))(*([ptr(data, i * B) for i in range(G * k)] +
+                                     [ptr(par, i * B) for i in range(G * m)]))
+    rc = rs.reed_solomon_reconstruct(h, ptrs, C.c_void_p(ptr(marks)), G * n, B)
+    rs.reed_solomon_release(h)
+    return rc
+
+
+def all_masks(n):
+    return np.array([[(mask >> i) & 1 for i in range(n)] for mask in range(1 << n)], dtype=np.uint8)
+
+
+def gen_reconstruct(rs):
+    """rs.c reconstruct, exhaustive over every erasure mask for (4,2) and (10,3), sampled
+    for (16,4).  Two payload kinds: 'cons' (parity = encode(data)) and 'incons' (random
+    parity) -- the latter pins the survivor-selection rule (rs.c:620-629) bit for bit.
+    Erased data buffers are pre-filled with 0x5A so an unwritten output shows."""
+    out = {}
+    cases = [(4, 2, 16, None), (10, 3, 8, None), (16, 4, 8, 2000), (2, 1, 5, None), (3, 2, 33, None)]
+    for k, m, B, sample in cases:
+        n = k + m
+        if sample is None:
+            gmarks = all_masks(n)
+        else:
+            gen = np.random.default_rng(0x5EED + k)
+            gmarks = (gen.random((sample, n)) < 0.2).astype(np.uint8)
+        G = gmarks.shape[0]
+        seed = 0x7EC0 + 31 * k + m
+        data0 = synth_bytes(seed, G * k * B).reshape(G * k, B)
+        # consistent parity via the reference encoder
+        par_c = np.zeros((G * m, B), dtype=np.uint8)
+        h = rs.reed_solomon_new(k, m)
+        ptrs = (C.c_void_p * (G * n))(*([ptr(data0, i * B) for i in range(G * k)] +
+                                         [ptr(par_c, i * B) for i in range(G * m)]))
+        rs.reed_solomon_encode(h, ptrs, G * n, B)
+        rs.reed_solomon_release(h)
+        par_i = synth_bytes(seed ^ 0xFFFF, G * m * B).reshape(G * m, B)
+        marks = np.concatenate([gmarks[:, :k].reshape(-1), gmarks[:, k:].reshape(-1)]).astype(np.uint8)
+        key = f"{k}_{m}_{B}"
+        for kind, par in (("cons", par_c), ("incons", par_i)):
+            d = data0.copy()
+            d[marks[:G * k] == 1] = 0x5A
+            p = par.copy()
+            rc = rs_reconstruct_batch(rs, k, m, d, p, marks, B)
+            assert np.array_equal(p, par)  # parity is never regenerated
+            if kind == "cons":  # recovered == original where recoverable: a digest suffices
+                out[f"{kind}_{key}"] = np.frombuffer(hashlib.sha256(d.tobytes()).digest(), dtype=np.uint8)
+            else:
+                out[f"{kind}_{key}"] = d
+            out[f"rc_{kind}_{key}"] = np.array([rc], dtype=np.int32)
+        out[f"seed_{key}"] = np.array([seed], dtype=np.uint64)
+        out[f"marks_{key}"] = gmarks
+        out[f"parc_{key}"] = np.frombuffer(hashlib.sha256(par_c.tobytes()).digest(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "reconstruct.npz"), **out)
+
+
+def gen_fec_decode(fec):
+    """fec.c fec_decode on k received packets: NetFecCodec order (first k valid in group
+    order), random arrival order (exercises shuffle, fec.c:738-771), and error cases
+    (duplicate data index -> conflict, index >= n -> invalid)."""
+    out = {}
+    gen = np.random.default_rng(0xDEC0DE)
+    cases = [(2, 4), (3, 5), (5, 8), (4, 6), (3, 4), (4, 5), (5, 6), (7, 8), (10, 13), (16, 20), (1, 3)]
+    B = 32
+    for k, n in cases:
+        fh = fec.fec_new(k, n)
+        full = np.ctypeslib.as_array(fh.contents.enc_matrix, shape=(n * k,)).copy().reshape(n, k)
+        T = 24
+        seed = 0xFEC0 + 97 * k + n
+        data = synth_bytes(seed, T * k * B).reshape(T, k, B)
+        par_rand = synth_bytes(seed ^ 0xABCD, T * (n - k) * B).reshape(T, n - k, B)
+        idx_in, idx_out, pk_in, pk_out, rcs = [], [], [], [], []
+        for t in range(T):
+            # full packet set of this trial: data + (consistent for even t, random for odd t) parity
+            pkts = np.zeros((n, B), dtype=np.uint8)
+            pkts[:k] = data[t]
+            if t % 2 == 0:
+                src = (C.c_void_p * k)(*[ptr(data[t], i * B) for i in range(k)])
+                for j in range(k, n):
+                    fec.fec_encode(fh, src, C.c_void_p(ptr(pkts, j * B)), j, B)
+            else:
+                pkts[k:] = par_rand[t]
+            mode = t % 4
+            if mode in (0, 1):       # NetFecCodec order: first k valid in group order
+                lost = gen.choice(n, size=min(n - k, gen.integers(0, n - k + 1)), replace=False)
+                valid = [i for i in range(n) if i not in set(lost.tolist())][:k]
+            elif mode == 2:          # arbitrary arrival order
+                valid = gen.choice(n, size=k, replace=False).tolist()
+            else:                    # error cases
+                valid = list(range(k))
+                if k >= 2 and t % 8 == 3:
+                    valid[1] = valid[0]          # duplicate data index -> shuffle conflict
+                else:
+                    valid[-1] = n + 1            # invalid index -> build_decode_matrix fails
+            idx = np.array(valid, dtype=np.int32)
+            buf = np.zeros((k, B), dtype=np.uint8)
+            for s, i in enumerate(valid):
+                buf[s] = pkts[i] if 0 <= i < n else 0xEE
+            bptrs = (C.c_void_p * k)(*[ptr(buf, s * B) for s in range(k)])
+            ia = (C.c_int * k)(*idx.tolist())
+            before = buf.copy()
+            rc = fec.fec_decode(fh, bptrs, ia, B)
+            # read back the (possibly permuted) pointer array: which original slot each now points to
+            perm = [(bptrs[s] - ptr(buf)) // B for s in range(k)]
+            after = np.stack([buf[p] for p in perm])
+            idx_in.append(idx)
+            idx_out.append(np.array(list(ia), dtype=np.int32))
+            pk_in.append(before)
+            pk_out.append(after)
+            rcs.append(rc)
+        fec.fec_free(fh)
+        key = f"{k}_{n}"
+        out[f"matrix_{key}"] = full
+        out[f"idx_in_{key}"] = np.stack(idx_in)
+        out[f"idx_out_{key}"] = np.stack(idx_out)
+        out[f"pk_in_{key}"] = np.stack(pk_in)
+        out[f"pk_out_{key}"] = np.stack(pk_out)
+        out[f"rc_{key}"] = np.array(rcs, dtype=np.int32)
+    np.savez_compressed(os.path.join(OUT, "fec_decode.npz"), **out)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    rs, fec = load_ref()
+    gen_matrices(rs, fec)
+    gen_encode(rs, fec)
+    gen_reconstruct(rs)
+    gen_fec_decode(fec)
+    manifest = {
+        "generator": "oracle/gen_golden.py",
+        "reference": "skywind3000/QuickNet @ 2024-10-08, module/rs.c + system/fec.c compiled by oracle/Makefile",
+        "files": sorted(f for f in os.listdir(OUT) if f.endswith(".npz")),
+    }
+    with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print("wrote", manifest["files"])
+
+
+if __name__ == "__main__":
+    main()

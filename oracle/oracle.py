@@ -1,0 +1,148 @@
+"""ctypes front-end for the parity checkers -- TEST INFRASTRUCTURE ONLY.
+
+Importable only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+
+* ``Oracle``   -- oracle/liboracle.so, the CPU restatement of the reference codecs
+                  (oracle/qfec_oracle.c; every function cites module/rs.c or module/fec.c).
+* ``RefCodec`` -- oracle/_ref/libref_{rs,fec}.so, the reference's own C compiled from
+                  /root/reference by ``make -C oracle ref`` (present only when built).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+U8P = C.POINTER(C.c_ubyte)
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+class Oracle:
+    def __init__(self, path=None):
+        path = path or os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        L = C.CDLL(path)
+        vp, i, ll = C.c_void_p, C.c_int, C.c_longlong
+        L.orc_init()
+        L.orc_cauchy_parity.argtypes = [i, i, vp]
+        L.orc_vandermonde_parity.argtypes = [i, i, vp]
+        L.orc_invert.argtypes = [vp, i]
+        L.orc_rs_encode_contig.argtypes = [i, i, vp, vp, vp, ll, i, ll]
+        L.orc_fec_encode_contig.argtypes = [i, i, vp, vp, vp, ll, i, ll]
+        L.orc_rs_reconstruct_contig.argtypes = [i, i, vp, vp, vp, vp, ll, i, ll]
+        L.orc_fec_reconstruct_contig.argtypes = [i, i, vp, vp, vp, vp, ll, i, ll]
+        L.orc_fec_reconstruct_contig.restype = ll
+        L.orc_fec_decode.argtypes = [i, i, vp, C.POINTER(vp), C.POINTER(C.c_int), i]
+        L.orc_fec_encode.argtypes = [i, i, vp, C.POINTER(vp), vp, i, i]
+        L.orc_mul.restype = C.c_ubyte
+        L.orc_mul.argtypes = [C.c_ubyte, C.c_ubyte]
+        L.orc_inv.restype = C.c_ubyte
+        L.orc_inv.argtypes = [C.c_ubyte]
+        L.orc_byte_sum.restype = C.c_uint32
+        L.orc_byte_sum.argtypes = [vp, ll]
+        self.L = L
+
+    # -- matrices
+    def cauchy(self, k, m):
+        out = np.zeros((max(m, 1), max(k, 1)), dtype=np.uint8)
+        rc = self.L.orc_cauchy_parity(k, m, _p(out))
+        return None if rc else out
+
+    def vandermonde(self, k, n):
+        """Parity rows k..n-1 of the fec.c systematic matrix ((n-k) x k)."""
+        out = np.zeros((max(n - k, 1), max(k, 1)), dtype=np.uint8)
+        rc = self.L.orc_vandermonde_parity(k, n, _p(out))
+        return None if rc else out[: n - k]
+
+    def invert(self, mat):
+        a = np.ascontiguousarray(mat, dtype=np.uint8).copy()
+        rc = self.L.orc_invert(_p(a), a.shape[0])
+        return None if rc else a
+
+    def mul(self, a, b):
+        return int(self.L.orc_mul(a, b))
+
+    # -- contiguous batches: data[G][k][pitch], parity[G][m][pitch]
+    def rs_encode(self, rows, data, parity, length):
+        G, k, pitch = data.shape
+        m = parity.shape[1]
+        self.L.orc_rs_encode_contig(k, m, _p(np.ascontiguousarray(rows)), _p(data), _p(parity), G, length, pitch)
+
+    def fec_encode(self, rows, data, parity, length):
+        G, k, pitch = data.shape
+        m = parity.shape[1]
+        self.L.orc_fec_encode_contig(k, m, _p(np.ascontiguousarray(rows)), _p(data), _p(parity), G, length, pitch)
+
+    def rs_reconstruct(self, rows, data, parity, marks_rs, length):
+        G, k, pitch = data.shape
+        m = parity.shape[1]
+        return self.L.orc_rs_reconstruct_contig(k, m, _p(np.ascontiguousarray(rows)), _p(data), _p(parity),
+                                                _p(marks_rs), G, length, pitch)
+
+    def fec_reconstruct(self, rows, data, parity, marks_rs, length):
+        G, k, pitch = data.shape
+        m = parity.shape[1]
+        return self.L.orc_fec_reconstruct_contig(k, m, _p(np.ascontiguousarray(rows)), _p(data), _p(parity),
+                                                 _p(marks_rs), G, length, pitch)
+
+    def fec_decode(self, k, n, full, pkts, idx):
+        """fec_decode on a copy: returns (rc, pkts_after[k][B], idx_after)."""
+        buf = np.ascontiguousarray(pkts, dtype=np.uint8).copy()
+        B = buf.shape[1]
+        base = buf.ctypes.data
+        ptrs = (C.c_void_p * k)(*[base + s * B for s in range(k)])
+        ia = (C.c_int * k)(*[int(x) for x in idx])
+        rc = self.L.orc_fec_decode(k, n, _p(np.ascontiguousarray(full)), ptrs, ia, B)
+        after = np.stack([buf[(ptrs[s] - base) // B] for s in range(k)])
+        return rc, after, np.array(list(ia), dtype=np.int32)
+
+    def byte_sum(self, a):
+        return int(self.L.orc_byte_sum(_p(a), a.size))
+
+
+class RS(C.Structure):  # module/rs.h:7-13
+    _fields_ = [("data_shards", C.c_int), ("parity_shards", C.c_int), ("shards", C.c_int),
+                ("m", U8P), ("parity", U8P)]
+
+
+class RefCodec:
+    """The reference's own codecs (oracle/_ref), for the CPU baseline and cross-checks."""
+
+    def __init__(self):
+        d = os.path.join(HERE, "_ref")
+        self.rs = C.CDLL(os.path.join(d, "libref_rs.so"))
+        self.fec = C.CDLL(os.path.join(d, "libref_fec.so"))
+        self.rs.reed_solomon_new.restype = C.POINTER(RS)
+        self.rs.reed_solomon_new.argtypes = [C.c_int, C.c_int]
+        self.rs.reed_solomon_release.argtypes = [C.POINTER(RS)]
+        self.rs.reed_solomon_encode.argtypes = [C.POINTER(RS), C.POINTER(C.c_void_p), C.c_int, C.c_int]
+        self.rs.reed_solomon_reconstruct.argtypes = [C.POINTER(RS), C.POINTER(C.c_void_p), C.c_void_p, C.c_int, C.c_int]
+        self.fec.fec_new.restype = C.c_void_p
+        self.fec.fec_new.argtypes = [C.c_int, C.c_int]
+        self.fec.fec_free.argtypes = [C.c_void_p]
+        self.fec.fec_encode.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.c_void_p, C.c_int, C.c_int]
+        self.fec.fec_decode.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.c_int]
+        self.rs.reed_solomon_init()
+
+    @staticmethod
+    def available():
+        d = os.path.join(HERE, "_ref")
+        return all(os.path.exists(os.path.join(d, f)) for f in ("libref_rs.so", "libref_fec.so"))
+
+    def shard_ptrs(self, data, parity):
+        """module/rs.c pointer layout: all data shards, then all parity shards."""
+        G, k, pitch = data.shape
+        m = parity.shape[1]
+        db, pb = data.ctypes.data, parity.ctypes.data
+        return (C.c_void_p * (G * (k + m)))(*([db + i * pitch for i in range(G * k)] +
+                                               [pb + i * pitch for i in range(G * m)]))
+
+    def rs_encode(self, h, ptrs, nshards, length):
+        return self.rs.reed_solomon_encode(h, ptrs, nshards, length)
+
+    def rs_reconstruct(self, h, ptrs, marks, nshards, length):
+        return self.rs.reed_solomon_reconstruct(h, ptrs, _p(marks), nshards, length)
