@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""bench.py -- RS(k,m) FEC encode+decode GiB/s, device-resident, on 1..8 MI355X.
+
+One step = the BASELINE.json configs[1] + configs[2] workload on one batch held in HBM:
+  encode      RS(10,3) of 1 000 000 x 1 KiB packets = 100 000 groups   (module/rs.c:574)
+  reconstruct the same 100 000 groups with 3 random erasures per group out of 13
+              (seed 0x5EED0003), rs.c survivor rule                     (module/rs.c:598)
+Cauchy matrix (bit-exact with module/rs.c).  Weak scaling: every rank owns its own
+100 000 groups (distinct seeds); value = all ranks' data bytes / the slowest rank's time.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Prints ONE JSON line (rank 0).  Data GiB/s counts payload bytes: k*B per encoded group and
+k*B per decoded group (groups with no erased data shard cost nothing, rs.c:620).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import quicknet_amd as qa  # noqa: E402
+from quicknet_amd.sharding import rank_seed  # noqa: E402
+from quicknet_amd.synth import SEED_DECODE, SEED_ENCODE, erasure_marks, marks_to_rs_layout  # noqa: E402
+
+METRIC = "RS(k,m) FEC encode+decode GiB/s (device-resident) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--m", type=int, default=3)
+    p.add_argument("--block", type=int, default=1024)
+    p.add_argument("--groups", type=int, default=100_000)
+    p.add_argument("--erasures", type=int, default=3)
+    p.add_argument("--flavour", choices=["cauchy", "vandermonde"], default="cauchy")
+    p.add_argument("--variant", type=int, default=0, help="0 perm tables (default), 1 LDS log/exp")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py), if present")
+    return p.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return rank, world, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def all_max(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_sum(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_baseline(args, budget_s):
+    """The reference's own rs.c (oracle/_ref, kind 'reference') -- or the CPU restatement
+    (oracle/liboracle.so, kind 'port') when _ref is absent -- on a bounded sample of the same
+    workload: encode + 3-erasure reconstruct of `sample` groups, 1 thread, repeated until the
+    budget is spent."""
+    from oracle.oracle import Oracle, RefCodec
+    k, m, B = args.k, args.m, args.block
+    sample = 10_000
+    from quicknet_amd.synth import synth_bytes
+    data = synth_bytes(SEED_ENCODE, sample * k * B).reshape(sample, k, B)
+    par = np.zeros((sample, m, B), np.uint8)
+    gm = erasure_marks(SEED_DECODE, sample, k + m, args.erasures)
+    marks = marks_to_rs_layout(gm, k)
+    dec_groups = int((gm[:, :k].sum(1) > 0).sum())
+    if RefCodec.available() and args.flavour == "cauchy":
+        ref = RefCodec()
+        kind = "reference"
+        h = ref.rs.reed_solomon_new(k, m)
+        work = data.copy()
+        ptrs = ref.shard_ptrs(work, par)
+        n = sample * (k + m)
+
+        def step():
+            ref.rs_encode(h, ptrs, n, B)
+            ref.rs_reconstruct(h, ptrs, marks, n, B)
+    else:
+        orc = Oracle()
+        kind = "port"
+        rows = orc.cauchy(k, m) if args.flavour == "cauchy" else orc.vandermonde(k, k + m)
+        work = data.copy()
+
+        def step():
+            orc.rs_encode(rows, work, par, B)
+            orc.rs_reconstruct(rows, work, par, marks, B)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        step()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    gib = reps * (sample + dec_groups) * k * B / GIB
+    return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{reps} x (encode {sample} groups + reconstruct {dec_groups} groups with {args.erasures} "
+                      f"random erasures/group), RS({k},{m}) B={B}, {el:.1f} s, 1 thread"}
+
+
+def load_traffic(path, workload_key):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    rank, world, local = dist_setup()
+    qa.set_kernel_variant(args.variant)
+    dev = torch.device("cuda", local)
+    k, m, B, G, E = args.k, args.m, args.block, args.groups, args.erasures
+    n = k + m
+    code = qa.Code.cauchy(k, m) if args.flavour == "cauchy" else qa.Code.vandermonde(k, m)
+    stream = torch.cuda.current_stream()
+
+    data = torch.empty((G, k, B), dtype=torch.uint8, device=dev)
+    qa.synth_fill(data, rank_seed(SEED_ENCODE, rank))
+    parity = torch.empty((G, m, B), dtype=torch.uint8, device=dev)
+    gm = erasure_marks(rank_seed(SEED_DECODE, rank), G, n, E)
+    marks = torch.from_numpy(marks_to_rs_layout(gm, k)).to(dev)
+    dec_groups = int((gm[:, :k].sum(1) > 0).sum())
+    erased_data = int(gm[:, :k].sum())
+    work = data.clone()  # the damaged copy reconstruct rewrites
+    work[torch.from_numpy(gm[:, :k].astype(bool)).to(dev)] = 0x5A
+    code.encode(data, parity)
+    code.prepare_reconstruct()
+    torch.cuda.synchronize()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        code.encode(data, parity)
+        if ev is not None:
+            ev[1].record(stream)
+        code.reconstruct(work, parity, marks)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # timed region: K steps between barrier + synchronize on both sides
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    el = all_max(t1 - t0, world)
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+
+    # correctness guard on the measured buffers: reconstruct restored the data exactly
+    ok = bool(torch.equal(work, data))
+    ok = all_sum(0.0 if ok else 1.0, world) == 0.0
+
+    data_bytes_rank = (G + dec_groups) * k * B * args.steps
+    total_bytes = all_sum(float(data_bytes_rank), world)
+    value = total_bytes / el / GIB
+
+    enc_alg = (k + m) * B * G                      # read k shards, write m
+    dec_alg = (k * dec_groups + erased_data) * B   # read k survivors, write e erased
+    enc_gbs = enc_alg / (enc_ms * 1e-3) / 1e9
+    dec_gbs = dec_alg / (dec_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.traffic, f"rs{k}_{m}_b{B}_g{G}")
+
+    def roof(kernel, ach, alg, ms, tkey):
+        tr = traffic.get(tkey) if isinstance(traffic, dict) else None
+        return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr, "kernel": kernel,
+                "algorithmic_bytes": alg, "avg_ms": round(ms, 4),
+                "read_frac": round((alg - (m * B * G if kernel == "encode" else erased_data * B)) / (ms * 1e-3) / 1e9
+                                   / HBM_PEAK_GBS, 4)}
+
+    r_enc = roof("encode", enc_gbs, enc_alg, enc_ms, "encode_bytes_per_launch")
+    r_dec = roof("reconstruct", dec_gbs, dec_alg, dec_ms, "reconstruct_bytes_per_launch")
+    dominant, other = (r_enc, r_dec) if enc_ms >= dec_ms else (r_dec, r_enc)
+
+    # calibration probe: the encode's traffic with XOR only (not a codec)
+    probe_ms = None
+    if rank == 0:
+        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        scratch = torch.empty_like(parity)
+        for _ in range(3):
+            qa.probe_stream(data, scratch, B)
+        pe0.record(stream)
+        for _ in range(10):
+            qa.probe_stream(data, scratch, B)
+        pe1.record(stream)
+        torch.cuda.synchronize()
+        probe_ms = pe0.elapsed_time(pe1) / 10
+        del scratch
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            cpu = cpu_baseline(args, args.cpu_seconds)
+        except Exception as exc:  # report, never fake
+            cpu = {"value": None, "error": repr(exc)}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes, device-generated), seeds 0x5EED0002/0x5EED0003 per rank",
+            "config": {
+                "workload": f"RS({k},{m}) encode of {G * k:,} x {B} B packets ({G:,} groups) + reconstruct with "
+                            f"{E} random erasures/group, per GPU (BASELINE configs[1]+[2])",
+                "k": k, "m": m, "block_size": B, "groups_per_gpu": G, "erasures_per_group": E,
+                "flavour": "cauchy (module/rs.c)" if args.flavour == "cauchy" else "vandermonde (module/fec.c)",
+                "kernel_variant": ["perm", "ldslog"][args.variant],
+                "parallelism": f"groups sharded, {world} rank(s), no collective on the data path",
+            },
+            "encode_gibs": round(G * k * B / (enc_ms * 1e-3) / GIB, 2),
+            "decode_gibs": round(dec_groups * k * B / (dec_ms * 1e-3) / GIB, 2),
+            "roofline": dominant,
+            "roofline_other": other,
+            "probe_stream_gbs": round(enc_alg / (probe_ms * 1e-3) / 1e9, 1) if probe_ms else None,
+            "verified": ok,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,111 @@
+/*
+ * qfec.h -- batched, device-resident GF(2^8) Reed-Solomon API of libqfec.so (MI355X).
+ *
+ * This is the GPU boundary the reference does not have: the reference codecs work one
+ * group (module/rs.c:574-643) or one packet (system/fec.c:714-862) at a time on the CPU.
+ * Here many independent (k+m)-shard groups are encoded or reconstructed by one kernel
+ * launch over device buffers, on the caller's HIP stream, with no host synchronisation.
+ * The per-packet / per-call C ABIs (qfec_fec.h, qfec_rs.h) are built on top of it.
+ *
+ * Device layout (one contiguous region per role; `pitch` bytes between shard starts):
+ *   data   [groups][k][pitch]   shard bytes [0, block_size) of each row are the payload
+ *   parity [groups][m][pitch]
+ *   marks  [groups*k data marks][groups*m parity marks]  (module/rs.c:609-612 layout;
+ *          non-zero = erased)
+ * With pitch == block_size, data followed by parity is exactly module/rs.c's shard order.
+ * Bytes in [block_size, round_up(block_size, 16)) of a row may be read and written when
+ * pitch allows (fast path); they are scratch.
+ *
+ * Arithmetic is bit-exact with module/rs.c (QFEC_CAUCHY) and module/fec.c / system/fec.c
+ * (QFEC_VANDERMONDE), including rs.c's column-0 zero-coefficient behaviour when a code is
+ * built with rs_stale_quirk = 1 (the default for QFEC_CAUCHY).
+ *
+ * All functions are thread-safe.  The device context of the calling thread's current HIP
+ * device is created lazily, once.  `stream` is a hipStream_t passed as void* (NULL = the
+ * null stream).  Return values: 0 or a negative QFEC_E* code.
+ */
+#ifndef QFEC_H
+#define QFEC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QFEC_CAUCHY 0      /* module/rs.c:437-440 parity rows (reed_solomon_new)   */
+#define QFEC_VANDERMONDE 1 /* module/fec.c:653-707 parity rows (fec_new)          */
+
+#define QFEC_OK 0
+#define QFEC_EINVAL (-1)   /* bad argument / shape                                   */
+#define QFEC_ENODEV (-2)   /* no HIP device                                          */
+#define QFEC_EHIP (-3)     /* a HIP runtime call failed                              */
+#define QFEC_ENOMEM (-4)   /* allocation failed                                      */
+#define QFEC_EUNSUP (-5)   /* shape not supported by this entry point                */
+
+#define QFEC_VARIANT_PERM 0    /* register byte-permute GF tables (v_perm_b32), default */
+#define QFEC_VARIANT_LDSLOG 1  /* log/exp tables staged in LDS                          */
+
+typedef struct qfec_code qfec_code;
+
+/* A code over k data and m parity shards with the given parity-row flavour.
+ * QFEC_CAUCHY: 1 <= k, 1 <= m, k + m <= 255 (rs.c:404).  QFEC_VANDERMONDE: 1 <= k,
+ * 0 <= m, k + m <= 256 (fec.c:664).  NULL on error. */
+qfec_code *qfec_code_new(int flavour, int k, int m);
+/* A code over explicit m x k parity rows (row-major). */
+qfec_code *qfec_code_from_rows(int k, int m, const unsigned char *parity_rows, int rs_stale_quirk);
+void qfec_code_free(qfec_code *code);
+int qfec_code_rows(const qfec_code *code, unsigned char *out_rows /* m*k */);
+int qfec_code_shape(const qfec_code *code, int *k, int *m);
+
+/* parity[g] = P x data[g] for every group g.  block_size >= 1, pitch >= block_size. */
+int qfec_encode(qfec_code *code, const unsigned char *d_data, unsigned char *d_parity,
+                long long groups, int block_size, long long pitch, void *stream);
+
+/* Rewrite every erased data shard from k survivors: the surviving data shards in
+ * ascending order, then the first e surviving parity shards in ascending order
+ * (module/rs.c:620-629; the same set network/NetFecCodec.cpp:504-528 hands to
+ * fec_decode).  Groups with no erased data are untouched; groups with more erased data
+ * than surviving parity are untouched and counted into *d_failed (device counter,
+ * may be NULL; accumulated, not reset).  Requires k + m <= 24. */
+int qfec_reconstruct(qfec_code *code, unsigned char *d_data, const unsigned char *d_parity,
+                     const unsigned char *d_marks, long long groups, int block_size,
+                     long long pitch, unsigned int *d_failed, void *stream);
+
+/* Build the per-erasure-pattern decode tables of `code` on the current device now
+ * (otherwise done on the first qfec_reconstruct). */
+int qfec_prepare_reconstruct(qfec_code *code);
+
+/* Host-side decode-matrix query for one group (group-order marks[n]).  Writes e <= m
+ * rows of k coefficients over the survivors listed in survivors[k] (shard ids 0..n-1).
+ * Returns e, 0 when nothing is erased, or -1 when under-determined.  CPU only. */
+int qfec_decode_rows(const qfec_code *code, const unsigned char *marks_n,
+                     unsigned char *rows_out, int *survivors_out, int *erased_out);
+
+/* The qfec_code behind a handle of the per-call ABIs, so a caller holding fec_new() /
+ * reed_solomon_new() handles (e.g. network/FecCodec.cpp's codec list) can batch groups
+ * through qfec_encode / qfec_reconstruct with the very same matrix. */
+struct _reed_solomon;
+qfec_code *qfec_fec_code(void *fec_handle);
+qfec_code *qfec_rs_code(struct _reed_solomon *rs);
+/* The n x k systematic matrix of a fec_new() handle (identity on top). */
+int qfec_fec_matrix(void *fec_handle, unsigned char *out_full);
+
+/* Fill nbytes of device memory with the synthetic stream of quicknet_amd/synth.py. */
+int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long seed, void *stream);
+
+/* Calibration probe, NOT a codec: streams the encode's traffic (k rows in, m rows out,
+ * XOR only).  Its time is the memory-side ceiling the GF kernels are compared with. */
+int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long long groups, int k, int m,
+                      int block_size, long long pitch, void *stream);
+
+int qfec_set_kernel_variant(int variant);
+int qfec_get_kernel_variant(void);
+int qfec_device_count(void);
+const char *qfec_strerror(int err);
+const char *qfec_last_error(void);
+const char *qfec_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QFEC_H */

@@ -1,0 +1,41 @@
+/*
+ * qfec_fec.h -- drop-in for the reference's per-packet systematic-Vandermonde codec.
+ *
+ * Replaces system/fec.h:233-246 (== module/fec.h) of skywind3000/QuickNet, the codec the
+ * network stack links (network/FecCodec.cpp:5,84,133; network/FecCodecBuf.cpp:13,151,204),
+ * with the same C ABI, exported by libqfec.so.  The GF(2^8) multiply-accumulate runs in
+ * HIP kernels on an MI355X; packet buffers may be host or device memory.
+ *
+ * Semantics kept bit-exact with system/fec.c:
+ *   - fec_new(k, n): parity rows = V_bottom * V_top^-1 of the Vandermonde matrix on the
+ *     points 0, 1, a, a^2 ...; NULL (and a message on stderr) for k > 256, n > 256 or
+ *     k > n                                                         (fec.c:653-707)
+ *   - fec_encode(): index < k copies src[index]; k <= index < n writes one parity packet
+ *     of sz bytes; any other index writes nothing                     (fec.c:714-733)
+ *   - fec_decode(): shuffles data packets into their own slots, permuting pkt[] and
+ *     index[] in place; recovered data i lands in slot i (a slot that held a parity
+ *     packet, whose index value is kept); returns 1 on a shuffle conflict, an index >= n
+ *     or a singular matrix, else 0                                    (fec.c:738-862)
+ *   - a negative index (undefined behaviour in the reference) is rejected with 1.
+ */
+#ifndef QFEC_FEC_H
+#define QFEC_FEC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* fec.h:237 */
+void *fec_new(int k, int n);
+/* fec.h:238 */
+void fec_free(void *p);
+/* fec.h:240 -- u_char in the reference; same ABI */
+void fec_encode(void *code, unsigned char **src, unsigned char *dst, int index, int sz);
+/* fec.h:241 */
+int fec_decode(void *code, unsigned char **pkt, int *index, int sz);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QFEC_FEC_H */

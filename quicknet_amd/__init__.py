@@ -1,0 +1,11 @@
+"""quicknet_amd -- MI355X-native Reed-Solomon FEC path for QuickNet-style packet-loss recovery.
+
+The product is ``libqfec.so`` (quicknet_amd/csrc: HIP kernels for gfx950 + the C ABIs of
+the reference's system/fec.h and module/rs.h + a batched device API, include/qfec*.h).
+This package is the thin Python face used by the tests and bench.py.
+"""
+from ._lib import LIB_PATH, QfecError, lib  # noqa: F401
+from .codec import (QFEC_CAUCHY, QFEC_VANDERMONDE, Code, FecParms, ReedSolomon,  # noqa: F401
+                    device_count, probe_stream, set_kernel_variant, synth_fill)
+
+__version__ = "0.1.0"

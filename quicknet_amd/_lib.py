@@ -1,0 +1,95 @@
+"""ctypes binding of libqfec.so (the HIP kernels + C ABI built from quicknet_amd/csrc).
+
+The library is loaded from the package directory (built in-tree by
+``__graft_entry__.build()`` / ``make -C quicknet_amd/csrc``).  There is no fallback: if
+the library is missing, importing the codec raises.
+"""
+import ctypes as C
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libqfec.so")
+
+# every symbol the headers in include/ declare (checked by tests/test_abi.py)
+EXPORTS = {
+    "qfec_fec.h": ["fec_new", "fec_free", "fec_encode", "fec_decode"],
+    "qfec_rs.h": ["reed_solomon_init", "reed_solomon_new", "reed_solomon_release", "reed_solomon_encode",
+                  "reed_solomon_reconstruct", "reed_solomon_error"],
+    "qfec.h": ["qfec_code_new", "qfec_code_from_rows", "qfec_code_free", "qfec_code_rows", "qfec_code_shape",
+               "qfec_encode", "qfec_reconstruct", "qfec_prepare_reconstruct", "qfec_decode_rows",
+               "qfec_fec_code", "qfec_rs_code", "qfec_fec_matrix", "qfec_synth_fill", "qfec_probe_stream",
+               "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
+               "qfec_last_error", "qfec_version"],
+}
+
+QFEC_CAUCHY = 0
+QFEC_VANDERMONDE = 1
+QFEC_VARIANT_PERM = 0
+QFEC_VARIANT_LDSLOG = 1
+
+_lib = None
+
+
+class RSStruct(C.Structure):  # include/qfec_rs.h (== module/rs.h:7-13)
+    _fields_ = [("data_shards", C.c_int), ("parity_shards", C.c_int), ("shards", C.c_int),
+                ("m", C.POINTER(C.c_ubyte)), ("parity", C.POINTER(C.c_ubyte))]
+
+
+def lib():
+    """The loaded library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "or `make -C quicknet_amd/csrc` (there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    vp, i, ll, u64 = C.c_void_p, C.c_int, C.c_longlong, C.c_ulonglong
+    sig = {
+        "qfec_code_new": (vp, [i, i, i]),
+        "qfec_code_from_rows": (vp, [i, i, vp, i]),
+        "qfec_code_free": (None, [vp]),
+        "qfec_code_rows": (i, [vp, vp]),
+        "qfec_code_shape": (i, [vp, C.POINTER(i), C.POINTER(i)]),
+        "qfec_encode": (i, [vp, vp, vp, ll, i, ll, vp]),
+        "qfec_reconstruct": (i, [vp, vp, vp, vp, ll, i, ll, vp, vp]),
+        "qfec_prepare_reconstruct": (i, [vp]),
+        "qfec_decode_rows": (i, [vp, vp, vp, vp, vp]),
+        "qfec_fec_code": (vp, [vp]),
+        "qfec_rs_code": (vp, [vp]),
+        "qfec_fec_matrix": (i, [vp, vp]),
+        "qfec_synth_fill": (i, [vp, ll, u64, vp]),
+        "qfec_probe_stream": (i, [vp, vp, ll, i, i, i, ll, vp]),
+        "qfec_set_kernel_variant": (i, [i]),
+        "qfec_get_kernel_variant": (i, []),
+        "qfec_device_count": (i, []),
+        "qfec_strerror": (C.c_char_p, [i]),
+        "qfec_last_error": (C.c_char_p, []),
+        "qfec_version": (C.c_char_p, []),
+        "fec_new": (vp, [i, i]),
+        "fec_free": (None, [vp]),
+        "fec_encode": (None, [vp, C.POINTER(vp), vp, i, i]),
+        "fec_decode": (i, [vp, C.POINTER(vp), C.POINTER(i), i]),
+        "reed_solomon_init": (None, []),
+        "reed_solomon_new": (C.POINTER(RSStruct), [i, i]),
+        "reed_solomon_release": (None, [C.POINTER(RSStruct)]),
+        "reed_solomon_encode": (i, [C.POINTER(RSStruct), C.POINTER(vp), i, i]),
+        "reed_solomon_reconstruct": (i, [C.POINTER(RSStruct), C.POINTER(vp), vp, i, i]),
+        "reed_solomon_error": (i, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+class QfecError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != 0:
+        L = lib()
+        raise QfecError(f"{what}: {L.qfec_strerror(rc).decode()} ({rc}): {L.qfec_last_error().decode()}")
+    return rc

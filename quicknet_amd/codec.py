@@ -1,0 +1,237 @@
+"""Python face of libqfec: the batched device codec and the reference's per-call ABIs.
+
+* ``Code``          -- a (k, m) code on the MI355X; ``encode`` / ``reconstruct`` run whole
+                       batches of groups on device tensors (torch, uint8) on the current
+                       HIP stream.  Mirrors module/rs.c's batched API (rs.h:22-49) over the
+                       contiguous layout of include/qfec.h.
+* ``FecParms``      -- system/fec.h's per-packet codec (fec_new / fec_encode / fec_decode),
+                       the interface network/FecCodec.cpp and network/FecCodecBuf.cpp bind.
+* ``ReedSolomon``   -- module/rs.h's per-call codec over shard pointer arrays.
+
+All arithmetic runs in the HIP kernels of libqfec.so; these classes only marshal.
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
+
+__all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
+           "set_kernel_variant", "synth_fill", "probe_stream", "device_count"]
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return C.c_void_p(stream)
+    return C.c_void_p(stream.cuda_stream)
+
+
+def _dev_ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise QfecError("expected a device tensor")
+    if not t.is_contiguous():
+        raise QfecError("expected a contiguous tensor")
+    return C.c_void_p(t.data_ptr())
+
+
+def device_count():
+    return lib().qfec_device_count()
+
+
+def set_kernel_variant(v):
+    check(lib().qfec_set_kernel_variant(v), "qfec_set_kernel_variant")
+
+
+def synth_fill(t, seed, stream=None):
+    """Fill a device uint8 tensor with quicknet_amd.synth.synth_bytes(seed, t.numel())."""
+    check(lib().qfec_synth_fill(_dev_ptr(t), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(stream)),
+          "qfec_synth_fill")
+
+
+def probe_stream(data, parity, block_size, stream=None):
+    """Calibration only: the encode's traffic with XOR in place of GF arithmetic."""
+    G, k, pitch = data.shape
+    m = parity.shape[1]
+    check(lib().qfec_probe_stream(_dev_ptr(data), _dev_ptr(parity), G, k, m, block_size, pitch,
+                                  _stream_handle(stream)), "qfec_probe_stream")
+
+
+class Code:
+    """A GF(2^8) RS code with k data and m parity shards per group."""
+
+    def __init__(self, handle, owner=True):
+        if not handle:
+            raise QfecError(f"invalid code: {lib().qfec_last_error().decode()}")
+        self._h = C.c_void_p(handle)
+        self._owner = owner
+        k, m = C.c_int(), C.c_int()
+        check(lib().qfec_code_shape(self._h, C.byref(k), C.byref(m)), "qfec_code_shape")
+        self.k, self.m = k.value, m.value
+
+    @classmethod
+    def cauchy(cls, k, m):
+        """module/rs.c's matrix (reed_solomon_new, rs.c:437-440)."""
+        return cls(lib().qfec_code_new(QFEC_CAUCHY, k, m))
+
+    @classmethod
+    def vandermonde(cls, k, m):
+        """module/fec.c's matrix (fec_new(k, k + m), fec.c:653-707)."""
+        return cls(lib().qfec_code_new(QFEC_VANDERMONDE, k, m))
+
+    @classmethod
+    def from_rows(cls, rows, rs_stale_quirk=False):
+        rows = np.ascontiguousarray(rows, dtype=np.uint8)
+        m, k = rows.shape
+        return cls(lib().qfec_code_from_rows(k, m, rows.ctypes.data, int(rs_stale_quirk)))
+
+    def close(self):
+        if self._h and self._owner:
+            lib().qfec_code_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def rows(self):
+        out = np.zeros((self.m, self.k), dtype=np.uint8)
+        check(lib().qfec_code_rows(self._h, out.ctypes.data), "qfec_code_rows")
+        return out
+
+    def encode(self, data, parity, block_size=None, stream=None):
+        """parity[g] = P x data[g]; data uint8 [G, k, pitch], parity uint8 [G, m, pitch] on device."""
+        G, k, pitch = data.shape
+        if k != self.k or parity.shape[0] != G or parity.shape[1] != self.m or parity.shape[2] != pitch:
+            raise QfecError(f"shape mismatch: data {tuple(data.shape)} parity {tuple(parity.shape)} for ({self.k},{self.m})")
+        block_size = pitch if block_size is None else block_size
+        check(lib().qfec_encode(self._h, _dev_ptr(data), _dev_ptr(parity), G, block_size, pitch,
+                                _stream_handle(stream)), "qfec_encode")
+
+    def prepare_reconstruct(self):
+        check(lib().qfec_prepare_reconstruct(self._h), "qfec_prepare_reconstruct")
+
+    def reconstruct(self, data, parity, marks, block_size=None, failed=None, stream=None):
+        """Rewrite erased data shards in place.  marks: uint8 [G*k + G*m] (rs.c layout) on device;
+        failed: optional device int32/uint32 [1] counter of under-determined groups."""
+        G, k, pitch = data.shape
+        if k != self.k or parity.shape[0] != G or parity.shape[1] != self.m or marks.numel() != G * (self.k + self.m):
+            raise QfecError("shape mismatch")
+        block_size = pitch if block_size is None else block_size
+        check(lib().qfec_reconstruct(self._h, _dev_ptr(data), _dev_ptr(parity), _dev_ptr(marks), G, block_size,
+                                     pitch, _dev_ptr(failed), _stream_handle(stream)), "qfec_reconstruct")
+
+    def decode_rows(self, marks_n):
+        """Host-side decode matrix for one group-order mark vector: (e, rows[e,k], survivors[k], erased[e])."""
+        marks_n = np.ascontiguousarray(marks_n, dtype=np.uint8)
+        rows = np.zeros((self.m, self.k), dtype=np.uint8)
+        surv = np.zeros(self.k, dtype=np.int32)
+        lost = np.zeros(max(self.m, 1), dtype=np.int32)
+        e = lib().qfec_decode_rows(self._h, marks_n.ctypes.data, rows.ctypes.data, surv.ctypes.data, lost.ctypes.data)
+        if e <= 0:
+            return e, None, None, None
+        return e, rows[:e].copy(), surv, lost[:e].copy()
+
+
+class FecParms:
+    """system/fec.h: fec_new(k, n) / fec_encode / fec_decode / fec_free over packet buffers."""
+
+    def __init__(self, k, n):
+        self.k, self.n = k, n
+        self._h = lib().fec_new(k, n)
+        if not self._h:
+            raise QfecError(f"fec_new({k}, {n}) failed")
+        self._h = C.c_void_p(self._h)
+
+    def close(self):
+        if self._h:
+            lib().fec_free(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def matrix(self):
+        out = np.zeros((self.n, self.k), dtype=np.uint8)
+        check(lib().qfec_fec_matrix(self._h, out.ctypes.data), "qfec_fec_matrix")
+        return out
+
+    def code(self):
+        """The batched Code sharing this handle's matrix (not owned)."""
+        return Code(lib().qfec_fec_code(self._h), owner=False)
+
+    def encode(self, src, dst, index, sz):
+        """src: k host uint8 arrays (or one [k, >=sz] array); dst: uint8 array written in place."""
+        rows = [np.ascontiguousarray(s) for s in src]
+        ptrs = (C.c_void_p * len(rows))(*[r.ctypes.data for r in rows])
+        lib().fec_encode(self._h, ptrs, C.c_void_p(dst.ctypes.data), index, sz)
+
+    def decode(self, pkts, index, sz):
+        """pkts: [k, >=sz] uint8 array (slots), index: k ints.  Returns (rc, pkts_after, index_after)
+        with the reference's in-place pointer/index permutation applied to copies."""
+        buf = np.ascontiguousarray(pkts, dtype=np.uint8).copy()
+        k, stride = buf.shape
+        base = buf.ctypes.data
+        ptrs = (C.c_void_p * k)(*[base + s * stride for s in range(k)])
+        ia = (C.c_int * k)(*[int(x) for x in index])
+        rc = lib().fec_decode(self._h, ptrs, ia, sz)
+        after = np.stack([buf[(ptrs[s] - base) // stride] for s in range(k)])
+        return rc, after, np.array(list(ia), dtype=np.int32)
+
+
+class ReedSolomon:
+    """module/rs.h: reed_solomon_new / encode / reconstruct / release over shard pointers."""
+
+    def __init__(self, k, m):
+        L = lib()
+        L.reed_solomon_init()
+        self._h = L.reed_solomon_new(k, m)
+        if not self._h:
+            raise QfecError(f"reed_solomon_new({k}, {m}) failed: errno {L.reed_solomon_error()}")
+        self.k, self.m = k, m
+
+    def close(self):
+        if self._h:
+            lib().reed_solomon_release(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def parity(self):
+        """The public parity matrix (editable, as in rs.h:12)."""
+        return np.ctypeslib.as_array(self._h.contents.parity, shape=(self.m, self.k))
+
+    @staticmethod
+    def _ptrs(data, parity):
+        G, k, pitch = data.shape
+        m = parity.shape[1]
+        db, pb = data.ctypes.data, parity.ctypes.data
+        return (C.c_void_p * (G * (k + m)))(*([db + i * pitch for i in range(G * k)] +
+                                               [pb + i * pitch for i in range(G * m)]))
+
+    def encode(self, data, parity, block_size):
+        """data [G,k,pitch], parity [G,m,pitch] host uint8 arrays (parity written)."""
+        G = data.shape[0]
+        return lib().reed_solomon_encode(self._h, self._ptrs(data, parity), G * (self.k + self.m), block_size)
+
+    def reconstruct(self, data, parity, marks, block_size):
+        G = data.shape[0]
+        marks = np.ascontiguousarray(marks, dtype=np.uint8)
+        return lib().reed_solomon_reconstruct(self._h, self._ptrs(data, parity), C.c_void_p(marks.ctypes.data),
+                                              G * (self.k + self.m), block_size)

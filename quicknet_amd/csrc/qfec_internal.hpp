@@ -1,0 +1,103 @@
+// qfec_internal.hpp -- shared declarations of libqfec (host runtime <-> kernels).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace qfec {
+
+// dwords per coefficient in a perm table:
+//   [0..4] v_perm_b32 tables (c*{0..7}, c*{0..7}<<3, c*{0..3}<<6, packed 4 bytes/dword)
+//   [5]    row flag on column 0: 1 = row starts from the output's previous bytes
+//   [6]    log(c) (0xFF for c == 0), for the LDS log/exp variant
+//   [7]    c itself
+constexpr int QFEC_TAB_STRIDE = 8;
+
+constexpr int QFEC_REC_NONE = -1;  // LUT: nothing erased in this group
+constexpr int QFEC_REC_FAIL = -2;  // LUT: more erased data than surviving parity
+constexpr int QFEC_LUT_MAX_N = 24; // n <= 24 -> 2^n-entry pattern LUT on the device
+
+constexpr int QFEC_VARIANT_PERM_I = 0;
+constexpr int QFEC_VARIANT_LDSLOG_I = 1;
+
+// n / d for n < 2^32 via a 33-bit magic (Granlund-Montgomery, round-up form)
+struct DivMagic {
+    uint64_t mul;
+    uint32_t shift;
+    uint32_t pow2;
+};
+
+DivMagic make_div_magic(uint32_t d);
+
+struct EncodeArgs {
+    const uint8_t* data;    // [groups][k][pitch]
+    uint8_t* parity;        // [groups][m][pitch]
+    const uint32_t* tab;    // [m][k][QFEC_TAB_STRIDE]
+    const uint8_t* gf_exp;  // LDS variant: exp[512]
+    const uint8_t* gf_log;  // LDS variant: log[256]
+    uint64_t work;          // groups * cols lanes (< 2^32)
+    uint64_t pitch;
+    DivMagic cols_div;
+    uint32_t cols;          // columns per row: 16-B columns (vec16) or bytes
+    int k, m;
+    int vec16;
+};
+
+struct ReconArgs {
+    uint8_t* data;            // [groups][k][pitch]
+    const uint8_t* parity;    // [groups][m][pitch]
+    const uint8_t* marks;     // rs.c layout, or NULL when group_rec is given
+    const int32_t* lut;       // [2^n] pattern -> record offset (dwords) / QFEC_REC_*
+    const int32_t* group_rec; // explicit mode: per-group record offset / QFEC_REC_*
+    const uint32_t* records;
+    unsigned int* failed;
+    uint64_t groups;
+    uint64_t pitch;
+    uint32_t cols;            // 16-B columns (vec16) or bytes per row
+    int k, m;
+    int surv_off, lost_off, hdr;
+    int vec16;
+};
+
+hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream);
+hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream);
+hipError_t launch_synth_fill(uint8_t* p, uint64_t nbytes, uint64_t seed, hipStream_t stream);
+hipError_t launch_probe_xor(const EncodeArgs& a, hipStream_t stream);
+
+// ---------------------------------------------------------------- host GF(2^8) (gf256.cpp)
+struct Field {
+    uint8_t exp[512];  // exp[i] = 2^i, doubled (exp[i + 255] = exp[i]) + 2 pad
+    uint8_t log[256];  // log[0] = 255 sentinel
+    uint8_t inv[256];  // inv[0] = 0
+    uint8_t mul[256][256];
+};
+
+const Field& field();
+
+// parity rows (m x k, row-major) of the two reference matrix flavours
+bool cauchy_rows(int k, int m, std::vector<uint8_t>& out);       // module/rs.c:437-440
+bool vandermonde_rows(int k, int m, std::vector<uint8_t>& out);  // module/fec.c:653-707
+
+// in-place GF inverse of a k x k matrix; false if singular
+bool gf_invert(uint8_t* a, int k);
+
+// one coefficient's 8-dword perm table
+void perm_entry(uint8_t c, uint32_t* out8);
+
+// decode record of one erasure pattern (see qfec_kernels.hip, "reconstruct").
+// group-order marks over n = k + m shards.  Returns e (>= 1), 0 if nothing is erased
+// or -1 if under-determined; on e >= 1 fills rows (e x k), survivors (k), lost (e).
+int decode_rows(const uint8_t* parity_rows, int k, int m, const uint8_t* marks_n,
+                std::vector<uint8_t>& rows, std::vector<int>& survivors, std::vector<int>& lost);
+
+struct RecordLayout {
+    int surv_off, lost_off, hdr;
+    size_t words(int e, int k) const { return (size_t)hdr + (size_t)e * k * QFEC_TAB_STRIDE; }
+};
+RecordLayout record_layout(int k, int m);
+void build_record(const RecordLayout& L, int k, int e, const uint8_t* rows, const int* survivors,
+                  const int* lost, bool rs_quirk, uint32_t* out);
+
+}  // namespace qfec

@@ -1,0 +1,1019 @@
+// qfec_runtime.cpp -- host runtime and C ABI of libqfec.so.
+//
+// Exports three ABIs (declared in include/):
+//   qfec_fec.h  fec_new / fec_free / fec_encode / fec_decode      (system/fec.h:237-241)
+//   qfec_rs.h   reed_solomon_init / new / release / encode /
+//               reconstruct / error                                (module/rs.h:22-49)
+//   qfec.h      the batched device API (qfec_*) both of the above are built on.
+//
+// Every GF multiply-accumulate runs in the HIP kernels of qfec_kernels.hip.  The host
+// does what the reference's host code does outside its byte loops: build the parity
+// matrices, shuffle packets, pick survivors, invert k x k matrices (cached per erasure
+// pattern), and move bytes between the caller's buffers and the device.  There is no CPU
+// arithmetic fallback: without a usable HIP device every entry point fails loudly.
+//
+// Threading: all entry points are thread-safe.  A device context (internal stream, pinned
+// and device staging buffers) is created lazily and exactly once per device; codes keep
+// their device tables per device.  No HIP state is visible to callers.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/qfec.h"
+#include "../../include/qfec_fec.h"
+#include "../../include/qfec_rs.h"
+#include "qfec_internal.hpp"
+
+#define QFEC_VERSION_STRING "qfec 0.1.0 (gfx950)"
+
+using namespace qfec;
+
+// ====================================================================== errors
+namespace {
+
+thread_local std::string t_last_error;
+
+void set_error(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    t_last_error = buf;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return QFEC_EHIP;
+}
+
+#define HIP_TRY(expr)                                       \
+    do {                                                    \
+        hipError_t _e = (expr);                             \
+        if (_e != hipSuccess) return hip_fail(_e, #expr);   \
+    } while (0)
+
+std::atomic<int> g_variant{QFEC_VARIANT_PERM};
+
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ====================================================================== device contexts
+constexpr int kMaxDevices = 64;
+
+struct DevCtx {
+    int device = 0;
+    std::mutex mu;  // serialises use of the staging buffers and the internal stream
+    hipStream_t stream = nullptr;
+    uint8_t* d_stage = nullptr;
+    size_t d_cap = 0;
+    uint8_t* h_stage = nullptr;  // pinned
+    size_t h_cap = 0;
+    uint8_t* d_gf = nullptr;     // exp[512] | log[256] for the LDS variant
+    uint32_t* d_small = nullptr; // per-call tables (fec_encode row, fec_decode matrix)
+    size_t small_cap = 0;
+    uint32_t* h_small = nullptr; // pinned mirror
+    unsigned* d_counter = nullptr;
+    int init_rc = QFEC_ENODEV;
+};
+
+DevCtx g_ctx[kMaxDevices];
+std::once_flag g_ctx_once[kMaxDevices];
+
+int init_ctx(DevCtx& c, int dev) {
+    c.device = dev;
+    HIP_TRY(hipSetDevice(dev));
+    HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    const Field& f = field();
+    HIP_TRY(hipMalloc(&c.d_gf, 768));
+    HIP_TRY(hipMemcpy(c.d_gf, f.exp, 512, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c.d_gf + 512, f.log, 256, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&c.d_counter, 256));
+    return QFEC_OK;
+}
+
+// context of the calling thread's current device (created on first use)
+int current_ctx(DevCtx** out) {
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) {
+        set_error("no HIP device available (%s)", e == hipSuccess ? "0 devices" : hipGetErrorString(e));
+        return QFEC_ENODEV;
+    }
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDevices) {
+        set_error("device %d out of range", dev);
+        return QFEC_ENODEV;
+    }
+    DevCtx& c = g_ctx[dev];
+    std::call_once(g_ctx_once[dev], [&] {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        c.init_rc = init_ctx(c, dev);
+        (void)hipSetDevice(prev);
+    });
+    if (c.init_rc != QFEC_OK) {
+        if (t_last_error.empty()) set_error("device %d context initialisation failed", dev);
+        return c.init_rc;
+    }
+    *out = &c;
+    return QFEC_OK;
+}
+
+int ensure_stage(DevCtx& c, size_t dbytes, size_t hbytes) {
+    if (dbytes > c.d_cap) {
+        if (c.d_stage) HIP_TRY(hipFree(c.d_stage));
+        c.d_stage = nullptr;
+        c.d_cap = 0;
+        const size_t cap = round_up(std::max(dbytes, (size_t)1 << 20), 1 << 20);
+        HIP_TRY(hipMalloc(&c.d_stage, cap));
+        c.d_cap = cap;
+    }
+    if (hbytes > c.h_cap) {
+        if (c.h_stage) HIP_TRY(hipHostFree(c.h_stage));
+        c.h_stage = nullptr;
+        c.h_cap = 0;
+        const size_t cap = round_up(std::max(hbytes, (size_t)1 << 20), 1 << 20);
+        HIP_TRY(hipHostMalloc(&c.h_stage, cap, hipHostMallocDefault));
+        c.h_cap = cap;
+    }
+    return QFEC_OK;
+}
+
+int ensure_small(DevCtx& c, size_t words) {
+    if (words <= c.small_cap) return QFEC_OK;
+    if (c.d_small) HIP_TRY(hipFree(c.d_small));
+    if (c.h_small) HIP_TRY(hipHostFree(c.h_small));
+    c.d_small = nullptr;
+    c.h_small = nullptr;
+    c.small_cap = 0;
+    const size_t cap = round_up(words, 4096);
+    HIP_TRY(hipMalloc(&c.d_small, cap * 4));
+    HIP_TRY(hipHostMalloc(&c.h_small, cap * 4, hipHostMallocDefault));
+    c.small_cap = cap;
+    return QFEC_OK;
+}
+
+// true if p is device (or managed) memory visible to the current device
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // clear the sticky error of the probe
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+}  // namespace
+
+// ====================================================================== code objects
+struct DevTables {
+    uint32_t* d_enc = nullptr;  // [m][k][8]
+    uint64_t enc_version = ~0ull;
+    int32_t* d_lut = nullptr;    // [2^n]
+    uint32_t* d_rec = nullptr;   // decode records
+    uint64_t rec_version = ~0ull;
+};
+
+struct qfec_code {
+    int k = 0, m = 0;
+    int quirk = 0;  // module/rs.c column-0 zero-coefficient behaviour
+    std::mutex mu;
+    std::vector<uint8_t> rows;  // m x k
+    uint64_t version = 0;
+    std::map<int, DevTables> dev;
+    // host-side decode cache: pattern key -> (record words); for explicit mode
+    std::unordered_map<uint64_t, std::vector<uint32_t>> rec_cache;
+    uint64_t rec_cache_version = ~0ull;
+};
+
+namespace {
+
+qfec_code* make_code(int k, int m, std::vector<uint8_t>&& rows, int quirk) {
+    qfec_code* c = new (std::nothrow) qfec_code();
+    if (!c) return nullptr;
+    c->k = k;
+    c->m = m;
+    c->quirk = quirk;
+    c->rows = std::move(rows);
+    return c;
+}
+
+void free_code(qfec_code* c) {
+    if (!c) return;
+    int prev = 0;
+    bool have = hipGetDevice(&prev) == hipSuccess;
+    for (auto& kv : c->dev) {
+        if (hipSetDevice(kv.first) != hipSuccess) continue;
+        if (kv.second.d_enc) (void)hipFree(kv.second.d_enc);
+        if (kv.second.d_lut) (void)hipFree(kv.second.d_lut);
+        if (kv.second.d_rec) (void)hipFree(kv.second.d_rec);
+    }
+    if (have) (void)hipSetDevice(prev);
+    delete c;
+}
+
+void enc_table_host(const qfec_code* c, std::vector<uint32_t>& t) {
+    const int k = c->k, m = c->m;
+    t.assign((size_t)m * k * QFEC_TAB_STRIDE, 0);
+    for (int r = 0; r < m; ++r) {
+        for (int i = 0; i < k; ++i) perm_entry(c->rows[(size_t)r * k + i], &t[((size_t)r * k + i) * QFEC_TAB_STRIDE]);
+        if (c->quirk && c->rows[(size_t)r * k] == 0) t[((size_t)r * k) * QFEC_TAB_STRIDE + 5] = 1;
+    }
+}
+
+// encode tables of `c` on device `dev` (caller holds c->mu)
+int ensure_enc(qfec_code* c, int dev, uint32_t** out) {
+    DevTables& d = c->dev[dev];
+    if (d.enc_version != c->version || !d.d_enc) {
+        std::vector<uint32_t> t;
+        enc_table_host(c, t);
+        if (d.d_enc) HIP_TRY(hipFree(d.d_enc));
+        d.d_enc = nullptr;
+        HIP_TRY(hipMalloc(&d.d_enc, std::max<size_t>(t.size(), 8) * 4));
+        if (!t.empty()) HIP_TRY(hipMemcpy(d.d_enc, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+        d.enc_version = c->version;
+    }
+    *out = d.d_enc;
+    return QFEC_OK;
+}
+
+// key of the decode matrix a group-order erasure mask selects: erased data bits and
+// the chosen parity bits (first e non-erased, ascending -- module/rs.c:620-629).
+// Returns false when under-determined.  e == 0 -> key 0.
+bool pattern_key(uint64_t mask, int k, int m, uint64_t* key, int* e_out) {
+    const uint64_t dm = k >= 64 ? mask : (mask & ((1ull << k) - 1));
+    const int e = __builtin_popcountll(dm);
+    *e_out = e;
+    if (e == 0) { *key = 0; return true; }
+    uint64_t avail = ~(mask >> k) & (m >= 64 ? ~0ull : ((1ull << m) - 1));
+    uint64_t chosen = 0;
+    for (int i = 0; i < e; ++i) {
+        if (!avail) return false;
+        const uint64_t low = avail & (~avail + 1);
+        chosen |= low;
+        avail ^= low;
+    }
+    *key = dm | (chosen << k);
+    return true;
+}
+
+int record_for_key(const qfec_code* c, uint64_t key, std::vector<uint32_t>& rec) {
+    const int k = c->k, m = c->m, n = k + m;
+    std::vector<uint8_t> marks(n, 0);
+    for (int i = 0; i < k; ++i) marks[i] = (key >> i) & 1;
+    // parity not chosen is treated as erased so decode_rows picks exactly `chosen`
+    for (int j = 0; j < m; ++j) marks[k + j] = ((key >> (k + j)) & 1) ? 0 : 1;
+    std::vector<uint8_t> rows;
+    std::vector<int> surv, lost;
+    const int e = decode_rows(c->rows.data(), k, m, marks.data(), rows, surv, lost);
+    if (e <= 0) return -1;
+    const RecordLayout L = record_layout(k, m);
+    rec.assign(L.words(e, k), 0);
+    build_record(L, k, e, rows.data(), surv.data(), lost.data(), c->quirk != 0, rec.data());
+    return e;
+}
+
+// device LUT (2^n entries) + all decode records of `c` (caller holds c->mu)
+int ensure_lut(qfec_code* c, int dev, DevTables** out) {
+    DevTables& d = c->dev[dev];
+    *out = &d;
+    if (d.rec_version == c->version && d.d_lut) return QFEC_OK;
+    const int k = c->k, m = c->m, n = k + m;
+    if (n > QFEC_LUT_MAX_N) {
+        set_error("qfec_reconstruct: k + m = %d > %d (use reed_solomon_reconstruct)", n, QFEC_LUT_MAX_N);
+        return QFEC_EUNSUP;
+    }
+    const size_t nmask = (size_t)1 << n;
+    std::vector<int32_t> lut(nmask);
+    std::unordered_map<uint64_t, int32_t> off_of;
+    std::vector<uint32_t> recs, one;
+    for (size_t mask = 0; mask < nmask; ++mask) {
+        uint64_t key;
+        int e;
+        if (!pattern_key(mask, k, m, &key, &e)) { lut[mask] = QFEC_REC_FAIL; continue; }
+        if (e == 0) { lut[mask] = QFEC_REC_NONE; continue; }
+        auto it = off_of.find(key);
+        if (it != off_of.end()) { lut[mask] = it->second; continue; }
+        if (record_for_key(c, key, one) <= 0) { lut[mask] = QFEC_REC_FAIL; continue; }
+        const int32_t off = (int32_t)recs.size();
+        recs.insert(recs.end(), one.begin(), one.end());
+        off_of.emplace(key, off);
+        lut[mask] = off;
+    }
+    if (d.d_lut) HIP_TRY(hipFree(d.d_lut));
+    if (d.d_rec) HIP_TRY(hipFree(d.d_rec));
+    d.d_lut = nullptr;
+    d.d_rec = nullptr;
+    HIP_TRY(hipMalloc(&d.d_lut, nmask * 4));
+    HIP_TRY(hipMalloc(&d.d_rec, std::max<size_t>(recs.size(), 8) * 4));
+    HIP_TRY(hipMemcpy(d.d_lut, lut.data(), nmask * 4, hipMemcpyHostToDevice));
+    if (!recs.empty()) HIP_TRY(hipMemcpy(d.d_rec, recs.data(), recs.size() * 4, hipMemcpyHostToDevice));
+    d.rec_version = c->version;
+    return QFEC_OK;
+}
+
+bool vec16_ok(const void* a, const void* b, int block, long long pitch) {
+    return ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0) && (pitch % 16 == 0) &&
+           (long long)round_up((size_t)block, 16) <= pitch;
+}
+
+// launch encode over `groups` groups with tables `tab` covering `m` rows
+int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, const uint8_t* d_data,
+               uint8_t* d_par, long long groups, int block, long long pitch, hipStream_t s) {
+    EncodeArgs a{};
+    a.tab = tab;
+    a.gf_exp = ctx.d_gf;
+    a.gf_log = ctx.d_gf + 512;
+    a.k = c->k;
+    a.m = m;
+    a.pitch = (uint64_t)pitch;
+    a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
+    a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
+    a.cols_div = make_div_magic(a.cols);
+    const long long per = std::max<long long>(1, (long long)(0x7FFFFFFFll / a.cols));
+    for (long long g0 = 0; g0 < groups; g0 += per) {
+        const long long gn = std::min(per, groups - g0);
+        a.data = d_data + (size_t)g0 * c->k * pitch;
+        a.parity = d_par + (size_t)g0 * m * pitch;
+        a.work = (uint64_t)gn * a.cols;
+        hipError_t e = launch_encode(a, g_variant.load(), s);
+        if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
+    }
+    return QFEC_OK;
+}
+
+int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const int32_t* group_rec,
+                    const uint32_t* recs, uint8_t* d_data, const uint8_t* d_par, const uint8_t* d_marks,
+                    long long groups, int block, long long pitch, unsigned* d_failed, hipStream_t s) {
+    (void)ctx;
+    ReconArgs a{};
+    const RecordLayout L = record_layout(c->k, c->m);
+    a.data = d_data;
+    a.parity = d_par;
+    a.marks = d_marks;
+    a.lut = lut;
+    a.group_rec = group_rec;
+    a.records = recs;
+    a.failed = d_failed;
+    a.groups = (uint64_t)groups;
+    a.pitch = (uint64_t)pitch;
+    a.k = c->k;
+    a.m = c->m;
+    a.surv_off = L.surv_off;
+    a.lost_off = L.lost_off;
+    a.hdr = L.hdr;
+    a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
+    a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
+    hipError_t e = launch_reconstruct(a, s);
+    if (e != hipSuccess) return hip_fail(e, "reconstruct kernel launch");
+    return QFEC_OK;
+}
+
+// decode records for groups given host-side marks (rs.c layout); explicit mode
+int host_records(qfec_code* c, const uint8_t* marks, long long groups, std::vector<int32_t>& grec,
+                 std::vector<uint32_t>& recs, long long* nfail) {
+    const int k = c->k, m = c->m;
+    if (c->rec_cache_version != c->version) {
+        c->rec_cache.clear();
+        c->rec_cache_version = c->version;
+    }
+    std::unordered_map<uint64_t, int32_t> off_of;
+    grec.assign((size_t)groups, QFEC_REC_NONE);
+    recs.clear();
+    *nfail = 0;
+    std::vector<uint8_t> gm(k + m);
+    for (long long g = 0; g < groups; ++g) {
+        // group-order view of this group's marks (module/rs.c:611-639 walk)
+        const uint8_t* dm = marks + (size_t)g * k;
+        const uint8_t* pm = marks + (size_t)groups * k + (size_t)g * m;
+        int e = 0;
+        for (int i = 0; i < k; ++i) e += dm[i] ? 1 : 0;
+        if (!e) continue;
+        // chosen parity: first e non-erased, ascending
+        uint64_t kd = 0;
+        std::vector<int> chosen;
+        for (int j = 0; j < m && (int)chosen.size() < e; ++j)
+            if (!pm[j]) chosen.push_back(j);
+        if ((int)chosen.size() < e) { grec[g] = QFEC_REC_FAIL; ++*nfail; continue; }
+        // key over erased data + chosen parity; k + m may exceed 64 here, so hash the lists
+        uint64_t h = 1469598103934665603ull;
+        for (int i = 0; i < k; ++i) if (dm[i]) { h = (h ^ (uint64_t)i) * 1099511628211ull; }
+        h = (h ^ 0xFFFFu) * 1099511628211ull;
+        for (int j : chosen) h = (h ^ (uint64_t)j) * 1099511628211ull;
+        kd = h;
+        auto it = off_of.find(kd);
+        if (it != off_of.end()) { grec[g] = it->second; continue; }
+        auto ct = c->rec_cache.find(kd);
+        if (ct == c->rec_cache.end()) {
+            for (int i = 0; i < k; ++i) gm[i] = dm[i];
+            for (int j = 0; j < m; ++j) gm[k + j] = 1;
+            for (int j : chosen) gm[k + j] = 0;
+            std::vector<uint8_t> rows;
+            std::vector<int> surv, lost;
+            const int ee = decode_rows(c->rows.data(), k, m, gm.data(), rows, surv, lost);
+            if (ee <= 0) { grec[g] = QFEC_REC_FAIL; ++*nfail; continue; }
+            const RecordLayout L = record_layout(k, m);
+            std::vector<uint32_t> one(L.words(ee, k));
+            build_record(L, k, ee, rows.data(), surv.data(), lost.data(), c->quirk != 0, one.data());
+            ct = c->rec_cache.emplace(kd, std::move(one)).first;
+        }
+        const int32_t off = (int32_t)recs.size();
+        recs.insert(recs.end(), ct->second.begin(), ct->second.end());
+        off_of.emplace(kd, off);
+        grec[g] = off;
+    }
+    return QFEC_OK;
+}
+
+}  // namespace
+
+// ====================================================================== batched device API
+extern "C" {
+
+const char* qfec_version(void) { return QFEC_VERSION_STRING; }
+
+const char* qfec_last_error(void) { return t_last_error.c_str(); }
+
+const char* qfec_strerror(int err) {
+    switch (err) {
+        case QFEC_OK: return "ok";
+        case QFEC_EINVAL: return "invalid argument";
+        case QFEC_ENODEV: return "no HIP device";
+        case QFEC_EHIP: return "HIP runtime error";
+        case QFEC_ENOMEM: return "out of memory";
+        case QFEC_EUNSUP: return "unsupported shape for this entry point";
+        default: return "unknown error";
+    }
+}
+
+int qfec_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int qfec_set_kernel_variant(int v) {
+    if (v != QFEC_VARIANT_PERM && v != QFEC_VARIANT_LDSLOG) return QFEC_EINVAL;
+    g_variant.store(v);
+    return QFEC_OK;
+}
+
+int qfec_get_kernel_variant(void) { return g_variant.load(); }
+
+qfec_code* qfec_code_new(int flavour, int k, int m) {
+    std::vector<uint8_t> rows;
+    bool ok = false;
+    if (flavour == QFEC_CAUCHY) ok = cauchy_rows(k, m, rows);
+    else if (flavour == QFEC_VANDERMONDE) ok = vandermonde_rows(k, m, rows);
+    if (!ok) {
+        set_error("qfec_code_new: invalid flavour/shape (%d, k=%d, m=%d)", flavour, k, m);
+        return nullptr;
+    }
+    return make_code(k, m, std::move(rows), flavour == QFEC_CAUCHY ? 1 : 0);
+}
+
+qfec_code* qfec_code_from_rows(int k, int m, const unsigned char* parity_rows, int rs_stale_quirk) {
+    if (k <= 0 || m < 0 || k > 256 || k + m > 256 || (m > 0 && !parity_rows)) {
+        set_error("qfec_code_from_rows: bad shape k=%d m=%d", k, m);
+        return nullptr;
+    }
+    std::vector<uint8_t> rows(parity_rows, parity_rows + (size_t)m * k);
+    return make_code(k, m, std::move(rows), rs_stale_quirk ? 1 : 0);
+}
+
+void qfec_code_free(qfec_code* code) { free_code(code); }
+
+int qfec_code_rows(const qfec_code* code, unsigned char* out) {
+    if (!code || !out) return QFEC_EINVAL;
+    memcpy(out, code->rows.data(), code->rows.size());
+    return QFEC_OK;
+}
+
+int qfec_code_shape(const qfec_code* code, int* k, int* m) {
+    if (!code) return QFEC_EINVAL;
+    if (k) *k = code->k;
+    if (m) *m = code->m;
+    return QFEC_OK;
+}
+
+int qfec_encode(qfec_code* code, const unsigned char* d_data, unsigned char* d_parity, long long groups,
+                int block_size, long long pitch, void* stream) {
+    if (!code || groups < 0 || block_size < 1 || pitch < block_size || (groups > 0 && (!d_data || !d_parity))) {
+        set_error("qfec_encode: invalid argument");
+        return QFEC_EINVAL;
+    }
+    if (groups == 0 || code->m == 0) return QFEC_OK;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    uint32_t* tab = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_enc(code, ctx->device, &tab);
+    }
+    if (rc) return rc;
+    return run_encode(*ctx, code, tab, code->m, d_data, d_parity, groups, block_size, pitch, (hipStream_t)stream);
+}
+
+int qfec_prepare_reconstruct(qfec_code* code) {
+    if (!code) return QFEC_EINVAL;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    DevTables* d = nullptr;
+    std::lock_guard<std::mutex> lk(code->mu);
+    return ensure_lut(code, ctx->device, &d);
+}
+
+int qfec_reconstruct(qfec_code* code, unsigned char* d_data, const unsigned char* d_parity,
+                     const unsigned char* d_marks, long long groups, int block_size, long long pitch,
+                     unsigned int* d_failed, void* stream) {
+    if (!code || groups < 0 || block_size < 1 || pitch < block_size ||
+        (groups > 0 && (!d_data || !d_marks || (code->m > 0 && !d_parity)))) {
+        set_error("qfec_reconstruct: invalid argument");
+        return QFEC_EINVAL;
+    }
+    if (groups == 0) return QFEC_OK;
+    if (groups > 0x7FFFFFFFll * 4) {
+        set_error("qfec_reconstruct: too many groups per call");
+        return QFEC_EINVAL;
+    }
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    DevTables* d = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_lut(code, ctx->device, &d);
+    }
+    if (rc) return rc;
+    return run_reconstruct(*ctx, code, d->d_lut, nullptr, d->d_rec, d_data, d_parity, d_marks, groups, block_size,
+                           pitch, d_failed, (hipStream_t)stream);
+}
+
+int qfec_decode_rows(const qfec_code* code, const unsigned char* marks_n, unsigned char* rows_out,
+                     int* survivors_out, int* erased_out) {
+    if (!code || !marks_n) return QFEC_EINVAL;
+    std::vector<uint8_t> rows;
+    std::vector<int> surv, lost;
+    const int e = decode_rows(code->rows.data(), code->k, code->m, marks_n, rows, surv, lost);
+    if (e > 0) {
+        if (rows_out) memcpy(rows_out, rows.data(), rows.size());
+        if (survivors_out) memcpy(survivors_out, surv.data(), surv.size() * sizeof(int));
+        if (erased_out) memcpy(erased_out, lost.data(), lost.size() * sizeof(int));
+    }
+    return e;
+}
+
+int qfec_synth_fill(unsigned char* d_ptr, long long nbytes, unsigned long long seed, void* stream) {
+    if (nbytes < 0 || (nbytes > 0 && !d_ptr)) return QFEC_EINVAL;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    hipError_t e = launch_synth_fill(d_ptr, (uint64_t)nbytes, seed, (hipStream_t)stream);
+    return e == hipSuccess ? QFEC_OK : hip_fail(e, "synth fill launch");
+}
+
+// streaming probe with the encode's traffic shape (XOR only, not a codec): calibration
+int qfec_probe_stream(const unsigned char* d_data, unsigned char* d_parity, long long groups, int k, int m,
+                      int block_size, long long pitch, void* stream) {
+    if (groups <= 0 || k <= 0 || m <= 0 || !vec16_ok(d_data, d_parity, block_size, pitch)) return QFEC_EINVAL;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    EncodeArgs a{};
+    a.data = d_data;
+    a.parity = d_parity;
+    a.k = k;
+    a.m = m;
+    a.pitch = (uint64_t)pitch;
+    a.vec16 = 1;
+    a.cols = (uint32_t)((block_size + 15) / 16);
+    a.cols_div = make_div_magic(a.cols);
+    a.work = (uint64_t)groups * a.cols;
+    if (a.work >= 0x80000000ull) return QFEC_EINVAL;
+    hipError_t e = launch_probe_xor(a, (hipStream_t)stream);
+    return e == hipSuccess ? QFEC_OK : hip_fail(e, "probe launch");
+}
+
+}  // extern "C"
+
+// ====================================================================== host-buffer paths
+namespace {
+
+// gather `count` rows of `len` bytes from ptrs[] (host or device) into device rows of
+// `pitch` at dst (device); uses the pinned stage at hst when the rows are host memory.
+int gather_rows(DevCtx& c, unsigned char* const* ptrs, size_t count, int len, size_t pitch, uint8_t* d_dst,
+                uint8_t* h_tmp, bool dev_src) {
+    if (dev_src) {
+        for (size_t i = 0; i < count; ++i)
+            HIP_TRY(hipMemcpyAsync(d_dst + i * pitch, ptrs[i], (size_t)len, hipMemcpyDeviceToDevice, c.stream));
+        return QFEC_OK;
+    }
+    for (size_t i = 0; i < count; ++i) memcpy(h_tmp + i * pitch, ptrs[i], (size_t)len);
+    HIP_TRY(hipMemcpyAsync(d_dst, h_tmp, count * pitch, hipMemcpyHostToDevice, c.stream));
+    return QFEC_OK;
+}
+
+int scatter_rows(DevCtx& c, unsigned char* const* ptrs, size_t count, int len, size_t pitch, const uint8_t* d_src,
+                 uint8_t* h_tmp, bool dev_dst, const uint8_t* only /* nullable: rows to write */) {
+    if (dev_dst) {
+        for (size_t i = 0; i < count; ++i)
+            if (!only || only[i])
+                HIP_TRY(hipMemcpyAsync(ptrs[i], d_src + i * pitch, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        return QFEC_OK;
+    }
+    HIP_TRY(hipMemcpyAsync(h_tmp, d_src, count * pitch, hipMemcpyDeviceToHost, c.stream));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    for (size_t i = 0; i < count; ++i)
+        if (!only || only[i]) memcpy(ptrs[i], h_tmp + i * pitch, (size_t)len);
+    return QFEC_OK;
+}
+
+// rows laid out back to back from ptrs[0] with stride len (a contiguous device batch)
+bool contiguous(unsigned char* const* ptrs, size_t count, int len) {
+    for (size_t i = 1; i < count; ++i)
+        if (ptrs[i] != ptrs[0] + i * (size_t)len) return false;
+    return true;
+}
+
+constexpr size_t kChunkBytes = (size_t)256 << 20;  // staging chunk for host-buffer batches
+
+}  // namespace
+
+// ====================================================================== module/rs.h ABI
+namespace {
+
+struct rs_handle {
+    reed_solomon pub;  // must stay first: callers see only this prefix (rs.h:7-13)
+    qfec_code* code;
+};
+
+std::atomic<int> g_rs_errno{0};
+std::once_flag g_rs_init_once;
+
+// pick up edits callers made to the public parity matrix since the last call
+void sync_rows(rs_handle* h) {
+    qfec_code* c = h->code;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (memcmp(c->rows.data(), h->pub.parity, c->rows.size()) != 0) {
+        memcpy(c->rows.data(), h->pub.parity, c->rows.size());
+        ++c->version;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+void reed_solomon_init(void) {
+    std::call_once(g_rs_init_once, [] { (void)field(); });
+}
+
+reed_solomon* reed_solomon_new(int data_shards, int parity_shards) {
+    reed_solomon_init();
+    int err = 0;
+    const int k = data_shards, m = parity_shards, n = k + m;
+    rs_handle* h = nullptr;
+    do {
+        if (n > DATA_SHARDS_MAX || k <= 0 || m <= 0) { err = 1; break; }  // rs.c:404-407
+        h = (rs_handle*)calloc(1, sizeof(rs_handle));
+        if (!h) { err = 2; break; }
+        h->pub.data_shards = k;
+        h->pub.parity_shards = m;
+        h->pub.shards = n;
+        h->pub.m = (unsigned char*)calloc((size_t)n * k, 1);
+        h->pub.parity = (unsigned char*)calloc((size_t)m * k, 1);
+        if (!h->pub.m || !h->pub.parity) { err = 4; break; }
+        std::vector<uint8_t> rows;
+        if (!cauchy_rows(k, m, rows)) { err = 1; break; }
+        for (int i = 0; i < k; ++i) h->pub.m[(size_t)i * k + i] = 1;
+        memcpy(h->pub.m + (size_t)k * k, rows.data(), rows.size());
+        memcpy(h->pub.parity, rows.data(), rows.size());
+        h->code = make_code(k, m, std::move(rows), 1);
+        if (!h->code) { err = 5; break; }
+        g_rs_errno = 0;
+        return &h->pub;
+    } while (0);
+    g_rs_errno = err;
+    fprintf(stderr, "err=%d\n", err);  // rs.c:458
+    if (h) {
+        free(h->pub.m);
+        free(h->pub.parity);
+        free(h);
+    }
+    return nullptr;
+}
+
+void reed_solomon_release(reed_solomon* rs) {
+    if (!rs) return;
+    rs_handle* h = (rs_handle*)rs;
+    free_code(h->code);
+    free(h->pub.m);
+    free(h->pub.parity);
+    free(h);
+}
+
+int reed_solomon_error(void) { return g_rs_errno.load(); }
+
+qfec_code* qfec_rs_code(reed_solomon* rs) {
+    if (!rs) return nullptr;
+    rs_handle* h = (rs_handle*)rs;
+    sync_rows(h);
+    return h->code;
+}
+
+int reed_solomon_encode(reed_solomon* rs, unsigned char** shards, int nr_shards, int block_size) {
+    if (!rs || !shards) return 0;
+    rs_handle* h = (rs_handle*)rs;
+    const int k = rs->data_shards, m = rs->parity_shards, n = rs->shards;
+    const long long G = nr_shards / n;
+    if (G <= 0 || block_size <= 0) return 0;
+    sync_rows(h);
+    qfec_code* c = h->code;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) { fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error()); return rc; }
+    uint32_t* tab = nullptr;
+    bool any_stale = false;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        rc = ensure_enc(c, ctx->device, &tab);
+        for (int r = 0; r < m; ++r) any_stale |= c->rows[(size_t)r * k] == 0;
+    }
+    if (rc) { fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error()); return rc; }
+    unsigned char** data = shards;
+    unsigned char** par = shards + G * k;
+    const bool dev = is_device_ptr(shards[0]);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (dev && contiguous(data, (size_t)G * k, block_size) && contiguous(par, (size_t)G * m, block_size)) {
+        rc = run_encode(*ctx, c, tab, m, data[0], par[0], G, block_size, block_size, ctx->stream);
+        if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : QFEC_EHIP;
+        if (rc) fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
+        return rc;
+    }
+    const size_t pitch = round_up((size_t)block_size, 16);
+    const long long per = std::max<long long>(1, (long long)(kChunkBytes / ((size_t)n * pitch)));
+    for (long long g0 = 0; g0 < G && !rc; g0 += per) {
+        const long long gn = std::min(per, G - g0);
+        const size_t dbytes = (size_t)gn * k * pitch, pbytes = (size_t)gn * m * pitch;
+        if ((rc = ensure_stage(*ctx, dbytes + pbytes, dbytes + pbytes))) break;
+        uint8_t* d_d = ctx->d_stage;
+        uint8_t* d_p = ctx->d_stage + dbytes;
+        if ((rc = gather_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, ctx->h_stage, dev))) break;
+        if (any_stale &&
+            (rc = gather_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, ctx->h_stage + dbytes, dev)))
+            break;
+        if ((rc = run_encode(*ctx, c, tab, m, d_d, d_p, gn, block_size, (long long)pitch, ctx->stream))) break;
+        rc = scatter_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, ctx->h_stage + dbytes, dev,
+                          nullptr);
+    }
+    if (rc) fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
+    return rc;
+}
+
+int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned char* marks, int nr_shards,
+                             int block_size) {
+    if (!rs || !shards || !marks) return 0;
+    rs_handle* h = (rs_handle*)rs;
+    const int k = rs->data_shards, m = rs->parity_shards, n = rs->shards;
+    const long long G = nr_shards / n;
+    if (G <= 0 || block_size <= 0) return 0;
+    sync_rows(h);
+    qfec_code* c = h->code;
+    const bool dev_marks = is_device_ptr(marks);
+    std::vector<uint8_t> hmarks;
+    const uint8_t* mk = marks;
+    if (dev_marks) {
+        hmarks.resize((size_t)G * n);
+        if (hipMemcpy(hmarks.data(), marks, hmarks.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+            fprintf(stderr, "[qfec] reed_solomon_reconstruct: cannot read device marks\n");
+            return QFEC_EHIP;
+        }
+        mk = hmarks.data();
+    }
+    // groups under-determined -> -1 (rs.c:631-634); host-side count, same rule as the kernel
+    std::vector<int32_t> grec;
+    std::vector<uint32_t> recs;
+    long long nfail = 0;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        host_records(c, mk, G, grec, recs, &nfail);
+    }
+    if (recs.empty()) return nfail ? -1 : 0;  // nothing to recover
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) { fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error()); return rc; }
+    unsigned char** data = shards;
+    unsigned char** par = shards + G * k;
+    const bool dev = is_device_ptr(shards[0]);
+    const size_t pitch = round_up((size_t)block_size, 16);
+    std::vector<uint8_t> only((size_t)G * k);
+    for (size_t i = 0; i < only.size(); ++i) only[i] = mk[i] ? 1 : 0;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    // one batch: data | parity | group records | record words (chunking keeps the
+    // record offsets of the whole call valid, so stage the groups in one pass)
+    const size_t dbytes = (size_t)G * k * pitch, pbytes = (size_t)G * m * pitch;
+    const size_t gbytes = round_up((size_t)G * 4, 16), rbytes = round_up(recs.size() * 4, 16);
+    if ((rc = ensure_stage(*ctx, dbytes + pbytes + gbytes + rbytes, dbytes + pbytes + gbytes + rbytes)) == 0) {
+        uint8_t* d_d = ctx->d_stage;
+        uint8_t* d_p = d_d + dbytes;
+        int32_t* d_g = (int32_t*)(d_p + pbytes);
+        uint32_t* d_r = (uint32_t*)((uint8_t*)d_g + gbytes);
+        uint8_t* hs = ctx->h_stage;
+        memcpy(hs + dbytes + pbytes, grec.data(), (size_t)G * 4);
+        memcpy(hs + dbytes + pbytes + gbytes, recs.data(), recs.size() * 4);
+        rc = gather_rows(*ctx, data, (size_t)G * k, block_size, pitch, d_d, hs, dev);
+        if (!rc) rc = gather_rows(*ctx, par, (size_t)G * m, block_size, pitch, d_p, hs + dbytes, dev);
+        if (!rc && hipMemcpyAsync(d_g, hs + dbytes + pbytes, gbytes + rbytes, hipMemcpyHostToDevice, ctx->stream) !=
+                       hipSuccess)
+            rc = QFEC_EHIP;
+        if (!rc) rc = run_reconstruct(*ctx, c, nullptr, d_g, d_r, d_d, d_p, nullptr, G, block_size, (long long)pitch,
+                                      nullptr, ctx->stream);
+        if (!rc) rc = scatter_rows(*ctx, data, (size_t)G * k, block_size, pitch, d_d, hs, dev, only.data());
+    }
+    if (rc) {
+        fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error());
+        return rc;
+    }
+    return nfail ? -1 : 0;
+}
+
+}  // extern "C"
+
+// ====================================================================== system/fec.h ABI
+namespace {
+
+struct fec_handle {
+    int k, n;
+    qfec_code* code;
+    std::vector<uint8_t> full;  // n x k systematic matrix (identity on top)
+};
+
+// run `rows` (e x k coefficient rows) over k input packets of sz bytes -> e outputs
+int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* const* in, unsigned char* const* out,
+               int sz) {
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    const bool dev = is_device_ptr(in[0]);
+    const size_t pitch = round_up((size_t)sz, 16);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if ((rc = ensure_small(*ctx, tab.size()))) return rc;
+    const size_t ib = (size_t)k * pitch, ob = (size_t)e * pitch;
+    if ((rc = ensure_stage(*ctx, ib + ob, ib + ob))) return rc;
+    memcpy(ctx->h_small, tab.data(), tab.size() * 4);
+    HIP_TRY(hipMemcpyAsync(ctx->d_small, ctx->h_small, tab.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = gather_rows(*ctx, in, (size_t)k, sz, pitch, ctx->d_stage, ctx->h_stage, dev))) return rc;
+    qfec_code tmp;
+    tmp.k = k;
+    tmp.m = e;
+    if ((rc = run_encode(*ctx, &tmp, ctx->d_small, e, ctx->d_stage, ctx->d_stage + ib, 1, sz, (long long)pitch,
+                         ctx->stream)))
+        return rc;
+    return scatter_rows(*ctx, out, (size_t)e, sz, pitch, ctx->d_stage + ib, ctx->h_stage + ib,
+                        is_device_ptr(out[0]), nullptr);
+}
+
+std::once_flag g_fec_init_once;
+
+}  // namespace
+
+extern "C" {
+
+void* fec_new(int k, int n) {
+    std::call_once(g_fec_init_once, [] { (void)field(); });  // init_fec (fec.c:612-625), once
+    if (k > 256 || n > 256 || k > n) {  // fec.c:664-668
+        fprintf(stderr, "Invalid parameters k %d n %d GF_SIZE %d\n", k, n, 255);
+        return nullptr;
+    }
+    std::vector<uint8_t> rows;
+    if (!vandermonde_rows(k, n - k, rows)) {
+        fprintf(stderr, "Invalid parameters k %d n %d GF_SIZE %d\n", k, n, 255);
+        return nullptr;
+    }
+    fec_handle* h = new (std::nothrow) fec_handle();
+    if (!h) {
+        fprintf(stderr, "-- malloc failure allocating new_code\n");
+        exit(1);  // my_malloc (fec.c:238-247)
+    }
+    h->k = k;
+    h->n = n;
+    h->full.assign((size_t)n * k, 0);
+    for (int i = 0; i < k; ++i) h->full[(size_t)i * k + i] = 1;
+    memcpy(h->full.data() + (size_t)k * k, rows.data(), rows.size());
+    h->code = make_code(k, n - k, std::move(rows), 0);
+    return h;
+}
+
+void fec_free(void* p) {
+    if (!p) {
+        fprintf(stderr, "bad parameters to fec_free\n");  // fec.c:641-643
+        return;
+    }
+    fec_handle* h = (fec_handle*)p;
+    free_code(h->code);
+    delete h;
+}
+
+qfec_code* qfec_fec_code(void* p) { return p ? ((fec_handle*)p)->code : nullptr; }
+
+int qfec_fec_matrix(void* p, unsigned char* out_full) {
+    if (!p || !out_full) return QFEC_EINVAL;
+    fec_handle* h = (fec_handle*)p;
+    memcpy(out_full, h->full.data(), h->full.size());
+    return QFEC_OK;
+}
+
+void fec_encode(void* code, unsigned char** src, unsigned char* dst, int index, int sz) {
+    fec_handle* h = (fec_handle*)code;
+    if (!h) return;
+    const int k = h->k;
+    if (index >= 0 && index < k) {  // fec.c:723-724: a copy
+        if (sz <= 0) return;
+        if (is_device_ptr(src[index]) || is_device_ptr(dst)) {
+            if (hipMemcpy(dst, src[index], (size_t)sz, hipMemcpyDefault) != hipSuccess)
+                fprintf(stderr, "[qfec] fec_encode: copy failed\n");
+        } else {
+            memcpy(dst, src[index], (size_t)sz);
+        }
+        return;
+    }
+    if (index < 0 || index >= h->n) {  // fec.c:730-732
+        fprintf(stderr, "Invalid index %d (max %d)\n", index, h->n - 1);
+        return;
+    }
+    if (sz <= 0) return;
+    std::vector<uint32_t> tab((size_t)k * QFEC_TAB_STRIDE);
+    for (int i = 0; i < k; ++i) perm_entry(h->full[(size_t)index * k + i], &tab[(size_t)i * QFEC_TAB_STRIDE]);
+    unsigned char* outs[1] = {dst};
+    int rc = apply_rows(tab, k, 1, src, outs, sz);
+    if (rc) fprintf(stderr, "[qfec] fec_encode: %s\n", qfec_last_error());
+}
+
+int fec_decode(void* code, unsigned char** pkt, int* index, int sz) {
+    fec_handle* h = (fec_handle*)code;
+    if (!h) return 1;
+    const int k = h->k, n = h->n;
+    // shuffle (fec.c:738-771): data packets move to the slot of their index
+    for (int i = 0; i < k;) {
+        const int c = index[i];
+        if (c >= k || c == i) { ++i; continue; }
+        if (c < 0) return 1;           // undefined in the reference; rejected
+        if (index[c] == c) return 1;   // conflict
+        std::swap(index[i], index[c]);
+        std::swap(pkt[i], pkt[c]);
+    }
+    // build_decode_matrix (fec.c:778-808)
+    std::vector<uint8_t> dm((size_t)k * k, 0);
+    for (int r = 0; r < k; ++r) {
+        if (index[r] < k) {
+            dm[(size_t)r * k + r] = 1;
+        } else if (index[r] < n) {
+            memcpy(&dm[(size_t)r * k], &h->full[(size_t)index[r] * k], (size_t)k);
+        } else {
+            fprintf(stderr, "decode: invalid index %d (max %d)\n", index[r], n - 1);
+            return 1;
+        }
+    }
+    if (!gf_invert(dm.data(), k)) {
+        fprintf(stderr, "singular matrix\n");
+        return 1;
+    }
+    if (sz <= 0) return 0;
+    // rows to recover: slots holding parity (fec.c:840-858)
+    std::vector<int> slots;
+    for (int r = 0; r < k; ++r)
+        if (index[r] >= k) slots.push_back(r);
+    if (slots.empty()) return 0;
+    const int e = (int)slots.size();
+    std::vector<uint32_t> tab((size_t)e * k * QFEC_TAB_STRIDE);
+    for (int j = 0; j < e; ++j)
+        for (int c = 0; c < k; ++c)
+            perm_entry(dm[(size_t)slots[j] * k + c], &tab[((size_t)j * k + c) * QFEC_TAB_STRIDE]);
+    std::vector<unsigned char*> outs(e);
+    for (int j = 0; j < e; ++j) outs[j] = pkt[slots[j]];
+    const int rc = apply_rows(tab, k, e, pkt, outs.data(), sz);
+    if (rc) {
+        fprintf(stderr, "[qfec] fec_decode: %s\n", qfec_last_error());
+        return 1;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,121 @@
+"""CPU tests of libqfec: it loads, exports every symbol include/*.h declares, and its host
+logic (matrix builders, decode-matrix selection, handle bookkeeping) matches the golden
+vectors the reference produced.  No kernel is launched here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+import quicknet_amd as qa
+from quicknet_amd._lib import EXPORTS, lib
+
+
+def header_functions(path):
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\(", txt, flags=re.M)
+    return sorted(set(n for n in names if n not in ("defined",)))
+
+
+@pytest.mark.parametrize("header", ["qfec.h", "qfec_fec.h", "qfec_rs.h"])
+def test_exports_match_headers(header):
+    L = lib()
+    declared = header_functions(os.path.join(ROOT, "include", header))
+    assert declared, header
+    assert sorted(EXPORTS[header]) == declared
+    for name in declared:
+        assert hasattr(L, name), f"{name} not exported"
+
+
+def test_version():
+    assert lib().qfec_version().decode().startswith("qfec")
+
+
+def test_matrices_vs_golden(golden):
+    z = golden("matrices.npz")
+    for key in z.files:
+        if key.startswith("rs_") and key != "rs_errors":
+            k, m = map(int, key.split("_")[1:])
+            assert np.array_equal(qa.Code.cauchy(k, m).rows, z[key]), key
+        elif key.startswith("fec_") and key != "fec_errors":
+            k, n = map(int, key.split("_")[1:])
+            if n > k:
+                assert np.array_equal(qa.Code.vandermonde(k, n - k).rows, z[key][k:]), key
+            f = qa.FecParms(k, n)
+            assert np.array_equal(f.matrix, z[key]), key
+
+
+def test_reed_solomon_handle_vs_golden(golden):
+    """reed_solomon_new exposes the same public struct contents as module/rs.c."""
+    z = golden("matrices.npz")
+    L = lib()
+    for k, m in [(1, 1), (4, 2), (10, 3), (16, 4), (200, 55), (1, 254)]:
+        rs = qa.ReedSolomon(k, m)
+        h = rs._h.contents
+        assert (h.data_shards, h.parity_shards, h.shards) == (k, m, k + m)
+        full = np.ctypeslib.as_array(h.m, shape=(k + m, k))
+        assert np.array_equal(full, z[f"rsfull_{k}_{m}"])
+        assert np.array_equal(rs.parity, z[f"rs_{k}_{m}"])
+        assert L.reed_solomon_error() == 0
+    for k, m, err in z["rs_errors"]:
+        assert not L.reed_solomon_new(int(k), int(m))
+        assert L.reed_solomon_error() == err
+
+
+def test_fec_new_rejects_like_reference(golden):
+    z = golden("matrices.npz")
+    for k, n, ok in z["fec_errors"]:
+        assert not lib().fec_new(int(k), int(n))
+
+
+def test_decode_rows_host(oracle):
+    """Decode-matrix selection (module/rs.c:620-629) + GF inversion on the host."""
+    rng = np.random.default_rng(5)
+    for flavour in ("cauchy", "vandermonde"):
+        for k, m in [(4, 2), (10, 3), (16, 4), (5, 3)]:
+            code = getattr(qa.Code, flavour)(k, m)
+            P = code.rows
+            for _ in range(40):
+                marks = (rng.random(k + m) < 0.25).astype(np.uint8)
+                e, rows, surv, lost = code.decode_rows(marks)
+                lost_ref = [i for i in range(k) if marks[i]]
+                avail = [j for j in range(m) if not marks[k + j]]
+                if not lost_ref:
+                    assert e == 0
+                    continue
+                if len(avail) < len(lost_ref):
+                    assert e == -1
+                    continue
+                chosen = avail[: len(lost_ref)]
+                surv_ref = [i for i in range(k) if not marks[i]] + [k + j for j in chosen]
+                assert e == len(lost_ref) and list(lost) == lost_ref and list(surv) == surv_ref
+                D = np.zeros((k, k), dtype=np.uint8)
+                for r, s in enumerate(surv_ref):
+                    if s < k:
+                        D[r, s] = 1
+                    else:
+                        D[r] = P[s - k]
+                inv = oracle.invert(D)
+                assert np.array_equal(rows, inv[lost_ref])
+
+
+def test_no_gpu_fails_loudly():
+    """Without a device every compute entry point errors (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    L = lib()
+    assert L.qfec_device_count() == 0
+    rc = L.qfec_synth_fill(C.c_void_p(64), 16, 1, None)
+    assert rc == -2 and "no HIP device" in L.qfec_last_error().decode()
+    code = qa.Code.cauchy(4, 2)
+    rc = L.qfec_encode(code._h, C.c_void_p(64), C.c_void_p(128), 1, 16, 16, None)
+    assert rc == -2
+    rs = qa.ReedSolomon(4, 2)
+    data = np.zeros((1, 4, 16), np.uint8)
+    par = np.zeros((1, 2, 16), np.uint8)
+    assert rs.encode(data, par, 16) != 0

@@ -1,0 +1,271 @@
+"""GPU parity: the HIP path (libqfec.so kernels, called through the C ABI) against the golden
+vectors the reference produced and against the CPU oracle.  Bit-exact (integer work).
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+import hashlib
+import itertools
+
+import numpy as np
+import pytest
+
+import quicknet_amd as qa
+from quicknet_amd.synth import erasure_marks, marks_to_rs_layout, synth_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+DEV = torch.device("cuda:0")
+ENC_CASES = [(2, 1), (4, 2), (10, 3), (16, 4), (7, 1), (3, 2)]
+ENC_LENS = [1, 8, 1024, 1400, 37]
+
+
+def to_dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def padded(a, pitch, fill=0):
+    """[..., B] -> [..., pitch] with pad bytes = fill."""
+    out = np.full(a.shape[:-1] + (pitch,), fill, dtype=np.uint8)
+    out[..., : a.shape[-1]] = a
+    return out
+
+
+def round16(x):
+    return (x + 15) // 16 * 16
+
+
+@pytest.fixture(autouse=True)
+def _variant_reset():
+    qa.set_kernel_variant(qa._lib.QFEC_VARIANT_PERM)
+    yield
+    qa.set_kernel_variant(qa._lib.QFEC_VARIANT_PERM)
+
+
+def test_synth_fill_matches_host():
+    for n, seed in [(1, 3), (7, 5), (4096, 0x5EED0002), (100003, 9)]:
+        t = torch.empty(n, dtype=torch.uint8, device=DEV)
+        qa.synth_fill(t, seed)
+        assert np.array_equal(t.cpu().numpy(), synth_bytes(seed, n))
+
+
+@pytest.mark.parametrize("km,B", list(itertools.product(ENC_CASES, ENC_LENS)))
+@pytest.mark.parametrize("variant", [0, 1])
+def test_encode_batched_vs_golden(golden, km, B, variant):
+    """qfec_encode on device buffers, fast (pitch = round16) and byte (pitch = B) paths."""
+    qa.set_kernel_variant(variant)
+    z = golden("encode.npz")
+    k, m = km
+    key = f"{k}_{m}_{B}"
+    G = 4
+    data = synth_bytes(int(z[f"seed_{key}"][0]), G * k * B).reshape(G, k, B)
+    for pitch in sorted({round16(B), B}):
+        for flavour, gold, ctor in (("rs", z[f"rs_{key}"], qa.Code.cauchy), ("fec", z[f"fec_{key}"], qa.Code.vandermonde)):
+            code = ctor(k, m)
+            d = to_dev(padded(data, pitch, 0xC3))
+            p = to_dev(np.full((G, m, pitch), 0x5A, np.uint8))
+            code.encode(d, p, B)
+            torch.cuda.synchronize()
+            got = p.cpu().numpy()[..., :B].reshape(G * m, B)
+            assert np.array_equal(got, gold), (flavour, pitch)
+
+
+@pytest.mark.parametrize("km,B", list(itertools.product(ENC_CASES, [8, 1400])))
+def test_encode_abi_vs_golden(golden, km, B):
+    """reed_solomon_encode (host pointer arrays) and per-packet fec_encode."""
+    z = golden("encode.npz")
+    k, m = km
+    key = f"{k}_{m}_{B}"
+    G = 4
+    data = synth_bytes(int(z[f"seed_{key}"][0]), G * k * B).reshape(G, k, B)
+    rs = qa.ReedSolomon(k, m)
+    par = np.full((G, m, B), 0x5A, np.uint8)
+    assert rs.encode(data, par, B) == 0
+    assert np.array_equal(par.reshape(G * m, B), z[f"rs_{key}"])
+    f = qa.FecParms(k, k + m)
+    fpar = np.full((G, m, B), 0xA5, np.uint8)
+    for g in range(G):
+        for j in range(m):
+            f.encode(list(data[g]), fpar[g, j], k + j, B)
+    assert np.array_equal(fpar.reshape(G * m, B), z[f"fec_{key}"])
+    cp = np.zeros(B, np.uint8)
+    f.encode(list(data[0]), cp, k - 1, B)
+    assert np.array_equal(cp, z[f"fcopy_{key}"])
+    bad = np.full(B, 0x33, np.uint8)
+    f.encode(list(data[0]), bad, k + m, B)
+    assert np.array_equal(bad, z[f"fbad_{key}"])
+
+
+def test_encode_rs_quirk(golden):
+    """A zero in column 0 of the public parity matrix leaves dst stale (rs.c:116-117)."""
+    z = golden("encode.npz")
+    k, m, B, G = 4, 2, 16, 2
+    data = synth_bytes(int(z["quirk_seed"][0]), G * k * B).reshape(G, k, B)
+    rs = qa.ReedSolomon(k, m)
+    rs.parity[:] = z["quirk_matrix"]
+    par = np.full((G, m, B), 0x5A, np.uint8)
+    rs.encode(data, par, B)
+    assert np.array_equal(par.reshape(G * m, B), z["quirk_parity"])
+    # same through the batched API with the quirk flag
+    code = qa.Code.from_rows(z["quirk_matrix"], rs_stale_quirk=True)
+    d = to_dev(data)
+    p = to_dev(np.full((G, m, B), 0x5A, np.uint8))
+    code.encode(d, p, B)
+    torch.cuda.synchronize()
+    assert np.array_equal(p.cpu().numpy().reshape(G * m, B), z["quirk_parity"])
+
+
+RECON = [(4, 2, 16), (10, 3, 8), (16, 4, 8), (2, 1, 5), (3, 2, 33)]
+
+
+@pytest.mark.parametrize("k,m,B", RECON)
+@pytest.mark.parametrize("path", ["device", "abi"])
+def test_reconstruct_vs_golden(golden, oracle, k, m, B, path):
+    z = golden("reconstruct.npz")
+    key = f"{k}_{m}_{B}"
+    gm = z[f"marks_{key}"]
+    G = gm.shape[0]
+    seed = int(z[f"seed_{key}"][0])
+    data0 = synth_bytes(seed, G * k * B).reshape(G, k, B)
+    par_c = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(oracle.cauchy(k, m), data0, par_c, B)
+    par_i = synth_bytes(seed ^ 0xFFFF, G * m * B).reshape(G, m, B)
+    marks = marks_to_rs_layout(gm, k)
+    for kind, par in (("cons", par_c), ("incons", par_i)):
+        d = data0.copy()
+        d.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+        if path == "abi":
+            rs = qa.ReedSolomon(k, m)
+            rc = rs.reconstruct(d, par.copy(), marks, B)
+            assert rc == z[f"rc_{kind}_{key}"][0]
+            out = d
+        else:
+            code = qa.Code.cauchy(k, m)
+            pitch = round16(B)
+            dd = to_dev(padded(d, pitch))
+            pp = to_dev(padded(par, pitch))
+            failed = torch.zeros(1, dtype=torch.int32, device=DEV)
+            code.reconstruct(dd, pp, to_dev(marks), B, failed)
+            torch.cuda.synchronize()
+            out = dd.cpu().numpy()[..., :B]
+            nfail = int(failed.item())
+            assert (nfail > 0) == (z[f"rc_{kind}_{key}"][0] == -1)
+        if kind == "cons":
+            assert hashlib.sha256(np.ascontiguousarray(out).tobytes()).digest() == z[f"cons_{key}"].tobytes()
+        else:
+            assert np.array_equal(out.reshape(G * k, B), z[f"incons_{key}"])
+
+
+FEC_DEC = [(2, 4), (3, 5), (5, 8), (4, 6), (3, 4), (4, 5), (5, 6), (7, 8), (10, 13), (16, 20), (1, 3)]
+
+
+@pytest.mark.parametrize("k,n", FEC_DEC)
+def test_fec_decode_vs_golden(golden, k, n):
+    z = golden("fec_decode.npz")
+    key = f"{k}_{n}"
+    f = qa.FecParms(k, n)
+    assert np.array_equal(f.matrix, z[f"matrix_{key}"])
+    B = z[f"pk_in_{key}"].shape[2]
+    for t in range(z[f"rc_{key}"].shape[0]):
+        rc, after, idx = f.decode(z[f"pk_in_{key}"][t], z[f"idx_in_{key}"][t], B)
+        assert rc == z[f"rc_{key}"][t]
+        assert np.array_equal(idx, z[f"idx_out_{key}"][t])
+        assert np.array_equal(after, z[f"pk_out_{key}"][t])
+
+
+@pytest.mark.parametrize("flavour", ["cauchy", "vandermonde"])
+@pytest.mark.parametrize("k,m,B", [(5, 2, 1024), (32, 8, 256), (20, 4, 1400), (9, 5, 100), (12, 4, 1024)])
+def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
+    """Shapes without a templated kernel (runtime k, m loops) and LUT-sized reconstruct."""
+    G = 33
+    code = getattr(qa.Code, flavour)(k, m)
+    rows = code.rows
+    data = synth_bytes(k * 1000 + m, G * k * B).reshape(G, k, B)
+    pitch = round16(B)
+    d = to_dev(padded(data, pitch))
+    p = to_dev(np.zeros((G, m, pitch), np.uint8))
+    code.encode(d, p, B)
+    torch.cuda.synchronize()
+    ref = np.zeros((G, m, B), np.uint8)
+    (oracle.rs_encode if flavour == "cauchy" else oracle.fec_encode)(rows, data, ref, B)
+    assert np.array_equal(p.cpu().numpy()[..., :B], ref)
+    # reconstruct: random erasures incl. unrecoverable ones; random (inconsistent) parity
+    par = synth_bytes(77 + k, G * m * B).reshape(G, m, B)
+    gm = (np.random.default_rng(k).random((G, k + m)) < 0.2).astype(np.uint8)
+    marks = marks_to_rs_layout(gm, k)
+    d0 = data.copy()
+    rc_ref = oracle.rs_reconstruct(rows, d0, par.copy(), marks, B)
+    rs_path = qa.ReedSolomon(k, m) if flavour == "cauchy" and k + m <= 255 else None
+    if rs_path is not None:
+        d1 = data.copy()
+        rs_path.reconstruct(d1, par.copy(), marks, B)  # explicit (host-record) path
+        assert np.array_equal(d1, d0)
+    if k + m <= 24:
+        dd = to_dev(padded(data, pitch))
+        code.reconstruct(dd, to_dev(padded(par, pitch)), to_dev(marks), B)
+        torch.cuda.synchronize()
+        assert np.array_equal(dd.cpu().numpy()[..., :B], d0)
+    assert rc_ref in (0, -1)
+
+
+def test_large_batch_roundtrip(oracle):
+    """BASELINE config 2/3 shape at full size: 100 000 groups x RS(10,3) x 1 KiB.
+    Encode checked byte for byte against the oracle; reconstruct with 3 random erasures
+    per group must return the original data (a size-independent property)."""
+    k, m, B, G = 10, 3, 1024, 100_000
+    code = qa.Code.cauchy(k, m)
+    data = torch.empty((G, k, B), dtype=torch.uint8, device=DEV)
+    qa.synth_fill(data, 0x5EED0002)
+    par = torch.empty((G, m, B), dtype=torch.uint8, device=DEV)
+    code.encode(data, par)
+    torch.cuda.synchronize()
+    h_data = data.cpu().numpy()
+    ref = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(code.rows, h_data, ref, B)
+    assert np.array_equal(par.cpu().numpy(), ref)
+    gm = erasure_marks(0x5EED0003, G, k + m, 3)
+    marks = to_dev(marks_to_rs_layout(gm, k))
+    damaged = data.clone()
+    lost = torch.from_numpy(gm[:, :k].astype(bool)).to(DEV)
+    damaged[lost] = 0x5A
+    failed = torch.zeros(1, dtype=torch.int32, device=DEV)
+    code.reconstruct(damaged, par, marks, B, failed)
+    torch.cuda.synchronize()
+    assert int(failed.item()) == 0
+    assert torch.equal(damaged, data)
+
+
+def test_ldslog_variant_matches_perm():
+    k, m, B, G = 10, 3, 1024, 2000
+    code = qa.Code.vandermonde(k, m)
+    data = torch.empty((G, k, B), dtype=torch.uint8, device=DEV)
+    qa.synth_fill(data, 1234)
+    p0 = torch.empty((G, m, B), dtype=torch.uint8, device=DEV)
+    p1 = torch.empty_like(p0)
+    code.encode(data, p0)
+    qa.set_kernel_variant(qa._lib.QFEC_VARIANT_LDSLOG)
+    code.encode(data, p1)
+    torch.cuda.synchronize()
+    assert torch.equal(p0, p1)
+
+
+def test_device_pointer_abi_paths():
+    """The per-call ABIs accept device pointers too (contiguous and gathered)."""
+    import ctypes as C
+    k, m, B, G = 4, 2, 64, 8
+    rs = qa.ReedSolomon(k, m)
+    data = torch.empty((G, k, B), dtype=torch.uint8, device=DEV)
+    qa.synth_fill(data, 99)
+    par = torch.zeros((G, m, B), dtype=torch.uint8, device=DEV)
+    L = qa.lib()
+    db, pb = data.data_ptr(), par.data_ptr()
+    ptrs = (C.c_void_p * (G * (k + m)))(*([db + i * B for i in range(G * k)] + [pb + i * B for i in range(G * m)]))
+    assert L.reed_solomon_encode(rs._h, ptrs, G * (k + m), B) == 0
+    torch.cuda.synchronize()
+    ref = np.zeros((G, m, B), np.uint8)
+    hd = data.cpu().numpy()
+    qa.ReedSolomon(k, m).encode(hd, ref, B)
+    assert np.array_equal(par.cpu().numpy(), ref)
