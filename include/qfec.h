@@ -97,6 +97,10 @@ int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long s
 int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long long groups, int k, int m,
                       int block_size, long long pitch, void *stream);
 
+/* Experiment knobs for interleaved A/B timing (tools/ab.py): "encode_impl" 0|1,
+ * "recon_impl" -1 (auto) | 0 | 1.  Defaults are the measured best; results are identical. */
+int qfec_tune(const char *key, int value);
+
 int qfec_set_kernel_variant(int variant);
 int qfec_get_kernel_variant(void);
 int qfec_device_count(void);

@@ -17,7 +17,7 @@ import numpy as np
 from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
 
 __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
-           "set_kernel_variant", "synth_fill", "probe_stream", "device_count"]
+           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count"]
 
 
 def _stream_handle(stream):
@@ -45,6 +45,11 @@ def device_count():
 
 def set_kernel_variant(v):
     check(lib().qfec_set_kernel_variant(v), "qfec_set_kernel_variant")
+
+
+def tune(key, value):
+    """Experiment knob (see include/qfec.h qfec_tune); outputs are identical either way."""
+    check(lib().qfec_tune(key.encode(), int(value)), f"qfec_tune({key})")
 
 
 def synth_fill(t, seed, stream=None):

@@ -48,6 +48,11 @@ void build_field() {
 
 }  // namespace
 
+Tuning& tuning() {
+    static Tuning t;
+    return t;
+}
+
 const Field& field() {
     std::call_once(g_field_once, build_field);
     return g_field;

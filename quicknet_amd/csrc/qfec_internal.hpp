@@ -43,6 +43,7 @@ struct EncodeArgs {
     uint32_t cols;          // columns per row: 16-B columns (vec16) or bytes
     int k, m;
     int vec16;
+    int impl;               // tuning "encode_impl"
 };
 
 struct ReconArgs {
@@ -59,7 +60,15 @@ struct ReconArgs {
     int k, m;
     int surv_off, lost_off, hdr;
     int vec16;
+    int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once
 };
+
+// runtime tuning knobs (qfec_tune); defaults are the measured best
+struct Tuning {
+    int recon_impl = -1;  // -1 auto (per shape), 0 row loop, 1 all rows
+    int encode_impl = 0;
+};
+Tuning& tuning();
 
 hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream);
 hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream);

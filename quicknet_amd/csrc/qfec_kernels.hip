@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "qfec_internal.hpp"
 
 namespace qfec {
@@ -91,6 +93,11 @@ __device__ __forceinline__ void gf_mac16x2(uint4& acc, const Sel (&sa)[4], const
     acc.w = mac2(acc.w, sa[3], sb[3], a5, b5);
 }
 
+// opaque register barrier: uses of v after it cannot be hoisted above it
+__device__ __forceinline__ void pin16(uint4& v) {
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+}
+
 __device__ __forceinline__ void sel16(Sel (&s)[4], const uint4& v) {
     s[0] = gf_sel(v.x);
     s[1] = gf_sel(v.y);
@@ -105,8 +112,12 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
 }
+// written once, read by a later launch or the host: non-temporal store (measured on
+// MI355X: the encode traffic shape streams at 6.3 TB/s with nt loads + nt stores against
+// 5.7 TB/s with plain stores, tools/membench.hip)
 __device__ __forceinline__ void st16(uint8_t* p, const uint4& v) {
-    *reinterpret_cast<uint4*>(p) = v;
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
 __device__ __forceinline__ uint64_t fast_div(uint64_t n, const DivMagic& d) {
@@ -155,6 +166,43 @@ __global__ void __launch_bounds__(256) k_encode_perm(EncodeArgs a) {
     }
 #pragma unroll
     for (int r = 0; r < M; ++r) st16(dst + (uint64_t)r * a.pitch, acc[r]);
+}
+
+// Variant (tuning "encode_impl" = 1): one output row at a time, selectors re-formed per
+// row (pinned against LICM) -- fewer registers, more VALU.
+template <int K, int M>
+__global__ void __launch_bounds__(256) k_encode_perm_rows(EncodeArgs a) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (t >= a.work) return;
+    const uint64_t g = fast_div(t, a.cols_div);
+    const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
+    const uint8_t* src = a.data + g * (uint64_t)(K * a.pitch) + (uint64_t)col * 16u;
+    uint8_t* dst = a.parity + g * (uint64_t)(M * a.pitch) + (uint64_t)col * 16u;
+    const uint32_t* __restrict__ tab = a.tab;
+    uint4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = ld16(src + (uint64_t)c * a.pitch);
+    for (int r = 0; r < M; ++r) {
+        const uint32_t* tr = tab + r * K * QFEC_TAB_STRIDE;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        if (tr[5]) acc = *reinterpret_cast<const uint4*>(dst + (uint64_t)r * a.pitch);
+#pragma unroll
+        for (int c = 0; c + 1 < K; c += 2) {
+            pin16(x[c]);
+            pin16(x[c + 1]);
+            Sel sa[4], sb[4];
+            sel16(sa, x[c]);
+            sel16(sb, x[c + 1]);
+            gf_mac16x2(acc, sa, sb, tr + c * QFEC_TAB_STRIDE, tr + (c + 1) * QFEC_TAB_STRIDE);
+        }
+        if (K & 1) {
+            pin16(x[K - 1]);
+            Sel sl[4];
+            sel16(sl, x[K - 1]);
+            gf_mac16(acc, sl, tr + (K - 1) * QFEC_TAB_STRIDE);
+        }
+        st16(dst + (uint64_t)r * a.pitch, acc);
+    }
 }
 
 // runtime k, m: output rows in chunks of RCH; the k input rows are re-read per chunk
@@ -294,60 +342,137 @@ __device__ __forceinline__ int group_record(const ReconArgs& a, uint64_t g, int 
     return __builtin_amdgcn_readfirstlane(rec);
 }
 
+// One 16-B column of a group's reconstruct.  The K survivor loads are issued together;
+// the e output rows are then produced one at a time (runtime, wave-uniform loop), so only
+// one accumulator and one pair of selector sets are live: ~90 VGPRs, and no work is spent
+// on the M - e rows a group does not need.  The row's coefficient tables are scalar loads.
 template <int K, int M>
-__global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t g = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (g >= a.groups) return;
-    const int rec = group_record(a, g, lane);
-    if (rec < 0) {
-        if (rec == QFEC_REC_FAIL && lane == 0 && a.failed) atomicAdd(a.failed, 1u);
-        return;
-    }
-    const uint32_t* __restrict__ r = a.records + rec;
-    const int e = (int)r[0];
-    const uint32_t* surv = r + a.surv_off;
-    const uint32_t* lost = r + a.lost_off;
-    const uint32_t* tab = r + a.hdr;
-
-    const uint8_t* src[K];
+__device__ __forceinline__ void recon_column(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
+                                             uint64_t lost_bits, const uint32_t* __restrict__ tab, int e,
+                                             uint64_t pitch, uint64_t off) {
+    uint4 x[K];
 #pragma unroll
-    for (int c = 0; c < K; ++c) src[c] = shard_ptr(a, g, surv[c]);
-    uint8_t* dst[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) dst[j] = a.data + (g * (uint64_t)K + (j < e ? lost[j] : 0)) * a.pitch;
-
-    for (uint32_t col = lane; col < (uint32_t)a.cols; col += 64) {
-        const uint64_t off = (uint64_t)col * 16u;
-        uint4 x[K];
-#pragma unroll
-        for (int c = 0; c < K; ++c) x[c] = ld16(src[c] + off);
-        uint4 acc[M];
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-            acc[j] = make_uint4(0, 0, 0, 0);
-            if (j < e && tab[(j * K) * QFEC_TAB_STRIDE + 5]) acc[j] = *reinterpret_cast<const uint4*>(dst[j] + off);
-        }
+    for (int c = 0; c < K; ++c) x[c] = ld16(src[c] + off);
+    for (int j = 0; j < e; ++j) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(lost_bits);
+        lost_bits &= lost_bits - 1;
+        uint8_t* dst = data_g + (uint64_t)l * pitch + off;
+        const uint32_t* tj = tab + j * K * QFEC_TAB_STRIDE;
+        uint4 acc = make_uint4(0, 0, 0, 0);
+        if (tj[5]) acc = *reinterpret_cast<const uint4*>(dst);  // rs.c column-0 quirk
 #pragma unroll
         for (int c = 0; c + 1 < K; c += 2) {
+            // opaque to LICM: re-form the selectors per row instead of keeping all K
+            // inputs' selector words (3x the input registers) live across the row loop
+            pin16(x[c]);
+            pin16(x[c + 1]);
             Sel sa[4], sb[4];
             sel16(sa, x[c]);
             sel16(sb, x[c + 1]);
-#pragma unroll
-            for (int j = 0; j < M; ++j)
-                if (j < e)
-                    gf_mac16x2(acc[j], sa, sb, tab + (j * K + c) * QFEC_TAB_STRIDE, tab + (j * K + c + 1) * QFEC_TAB_STRIDE);
+            gf_mac16x2(acc, sa, sb, tj + c * QFEC_TAB_STRIDE, tj + (c + 1) * QFEC_TAB_STRIDE);
         }
         if (K & 1) {
-            Sel s[4];
-            sel16(s, x[K - 1]);
-#pragma unroll
-            for (int j = 0; j < M; ++j)
-                if (j < e) gf_mac16(acc[j], s, tab + (j * K + K - 1) * QFEC_TAB_STRIDE);
+            pin16(x[K - 1]);
+            Sel sl[4];
+            sel16(sl, x[K - 1]);
+            gf_mac16(acc, sl, tj + (K - 1) * QFEC_TAB_STRIDE);
         }
+        st16(dst, acc);
+    }
+}
+
+// Variant (tuning "recon_impl" = 1): all M rows computed at once, selectors formed once
+// per input and shared by the rows; more registers (2-3 waves/SIMD), fewer VALU ops.
+template <int K, int M>
+__device__ __forceinline__ void recon_column_allrows(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
+                                                     uint64_t lost_bits, const uint32_t* __restrict__ tab, int e,
+                                                     uint64_t pitch, uint64_t off) {
+    uint4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = ld16(src[c] + off);
+    uint8_t* dst[M];
+    uint4 acc[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        uint32_t l = 0;
+        if (j < e) {
+            l = (uint32_t)__builtin_ctzll(lost_bits);
+            lost_bits &= lost_bits - 1;
+        }
+        dst[j] = data_g + (uint64_t)l * pitch + off;
+        acc[j] = make_uint4(0, 0, 0, 0);
+        if (j < e && tab[(j * K) * QFEC_TAB_STRIDE + 5]) acc[j] = *reinterpret_cast<const uint4*>(dst[j]);
+    }
+#pragma unroll
+    for (int c = 0; c + 1 < K; c += 2) {
+        Sel sa[4], sb[4];
+        sel16(sa, x[c]);
+        sel16(sb, x[c + 1]);
 #pragma unroll
         for (int j = 0; j < M; ++j)
-            if (j < e) st16(dst[j] + off, acc[j]);
+            gf_mac16x2(acc[j], sa, sb, tab + (j * K + c) * QFEC_TAB_STRIDE, tab + (j * K + c + 1) * QFEC_TAB_STRIDE);
+    }
+    if (K & 1) {
+        Sel sl[4];
+        sel16(sl, x[K - 1]);
+#pragma unroll
+        for (int j = 0; j < M; ++j) gf_mac16(acc[j], sl, tab + (j * K + K - 1) * QFEC_TAB_STRIDE);
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+        if (j < e) st16(dst[j], acc[j]);
+}
+
+// LUT mode, compile-time K, M.  The survivor set follows from the erasure mask alone --
+// it is the lowest K non-erased shard ids (all surviving data, then the first e surviving
+// parity rows: module/rs.c:620-629) -- so the shard loads issue right after the ballot,
+// while the decode record (coefficients only) is still in flight.
+// ONE_PASS: block_size <= 1 KiB, one 16-B column per lane, no column loop.
+template <int K, int M, bool ONE_PASS, bool ALLROWS>
+__global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
+                                                          const uint8_t* __restrict__ parity,
+                                                          const uint8_t* __restrict__ marks,
+                                                          const int32_t* __restrict__ lut,
+                                                          const uint32_t* __restrict__ records) {
+    // __restrict__ parameters: the LUT and records are provably not written by this
+    // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
+    constexpr int N = K + M;
+    const int lane = threadIdx.x & 63;
+    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (g >= a.groups) return;
+    uint32_t mk = 0;
+    if (lane < K) mk = marks[g * K + lane];
+    else if (lane < N) mk = marks[a.groups * K + g * M + (lane - K)];
+    const uint64_t mask = __ballot(mk != 0) & ((1ull << N) - 1ull);
+    const uint64_t lost_bits = mask & ((1ull << K) - 1ull);
+    const int e = __builtin_popcountll(lost_bits);
+    if (e == 0) return;
+    uint64_t avail = ~mask & ((1ull << N) - 1ull);
+    if (__builtin_popcountll(avail) < K) {
+        if (lane == 0 && a.failed) atomicAdd(a.failed, 1u);
+        return;
+    }
+    const int rec = __builtin_amdgcn_readfirstlane(lut[mask]);
+    const uint32_t* tab = records + rec + a.hdr;
+    const uint64_t pitch = a.pitch;
+    uint8_t* data_g = data + g * K * pitch;
+    const uint8_t* src[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const uint32_t s = (uint32_t)__builtin_ctzll(avail);
+        avail &= avail - 1;
+        src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : parity + (g * M + (s - K)) * pitch;
+    }
+    if (ONE_PASS) {
+        if (lane < (int)a.cols) {
+            if (ALLROWS) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)lane * 16u);
+            else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)lane * 16u);
+        }
+    } else {
+        for (uint32_t col = lane; col < (uint32_t)a.cols; col += 64) {
+            if (ALLROWS) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+            else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+        }
     }
 }
 
@@ -463,10 +588,13 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
     return (unsigned)((work + block - 1) / block);
 }
 
-#define QFEC_ENC_CASE(KK, MM)                                                            \
-    if (a.k == KK && a.m == MM) {                                                        \
-        hipLaunchKernelGGL((k_encode_perm<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
-        return hipGetLastError();                                                        \
+#define QFEC_ENC_CASE(KK, MM)                                                                 \
+    if (a.k == KK && a.m == MM) {                                                             \
+        if (a.impl == 1)                                                                      \
+            hipLaunchKernelGGL((k_encode_perm_rows<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_encode_perm<KK, MM>), dim3(grid), dim3(256), 0, stream, a);  \
+        return hipGetLastError();                                                             \
     }
 
 hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
@@ -500,10 +628,21 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
     return hipGetLastError();
 }
 
-#define QFEC_REC_CASE(KK, MM)                                                                 \
-    if (a.k == KK && a.m == MM) {                                                             \
-        hipLaunchKernelGGL((k_reconstruct_perm<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
-        return hipGetLastError();                                                             \
+#define QFEC_REC_LAUNCH(KK, MM, OP, AR)                                                                  \
+    hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, OP, AR>), dim3(grid), dim3(256), 0, stream, a, a.data, a.parity, \
+                       a.marks, a.lut, a.records)
+
+#define QFEC_REC_CASE(KK, MM)                                                  \
+    if (a.k == KK && a.m == MM) {                                              \
+        const bool op = a.cols <= 64;                                          \
+        /* auto: all rows at once while the register budget allows (measured: */ \
+        /* (10,3) 5.69 vs 5.31 TB/s; (16,4) 1.31 vs 3.01 TB/s, tools/ab.py)   */ \
+        const bool ar = a.impl < 0 ? (KK * MM <= 30) : a.impl == 1;           \
+        if (op && ar) QFEC_REC_LAUNCH(KK, MM, true, true);                     \
+        else if (op) QFEC_REC_LAUNCH(KK, MM, true, false);                     \
+        else if (ar) QFEC_REC_LAUNCH(KK, MM, false, true);                     \
+        else QFEC_REC_LAUNCH(KK, MM, false, false);                            \
+        return hipGetLastError();                                              \
     }
 
 hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
@@ -511,6 +650,10 @@ hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
     const unsigned grid = grid_for(a.groups, 4);
     if (!a.vec16) {
         hipLaunchKernelGGL((k_reconstruct_any<false>), dim3(grid), dim3(256), 0, stream, a);
+        return hipGetLastError();
+    }
+    if (a.group_rec) {  // explicit (host-record) mode: survivors come from the record
+        hipLaunchKernelGGL((k_reconstruct_any<true>), dim3(grid), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
     QFEC_REC_CASE(10, 3)

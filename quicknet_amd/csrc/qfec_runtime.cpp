@@ -309,6 +309,7 @@ int ensure_lut(qfec_code* c, int dev, DevTables** out) {
         auto it = off_of.find(key);
         if (it != off_of.end()) { lut[mask] = it->second; continue; }
         if (record_for_key(c, key, one) <= 0) { lut[mask] = QFEC_REC_FAIL; continue; }
+        one.resize(record_layout(k, m).words(m, k), 0);  // pad to m rows (branch-free kernel)
         const int32_t off = (int32_t)recs.size();
         recs.insert(recs.end(), one.begin(), one.end());
         off_of.emplace(key, off);
@@ -342,6 +343,7 @@ int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, cons
     a.m = m;
     a.pitch = (uint64_t)pitch;
     a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
+    a.impl = tuning().encode_impl;
     a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
     a.cols_div = make_div_magic(a.cols);
     const long long per = std::max<long long>(1, (long long)(0x7FFFFFFFll / a.cols));
@@ -359,7 +361,6 @@ int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, cons
 int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const int32_t* group_rec,
                     const uint32_t* recs, uint8_t* d_data, const uint8_t* d_par, const uint8_t* d_marks,
                     long long groups, int block, long long pitch, unsigned* d_failed, hipStream_t s) {
-    (void)ctx;
     ReconArgs a{};
     const RecordLayout L = record_layout(c->k, c->m);
     a.data = d_data;
@@ -378,6 +379,7 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.hdr = L.hdr;
     a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
     a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
+    a.impl = tuning().recon_impl;
     hipError_t e = launch_reconstruct(a, s);
     if (e != hipSuccess) return hip_fail(e, "reconstruct kernel launch");
     return QFEC_OK;
@@ -473,6 +475,15 @@ int qfec_set_kernel_variant(int v) {
 }
 
 int qfec_get_kernel_variant(void) { return g_variant.load(); }
+
+// experiment knobs, for A/B timing in one process (tools/ab.py); not needed in production
+int qfec_tune(const char* key, int value) {
+    if (!key) return QFEC_EINVAL;
+    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 1) { tuning().recon_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
+    set_error("qfec_tune: unknown key/value %s=%d", key, value);
+    return QFEC_EINVAL;
+}
 
 qfec_code* qfec_code_new(int flavour, int k, int m) {
     std::vector<uint8_t> rows;

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of kernel variants in ONE process (cdna_hip_programming.md
+section 5.4 rule 24): every round times each variant back to back on the same buffers, so
+device-to-device and run-to-run drift does not masquerade as a kernel difference.
+
+  python tools/ab.py [--rounds 12] [--reps 10] [--k 10 --m 3 --block 1024 --groups 100000]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import quicknet_amd as qa  # noqa: E402
+from quicknet_amd.synth import erasure_marks, marks_to_rs_layout  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--rounds", type=int, default=12)
+    p.add_argument("--reps", type=int, default=10)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--m", type=int, default=3)
+    p.add_argument("--block", type=int, default=1024)
+    p.add_argument("--groups", type=int, default=100_000)
+    p.add_argument("--erasures", type=int, default=3)
+    a = p.parse_args()
+    k, m, B, G = a.k, a.m, a.block, a.groups
+    dev = torch.device("cuda:0")
+    pitch = (B + 15) // 16 * 16
+    code = qa.Code.cauchy(k, m)
+    data = torch.empty((G, k, pitch), dtype=torch.uint8, device=dev)
+    qa.synth_fill(data, 0x5EED0002)
+    par = torch.empty((G, m, pitch), dtype=torch.uint8, device=dev)
+    gm = erasure_marks(0x5EED0003, G, k + m, a.erasures)
+    marks = torch.from_numpy(marks_to_rs_layout(gm, k)).to(dev)
+    work = data.clone()
+    code.encode(data, par, B)
+    code.prepare_reconstruct()
+    dec_groups = int((gm[:, :k].sum(1) > 0).sum())
+    enc_bytes = (k + m) * B * G
+    dec_bytes = (k * dec_groups + int(gm[:, :k].sum())) * B
+    ref_par = par.clone()
+
+    def enc():
+        code.encode(data, par, B)
+
+    def rec():
+        code.reconstruct(work, par, marks, B)
+
+    def probe():
+        qa.probe_stream(data, par, B)
+
+    variants = [
+        ("encode impl0 (all rows)", lambda: qa.tune("encode_impl", 0), enc, enc_bytes),
+        ("encode impl1 (row loop)", lambda: qa.tune("encode_impl", 1), enc, enc_bytes),
+        ("encode ldslog", lambda: (qa.tune("encode_impl", 0), qa.set_kernel_variant(1)), enc, enc_bytes),
+        ("probe xor (traffic only)", lambda: None, probe, enc_bytes),
+        ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
+        ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
+    ]
+    times = {v[0]: [] for v in variants}
+    s = torch.cuda.current_stream()
+    for r in range(a.rounds):
+        for name, setup, fn, _ in variants:
+            qa.set_kernel_variant(0)
+            setup()
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(a.reps):
+                fn()
+            e1.record(s)
+            torch.cuda.synchronize()
+            times[name].append(e0.elapsed_time(e1) / a.reps)
+    qa.set_kernel_variant(0)
+    qa.tune("encode_impl", 0)
+    qa.tune("recon_impl", 0)
+    code.encode(data, par, B)
+    torch.cuda.synchronize()
+    assert torch.equal(par, ref_par)
+    print(f"RS({k},{m}) B={B} G={G}: {a.rounds} interleaved rounds x {a.reps} launches")
+    for name, _, _, nbytes in variants:
+        t = times[name]
+        med, mn = statistics.median(t), min(t)
+        print(f"  {name:28s} median {med*1e3:8.1f} us  min {mn*1e3:8.1f} us  -> {nbytes/(med*1e-3)/1e9:7.1f} GB/s "
+              f"(best {nbytes/(mn*1e-3)/1e9:7.1f})")
+
+
+if __name__ == "__main__":
+    main()
