@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from rocprofv3 PMC counters (MI355X_MICROARCH.md, HBM section).
+
+Two separate counter passes over the same bench workload (FETCH_SIZE and WRITE_SIZE do not
+fit one pass on gfx950), each its own `rocprofv3 --pmc` run with no tracing domains.
+Corrections per the guide: FETCH_SIZE reads exactly half the bytes of a wide coalesced
+streaming read on gfx950, so reads = 2 * FETCH_SIZE; WRITE_SIZE is exact for 16-B/lane
+streaming stores.  Both counters are in KiB.  The XOR probe kernel (known bytes) is
+profiled in the same run as a calibration check.
+
+Writes profiles/traffic.json (read by bench.py as roofline.traffic) and the raw CSVs to
+the output directory.  Run on the GPU box:
+    python tools/pmc_traffic.py --out gpurun_out/pmc
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"encode": "k_encode_perm<", "reconstruct": "k_reconstruct_perm<", "probe": "k_probe_xor"}
+
+
+def run_pass(counter, out, bench_args):
+    d = os.path.abspath(os.path.join(out, counter.lower()))
+    os.makedirs(d, exist_ok=True)
+    cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", counter.lower(), "--",
+           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu"] + bench_args
+    env = dict(os.environ, TMPDIR="/tmp")
+    with open(os.path.join(d, "run.log"), "w") as log:
+        subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=env, cwd="/tmp", timeout=600)
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise RuntimeError(f"no counter_collection.csv under {d}")
+    per = {k: [] for k in KERNELS}
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                name = row.get("Kernel_Name", "")
+                for key, pat in KERNELS.items():
+                    if pat in name:
+                        per[key].append(float(row["Counter_Value"]))
+    return per
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc"))
+    p.add_argument("--json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--m", type=int, default=3)
+    p.add_argument("--block", type=int, default=1024)
+    p.add_argument("--groups", type=int, default=100_000)
+    a = p.parse_args()
+    bench_args = ["--steps", "5", "--warmup", "1", "--k", str(a.k), "--m", str(a.m), "--block", str(a.block),
+                  "--groups", str(a.groups)]
+    fetch = run_pass("FETCH_SIZE", a.out, bench_args)
+    write = run_pass("WRITE_SIZE", a.out, bench_args)
+    k, m, B, G = a.k, a.m, a.block, a.groups
+    probe_alg_read, probe_alg_write = k * B * G, m * B * G
+    res = {}
+    for key in KERNELS:
+        if not fetch[key] or not write[key]:
+            continue
+        f = sum(fetch[key]) / len(fetch[key])
+        w = sum(write[key]) / len(write[key])
+        res[key] = {"fetch_kib_raw": f, "write_kib_raw": w, "read_bytes": 2 * f * 1024, "write_bytes": w * 1024,
+                    "bytes_per_launch": 2 * f * 1024 + w * 1024, "launches": len(fetch[key])}
+    if "probe" in res:
+        res["probe"]["algorithmic_read"] = probe_alg_read
+        res["probe"]["algorithmic_write"] = probe_alg_write
+    key = f"rs{k}_{m}_b{B}_g{G}"
+    doc = {}
+    if os.path.exists(a.json):
+        with open(a.json) as fh:
+            doc = json.load(fh)
+    doc[key] = {
+        "encode_bytes_per_launch": res.get("encode", {}).get("bytes_per_launch"),
+        "reconstruct_bytes_per_launch": res.get("reconstruct", {}).get("bytes_per_launch"),
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes = 2*FETCH_SIZE*1024 "
+                  "+ WRITE_SIZE*1024 (gfx950 corrections, MI355X_MICROARCH.md HBM section)",
+        "raw": res,
+    }
+    os.makedirs(os.path.dirname(a.json), exist_ok=True)
+    with open(a.json, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(json.dumps(doc[key], indent=1))
+
+
+if __name__ == "__main__":
+    main()
