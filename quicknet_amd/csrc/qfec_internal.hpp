@@ -61,6 +61,7 @@ struct ReconArgs {
     int surv_off, lost_off, hdr;
     int vec16;
     int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once
+    uint32_t wpg;             // waves per group = ceil(cols / 64) (vec16 LUT kernels)
 };
 
 // runtime tuning knobs (qfec_tune); defaults are the measured best

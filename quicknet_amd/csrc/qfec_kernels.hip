@@ -427,8 +427,9 @@ __device__ __forceinline__ void recon_column_allrows(const uint8_t* const (&src)
 // it is the lowest K non-erased shard ids (all surviving data, then the first e surviving
 // parity rows: module/rs.c:620-629) -- so the shard loads issue right after the ballot,
 // while the decode record (coefficients only) is still in flight.
-// ONE_PASS: block_size <= 1 KiB, one 16-B column per lane, no column loop.
-template <int K, int M, bool ONE_PASS, bool ALLROWS>
+// One wave per 64 16-B columns of a group: a group of `cols` columns gets
+// wpg = ceil(cols / 64) waves (B = 1400 -> 2), all in flight together, no column loop.
+template <int K, int M, bool ALLROWS>
 __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ parity,
                                                           const uint8_t* __restrict__ marks,
@@ -438,7 +439,10 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
-    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t wpg = a.wpg;
+    const uint64_t g = wid / wpg;
+    const uint32_t part = wid - (uint32_t)g * wpg;
     if (g >= a.groups) return;
     uint32_t mk = 0;
     if (lane < K) mk = marks[g * K + lane];
@@ -449,7 +453,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     if (e == 0) return;
     uint64_t avail = ~mask & ((1ull << N) - 1ull);
     if (__builtin_popcountll(avail) < K) {
-        if (lane == 0 && a.failed) atomicAdd(a.failed, 1u);
+        if (part == 0 && lane == 0 && a.failed) atomicAdd(a.failed, 1u);
         return;
     }
     const int rec = __builtin_amdgcn_readfirstlane(lut[mask]);
@@ -463,16 +467,10 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
         avail &= avail - 1;
         src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : parity + (g * M + (s - K)) * pitch;
     }
-    if (ONE_PASS) {
-        if (lane < (int)a.cols) {
-            if (ALLROWS) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)lane * 16u);
-            else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)lane * 16u);
-        }
-    } else {
-        for (uint32_t col = lane; col < (uint32_t)a.cols; col += 64) {
-            if (ALLROWS) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
-            else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
-        }
+    const uint32_t col = part * 64u + lane;
+    if (col < a.cols) {
+        if (ALLROWS) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+        else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
     }
 }
 
@@ -628,20 +626,17 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
     return hipGetLastError();
 }
 
-#define QFEC_REC_LAUNCH(KK, MM, OP, AR)                                                                  \
-    hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, OP, AR>), dim3(grid), dim3(256), 0, stream, a, a.data, a.parity, \
+#define QFEC_REC_LAUNCH(KK, MM, AR)                                                                  \
+    hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR>), dim3(pgrid), dim3(256), 0, stream, a, a.data, a.parity, \
                        a.marks, a.lut, a.records)
 
 #define QFEC_REC_CASE(KK, MM)                                                  \
     if (a.k == KK && a.m == MM) {                                              \
-        const bool op = a.cols <= 64;                                          \
         /* auto: all rows at once while the register budget allows (measured: */ \
         /* (10,3) 5.69 vs 5.31 TB/s; (16,4) 1.31 vs 3.01 TB/s, tools/ab.py)   */ \
         const bool ar = a.impl < 0 ? (KK * MM <= 30) : a.impl == 1;           \
-        if (op && ar) QFEC_REC_LAUNCH(KK, MM, true, true);                     \
-        else if (op) QFEC_REC_LAUNCH(KK, MM, true, false);                     \
-        else if (ar) QFEC_REC_LAUNCH(KK, MM, false, true);                     \
-        else QFEC_REC_LAUNCH(KK, MM, false, false);                            \
+        if (ar) QFEC_REC_LAUNCH(KK, MM, true);                                 \
+        else QFEC_REC_LAUNCH(KK, MM, false);                                   \
         return hipGetLastError();                                              \
     }
 
@@ -656,6 +651,9 @@ hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
         hipLaunchKernelGGL((k_reconstruct_any<true>), dim3(grid), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
+    const uint64_t waves = a.groups * (uint64_t)a.wpg;
+    if (waves > 0xFFFFFFFFull) return hipErrorInvalidValue;  // caller chunks batches
+    const unsigned pgrid = grid_for(waves, 4);
     QFEC_REC_CASE(10, 3)
     QFEC_REC_CASE(16, 4)
     QFEC_REC_CASE(4, 2)

@@ -380,6 +380,7 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
     a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
     a.impl = tuning().recon_impl;
+    a.wpg = (a.cols + 63) / 64;
     hipError_t e = launch_reconstruct(a, s);
     if (e != hipSuccess) return hip_fail(e, "reconstruct kernel launch");
     return QFEC_OK;

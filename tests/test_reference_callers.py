@@ -1,0 +1,161 @@
+"""Drop-in check at the reference's own call sites.
+
+The reference's codec callers -- network/FecCodec.cpp and network/FecCodecBuf.cpp, compiled
+UNCHANGED from /root/reference by `make -C oracle ref` -- are linked twice:
+  oracle/_ref/libref_feccodec_ref.so   against the reference's system/fec.c
+  oracle/_ref/libref_feccodec_qfec.so  against libqfec.so (the product, HIP kernels)
+The same packet stream is pushed through both, the way network/NetFecCodec.cpp drives them
+(zfec_pack_input: set_fec_enc_buf -> pack_fec_head, get_fec_encoded_pkt for ik = k..n-1;
+zfec_unpack_input: unpack_fec_head -> set_fec_dec_buf for the first k valid in group order ->
+fec_decode_pkts -> get_fec_decoded_pkt -> dec_src_pkt_info), and every wire byte and every
+recovered payload must match.  Skipped where oracle/_ref was not built.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+REF_DIR = os.path.join(ROOT, "oracle", "_ref")
+LIBS = {"ref": os.path.join(REF_DIR, "libref_feccodec_ref.so"), "qfec": os.path.join(REF_DIR, "libref_feccodec_qfec.so")}
+
+if not all(os.path.exists(p) for p in LIBS.values()):
+    pytest.skip("oracle/_ref caller builds absent (built only where /root/reference exists)", allow_module_level=True)
+
+
+class FecCodecBufS(C.Structure):  # network/FecCodecBuf.h:19-36
+    _fields_ = [("enc_pkt_size", C.c_int), ("enc_kmax", C.c_int), ("is_checksum", C.c_bool),
+                ("is_send_checksum", C.c_bool), ("fec_en_buf", C.c_void_p), ("sent_buf", C.c_void_p),
+                ("en_check_pkt", C.c_void_p), ("dec_pkt_size", C.c_int), ("dec_kmax", C.c_int),
+                ("fecDecoderBuf", C.c_void_p), ("fecDecoderIndices", C.c_void_p), ("dec_buf", C.c_void_p),
+                ("dec_check_pkt", C.c_void_p)]
+
+
+class FecCodecHead(C.Structure):  # network/FecCodecBuf.h:10-17
+    _fields_ = [("sent_pkt_index", C.c_uint32), ("src_pkt_index", C.c_uint32), ("codec_n", C.c_ubyte),
+                ("codec_k", C.c_ubyte), ("ik", C.c_ubyte)]
+
+
+def load(kind):
+    L = C.CDLL(LIBS[kind])
+    P, vp, i, ip = C.POINTER(FecCodecBufS), C.c_void_p, C.c_int, C.POINTER(C.c_int)
+    L.init_fec_buf.argtypes = [P, i, i]
+    L.release_fec_buf.argtypes = [P]
+    L.set_fec_enc_buf.argtypes = [P, i, vp, i, ip]
+    L.set_fec_enc_buf.restype = vp
+    L.get_fec_encoded_pkt.argtypes = [P, vp, i, i, ip]
+    L.get_fec_encoded_pkt.restype = vp
+    L.pack_fec_head.argtypes = [P, C.POINTER(FecCodecHead), vp, i, ip]
+    L.pack_fec_head.restype = vp
+    L.unpack_fec_head.argtypes = [P, C.POINTER(FecCodecHead), vp, i, ip]
+    L.unpack_fec_head.restype = vp
+    L.set_fec_dec_buf.argtypes = [P, i, vp, i, i]
+    L.set_fec_dec_buf.restype = vp
+    L.reset_fec_dec_buf.argtypes = [P]
+    L.fec_decode_pkts.argtypes = [P, vp, i]
+    L.get_fec_decoded_pkt.argtypes = [P, i]
+    L.get_fec_decoded_pkt.restype = vp
+    L.dec_src_pkt_info.argtypes = [vp, P, C.POINTER(C.c_uint16)]
+    L.dec_src_pkt_info.restype = vp
+    if kind == "ref":
+        L.fec_new.restype = vp
+        L.fec_new.argtypes = [i, i]
+        L.fec_free.argtypes = [vp]
+        new, free = L.fec_new, L.fec_free
+    else:
+        import quicknet_amd
+        Q = quicknet_amd.lib()  # the very libqfec.so the callers resolved fec_* to
+        new, free = Q.fec_new, Q.fec_free
+    return L, new, free
+
+
+def run_stream(kind, k, n, payloads, lost):
+    """One group through the caller layer: returns (wire packets, recovered payloads)."""
+    L, fec_new, fec_free = load(kind)
+    S, R = FecCodecBufS(), FecCodecBufS()
+    L.init_fec_buf(C.byref(S), 2048, 16)
+    L.init_fec_buf(C.byref(R), 2048, 16)
+    S.is_send_checksum = True  # init_zfec_layer (NetFecCodec.cpp:617)
+    codec = fec_new(k, n)
+    wire, en = [], C.c_int()
+    group_max = 0
+    for ik, pl in enumerate(payloads):  # zfec_pack_input source branch (NetFecCodec.cpp:100-132)
+        p = L.set_fec_enc_buf(C.byref(S), ik, pl.ctypes.data, len(pl), C.byref(en))
+        group_max = en.value if ik == 0 else max(group_max, en.value)
+        h = FecCodecHead(ik, ik, n, k, ik)
+        out = C.c_int()
+        q = L.pack_fec_head(C.byref(S), C.byref(h), p, en.value, C.byref(out))
+        wire.append(C.string_at(q, out.value))
+    for ik in range(k, n):  # check packets (NetFecCodec.cpp:133-166)
+        p = L.get_fec_encoded_pkt(C.byref(S), codec, ik, group_max, C.byref(en))
+        h = FecCodecHead(ik, k - 1, n, k, ik)
+        out = C.c_int()
+        q = L.pack_fec_head(C.byref(S), C.byref(h), p, en.value, C.byref(out))
+        wire.append(C.string_at(q, out.value))
+    # receive side: unpack every surviving datagram, keep the first k valid in group order
+    got = []
+    for ik, w in enumerate(wire):
+        if ik in lost:
+            continue
+        h = FecCodecHead()
+        un = C.c_int()
+        buf = np.frombuffer(w, dtype=np.uint8).copy()
+        q = L.unpack_fec_head(C.byref(R), C.byref(h), buf.ctypes.data, len(w), C.byref(un))
+        assert q and h.ik == ik and h.codec_k == k and h.codec_n == n
+        got.append((ik, C.string_at(q, un.value)))
+    L.reset_fec_dec_buf(C.byref(R))
+    max_size = 0
+    for v, (ik, shard) in enumerate(got[:k]):  # add_packet_fec_buf (NetFecCodec.cpp:504-528)
+        b = np.frombuffer(shard, dtype=np.uint8).copy()
+        assert L.set_fec_dec_buf(C.byref(R), v, b.ctypes.data, len(shard), ik)
+        max_size = max(max_size, len(shard))
+    rec = []
+    if any(i < k for i in lost):
+        assert L.fec_decode_pkts(C.byref(R), codec, max_size) == 0
+        for i in range(k):
+            d = L.get_fec_decoded_pkt(C.byref(R), i)
+            sz = C.c_uint16()
+            src = L.dec_src_pkt_info(d, C.byref(R), C.byref(sz))
+            rec.append(C.string_at(src, sz.value) if src else None)
+    fec_free(codec)
+    L.release_fec_buf(C.byref(S))
+    L.release_fec_buf(C.byref(R))
+    return wire, rec
+
+
+CASES = [(4, 5, [1]), (4, 6, [0, 3]), (3, 5, [0, 1]), (5, 8, [1, 2, 4]), (7, 8, [6]), (10, 13, [0, 5, 9]),
+         (2, 4, [0, 1]), (10, 13, [2, 10])]
+
+
+def _payloads(k, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, int(rng.integers(1, 1400)), dtype=np.uint8) for _ in range(k)]
+
+
+def test_reference_callers_roundtrip_cpu():
+    """Harness sanity on CPU: the reference callers + reference fec.c recover the payloads."""
+    for t, (k, n, lost) in enumerate(CASES):
+        pls = _payloads(k, t)
+        wire, rec = run_stream("ref", k, n, pls, set(lost))
+        assert len(wire) == n
+        for i in range(k):
+            if i in lost:
+                assert rec[i] == pls[i].tobytes()
+
+
+@pytest.mark.gpu
+def test_reference_callers_on_libqfec_match_reference():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    for t, (k, n, lost) in enumerate(CASES):
+        pls = _payloads(k, 100 + t)
+        w_ref, r_ref = run_stream("ref", k, n, pls, set(lost))
+        w_q, r_q = run_stream("qfec", k, n, pls, set(lost))
+        assert w_ref == w_q, (k, n)  # every wire byte, incl. parity packets and checksums
+        assert r_ref == r_q, (k, n)
+        for i in lost:
+            if i < k:
+                assert r_q[i] == pls[i].tobytes()
