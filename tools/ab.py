@@ -28,6 +28,7 @@ def main():
     p.add_argument("--block", type=int, default=1024)
     p.add_argument("--groups", type=int, default=100_000)
     p.add_argument("--erasures", type=int, default=3)
+    p.add_argument("--pairs", action="store_true", help="time reconstruct right after encode, as bench.py does")
     a = p.parse_args()
     k, m, B, G = a.k, a.m, a.block, a.groups
     dev = torch.device("cuda:0")
@@ -55,6 +56,9 @@ def main():
     def probe():
         qa.probe_stream(data, par, B)
 
+    def pair_enc():  # bench.py's order: reconstruct right after an encode
+        code.encode(data, par, B)
+
     variants = [
         ("encode impl0 (all rows)", lambda: qa.tune("encode_impl", 0), enc, enc_bytes),
         ("encode impl1 (row loop)", lambda: qa.tune("encode_impl", 1), enc, enc_bytes),
@@ -63,6 +67,8 @@ def main():
         ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
         ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
     ]
+    if a.pairs:
+        variants = []
     times = {v[0]: [] for v in variants}
     s = torch.cuda.current_stream()
     for r in range(a.rounds):
@@ -77,6 +83,26 @@ def main():
             e1.record(s)
             torch.cuda.synchronize()
             times[name].append(e0.elapsed_time(e1) / a.reps)
+    if a.pairs:
+        qa.tune("recon_impl", -1)
+        for gap_us in (0, 200):
+            te, tr = [], []
+            for r in range(a.rounds * a.reps):
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record(s)
+                enc()
+                e1.record(s)
+                if gap_us:
+                    torch.cuda._sleep(int(gap_us * 2000))  # ~cycles at ~2 GHz
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record(s)
+                rec()
+                e2.record(s)
+                torch.cuda.synchronize()
+                te.append(e0.elapsed_time(e1) if not gap_us else 0.0)
+                tr.append(e1.elapsed_time(e2))
+            med = statistics.median(tr)
+            print(f"  pair gap={gap_us:4d}us: reconstruct median {med*1e3:7.1f} us -> {dec_bytes/(med*1e-3)/1e9:7.1f} GB/s")
     qa.set_kernel_variant(0)
     qa.tune("encode_impl", 0)
     qa.tune("recon_impl", 0)
