@@ -85,24 +85,21 @@ def main():
             times[name].append(e0.elapsed_time(e1) / a.reps)
     if a.pairs:
         qa.tune("recon_impl", -1)
-        for gap_us in (0, 200):
-            te, tr = [], []
+        scratch = torch.empty_like(par)
+        befores = [("after encode", enc), ("after XOR probe (same traffic, light VALU)", lambda: qa.probe_stream(data, scratch, B)),
+                   ("after 200us sleep", lambda: torch.cuda._sleep(400000)), ("after reconstruct", rec)]
+        for label, before in befores:
+            tr = []
             for r in range(a.rounds * a.reps):
-                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-                e0.record(s)
-                enc()
+                e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
+                before()
                 e1.record(s)
-                if gap_us:
-                    torch.cuda._sleep(int(gap_us * 2000))  # ~cycles at ~2 GHz
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e1.record(s)
                 rec()
                 e2.record(s)
                 torch.cuda.synchronize()
-                te.append(e0.elapsed_time(e1) if not gap_us else 0.0)
                 tr.append(e1.elapsed_time(e2))
             med = statistics.median(tr)
-            print(f"  pair gap={gap_us:4d}us: reconstruct median {med*1e3:7.1f} us -> {dec_bytes/(med*1e-3)/1e9:7.1f} GB/s")
+            print(f"  reconstruct {label:44s} median {med*1e3:7.1f} us -> {dec_bytes/(med*1e-3)/1e9:7.1f} GB/s")
     qa.set_kernel_variant(0)
     qa.tune("encode_impl", 0)
     qa.tune("recon_impl", 0)

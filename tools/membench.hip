@@ -61,6 +61,29 @@ __global__ void __launch_bounds__(256) k_shape(const uint8_t* __restrict__ data,
     }
 }
 
+// store cache-policy variants through buffer stores (aux: 1 sc0, 2 nt, 16 sc1)
+template <int AUX>
+__global__ void __launch_bounds__(256) k_shape_aux(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
+                                                   uint64_t groups, uint32_t cols, uint64_t pitch) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t g = t / cols;
+    if (g >= groups) return;
+    const uint32_t col = (uint32_t)(t - g * cols);
+    const u32x4* src = (const u32x4*)(data + g * 10 * pitch + col * 16u);
+    u32x4 x[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) x[c] = __builtin_nontemporal_load(src + c * (pitch / 16));
+    u32x4 acc = x[0];
+#pragma unroll
+    for (int c = 1; c < 10; ++c) acc ^= x[c];
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(par + g * 3 * pitch, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        __builtin_amdgcn_raw_buffer_store_b128(acc, rs, (int)(r * pitch + col * 16u), 0, AUX);
+        acc.x += 1;
+    }
+}
+
 // grid-stride persistent version
 template <int K, int M, int NT_LD>
 __global__ void __launch_bounds__(256) k_shape_gs(const uint8_t* __restrict__ data, uint8_t* __restrict__ par,
@@ -161,6 +184,56 @@ int main() {
     rep("write-only nt 1.2GB grid 4096", time_ms([&] { k_write_nt<<<4096, 256>>>((u32x4*)p, pbytes * 4 / 16); }, R), (double)pbytes * 4);
     rep("copy nt 512MB 1 elem/thread", time_ms([&] { k_copy_nt<<<(unsigned)((n16 + 255) / 256), 256>>>((const u32x4*)d, (u32x4*)p, n16); }, R), 2.0 * n16 * 16);
     rep("shape nt-ld nt-st 256 thr (again)", time_ms([&] { k_shape<10, 3, 1, 1, 1><<<grid1, 256>>>(d, p, G, cols, B); }, R), alg);
+    // what the NEXT kernel pays after each store flavour (bench.py runs reconstruct right after encode)
+    {
+        hipEvent_t e0, e1, e2;
+        CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1)); CHECK(hipEventCreate(&e2));
+        auto pair = [&](const char* nm, auto kfn) {
+            double tw = 0, tr = 0;
+            for (int i = 0; i < 12; ++i) {
+                CHECK(hipEventRecord(e0, 0));
+                kfn();
+                CHECK(hipEventRecord(e1, 0));
+                k_read<<<4096, 256>>>((const u32x4*)d, dbytes / 16, flag);
+                CHECK(hipEventRecord(e2, 0));
+                CHECK(hipEventSynchronize(e2));
+                float a = 0, b = 0;
+                CHECK(hipEventElapsedTime(&a, e0, e1));
+                CHECK(hipEventElapsedTime(&b, e1, e2));
+                if (i >= 2) { tw += a; tr += b; }
+            }
+            printf("%-40s shape %7.1f us (%6.1f GB/s) | next read-only 1GB %7.1f us (%6.1f GB/s)\n", nm, tw / 10 * 1e3,
+                   alg / (tw / 10 * 1e-3) / 1e9, tr / 10 * 1e3, dbytes / (tr / 10 * 1e-3) / 1e9);
+        };
+        pair("store plain (aux 0)", [&] { k_shape_aux<0><<<grid1, 256>>>(d, p, G, cols, B); });
+        pair("store nt (aux 2)", [&] { k_shape_aux<2><<<grid1, 256>>>(d, p, G, cols, B); });
+        pair("store sc1 (aux 16)", [&] { k_shape_aux<16><<<grid1, 256>>>(d, p, G, cols, B); });
+        pair("store nt sc1 (aux 18)", [&] { k_shape_aux<18><<<grid1, 256>>>(d, p, G, cols, B); });
+        pair("store sc0 sc1 (aux 17)", [&] { k_shape_aux<17><<<grid1, 256>>>(d, p, G, cols, B); });
+        pair("store nt sc0 sc1 (aux 19)", [&] { k_shape_aux<19><<<grid1, 256>>>(d, p, G, cols, B); });
+        pair("read-only itself (baseline)", [&] { k_read<<<4096, 256>>>((const u32x4*)d, dbytes / 16, flag); });
+        // does reading the lines the previous kernel just wrote cost more?
+        double tw = 0, tr = 0, tr2 = 0;
+        for (int i = 0; i < 12; ++i) {
+            CHECK(hipEventRecord(e0, 0));
+            k_shape_aux<2><<<grid1, 256>>>(d, p, G, cols, B);
+            CHECK(hipEventRecord(e1, 0));
+            k_read<<<4096, 256>>>((const u32x4*)p, pbytes / 16, flag);
+            CHECK(hipEventRecord(e2, 0));
+            CHECK(hipEventSynchronize(e2));
+            float a = 0, b = 0;
+            CHECK(hipEventElapsedTime(&b, e1, e2));
+            k_read<<<4096, 256>>>((const u32x4*)(d + dbytes - pbytes), pbytes / 16, flag);
+            CHECK(hipEventRecord(e1, 0));
+            k_read<<<4096, 256>>>((const u32x4*)(p + pbytes), pbytes / 16, flag);
+            CHECK(hipEventRecord(e2, 0));
+            CHECK(hipEventSynchronize(e2));
+            CHECK(hipEventElapsedTime(&a, e1, e2));
+            if (i >= 2) { tr += b; tr2 += a; }
+        }
+        printf("after nt-store shape: read of the 307MB just written %7.1f us; read of 307MB not written %7.1f us\n",
+               tr / 10 * 1e3, tr2 / 10 * 1e3);
+    }
     rep("write-only 1.2GB grid 4096", time_ms([&] { k_write<<<4096, 256>>>((u32x4*)p, pbytes * 4 / 16); }, R), (double)pbytes * 4);
     return 0;
 }
