@@ -312,6 +312,100 @@ def gen_fec_decode(fec):
     np.savez_compressed(os.path.join(OUT, "fec_decode.npz"), **out)
 
 
+WIRE_CASES = [(4, 5), (4, 6), (3, 5), (5, 8), (7, 8), (10, 13), (2, 4), (3, 4), (14, 15), (1, 2)]
+
+
+def gen_wire():
+    """The FEC wire format, produced by the reference's own network/FecCodecBuf.cpp (built
+    unchanged into oracle/_ref/libref_feccodec_ref.so with system/fec.c): full groups sent
+    the way zfec_pack_input does (NetFecCodec.cpp:96-172), then every datagram -- and a
+    corrupted copy -- parsed by unpack_fec_head, source shards by dec_src_pkt_info, and one
+    lossy group decoded by fec_decode_pkts."""
+    sys.path.insert(0, ROOT)
+    from oracle.oracle import FecCodecBufS, FecCodecHead, load_callers
+    L = load_callers(os.path.join(HERE, "_ref", "libref_feccodec_ref.so"))
+    L.fec_new.restype = C.c_void_p
+    L.fec_new.argtypes = [C.c_int, C.c_int]
+    L.fec_free.argtypes = [C.c_void_p]
+    out = {}
+    gen = np.random.default_rng(0x31BE)
+    for (k, n), checksum in itertools.product(WIRE_CASES, (1, 0)):
+        G = 3
+        S = FecCodecBufS()
+        L.init_fec_buf(C.byref(S), 2048, 16)
+        S.is_send_checksum = bool(checksum)
+        codec = L.fec_new(k, n)
+        sizes = gen.integers(0, 2049, size=G * k).astype(np.int32)
+        if k > 1:
+            sizes[0] = 0  # an empty payload
+            sizes[1] = 2048  # the largest the default init allows
+        offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+        payload = gen.integers(0, 256, size=int(sizes.sum()) + 1, dtype=np.uint8)
+        sent0 = np.array([0xFFFFFFF0 + 0, 7, 123456], dtype=np.uint32)[:G]  # incl. u32 wrap
+        src0 = np.array([0xFFFFFFFA, 5, 99999], dtype=np.uint32)[:G]
+        pitch = 2048 + 4 + 13 + 3
+        dgrams = np.zeros((G, n, pitch), dtype=np.uint8)
+        dlen = np.zeros((G, n), dtype=np.int32)
+        gmax = np.zeros(G, dtype=np.int32)
+        for g in range(G):
+            en = C.c_int()
+            for ik in range(k):
+                i = g * k + ik
+                pl = payload[offs[i]:offs[i] + sizes[i]]
+                pp = L.set_fec_enc_buf(C.byref(S), ik, C.c_void_p(pl.ctypes.data if sizes[i] else payload.ctypes.data),
+                                       int(sizes[i]), C.byref(en))
+                gmax[g] = en.value if ik == 0 else max(gmax[g], en.value)
+                h = FecCodecHead(int(sent0[g]) + ik & 0xFFFFFFFF, int(src0[g]) + ik & 0xFFFFFFFF, n, k, ik)
+                ol = C.c_int()
+                q = L.pack_fec_head(C.byref(S), C.byref(h), pp, en.value, C.byref(ol))
+                dgrams[g, ik, :ol.value] = np.frombuffer(C.string_at(q, ol.value), dtype=np.uint8)
+                dlen[g, ik] = ol.value
+            for ik in range(k, n):
+                pp = L.get_fec_encoded_pkt(C.byref(S), codec, ik, int(gmax[g]), C.byref(en))
+                h = FecCodecHead(int(sent0[g]) + ik & 0xFFFFFFFF, int(src0[g]) + k - 1 & 0xFFFFFFFF, n, k, ik)
+                ol = C.c_int()
+                q = L.pack_fec_head(C.byref(S), C.byref(h), pp, en.value, C.byref(ol))
+                dgrams[g, ik, :ol.value] = np.frombuffer(C.string_at(q, ol.value), dtype=np.uint8)
+                dlen[g, ik] = ol.value
+        # receive side: parse every datagram and a corrupted copy of it
+        R = FecCodecBufS()
+        L.init_fec_buf(C.byref(R), 2048, 16)
+        parsed = np.zeros((G, n, 2, 8), dtype=np.int64)  # ok, sent, src, n, k, ik, unpacked_len, is_checksum
+        shards = np.zeros((G, n, pitch), dtype=np.uint8)
+        srcinfo = np.full((G, k, 2), -1, dtype=np.int64)  # (payload offset in shard or -1, size)
+        for g in range(G):
+            for ik in range(n):
+                for var in range(2):
+                    d = dgrams[g, ik, :dlen[g, ik]].copy()
+                    if var == 1 and dlen[g, ik] > 14:
+                        d[14] ^= 0x40  # a payload byte: caught by the shard checksum when present
+                    h = FecCodecHead()
+                    un = C.c_int()
+                    q = L.unpack_fec_head(C.byref(R), C.byref(h), C.c_void_p(d.ctypes.data), len(d), C.byref(un))
+                    parsed[g, ik, var] = [1 if q else 0, h.sent_pkt_index, h.src_pkt_index, h.codec_n, h.codec_k, h.ik,
+                                          un.value, int(R.is_checksum)]
+                    if q and var == 0:
+                        shards[g, ik, :un.value] = np.frombuffer(C.string_at(q, un.value), dtype=np.uint8)
+                        if ik < k:
+                            sz = C.c_uint16()
+                            sp = L.dec_src_pkt_info(q, C.byref(R), C.byref(sz))
+                            srcinfo[g, ik] = [(sp - q) if sp else -1, sz.value]
+        L.fec_free(codec)
+        L.release_fec_buf(C.byref(S))
+        L.release_fec_buf(C.byref(R))
+        key = f"{k}_{n}_{checksum}"
+        out[f"sizes_{key}"] = sizes
+        out[f"payload_{key}"] = payload
+        out[f"seq_{key}"] = np.stack([sent0, src0], axis=1)
+        out[f"dgrams_{key}"] = dgrams
+        out[f"dlen_{key}"] = dlen
+        out[f"gmax_{key}"] = gmax
+        out[f"parsed_{key}"] = parsed
+        out[f"shards_{key}"] = shards
+        out[f"srcinfo_{key}"] = srcinfo
+    np.savez_compressed(os.path.join(OUT, "wire.npz"), **out)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     rs, fec = load_ref()
@@ -319,6 +413,7 @@ def main():
     gen_encode(rs, fec)
     gen_reconstruct(rs)
     gen_fec_decode(fec)
+    gen_wire()
     manifest = {
         "generator": "oracle/gen_golden.py",
         "reference": "skywind3000/QuickNet @ 2024-10-08, module/rs.c + system/fec.c compiled by oracle/Makefile",

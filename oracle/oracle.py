@@ -44,6 +44,9 @@ class Oracle:
         L.orc_inv.argtypes = [C.c_ubyte]
         L.orc_byte_sum.restype = C.c_uint32
         L.orc_byte_sum.argtypes = [vp, ll]
+        L.orc_pack_group.argtypes = [i, i, vp, vp, vp, vp, C.c_uint32, C.c_uint32, i, i, vp, ll, vp]
+        L.orc_unpack_head.argtypes = [vp, i] + [C.POINTER(C.c_uint32)] * 2 + [C.POINTER(i)] * 4 + [vp, C.POINTER(i)]
+        L.orc_dec_src.argtypes = [vp, i, i, C.POINTER(i)]
         self.L = L
 
     # -- matrices
@@ -103,6 +106,35 @@ class Oracle:
     def byte_sum(self, a):
         return int(self.L.orc_byte_sum(_p(a), a.size))
 
+    # -- FEC wire marshalling (network/FecCodecBuf.cpp)
+    def pack_group(self, k, n, rows_full, payload, offs, sizes, sent0, src0, checksum, shard_cap=2052, pitch=2068):
+        """One full group through zfec_pack_input's send path: (datagrams [n][pitch], lengths[n], groupMax)."""
+        out = np.zeros((n, pitch), dtype=np.uint8)
+        ln = np.zeros(n, dtype=np.int32)
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        sizes = np.ascontiguousarray(sizes, dtype=np.int32)
+        pl = payload if payload.size else np.zeros(1, np.uint8)
+        gmax = self.L.orc_pack_group(k, n, _p(np.ascontiguousarray(rows_full)), _p(pl), _p(offs), _p(sizes),
+                                     sent0, src0, checksum, shard_cap, _p(out), pitch, _p(ln))
+        return out, ln, gmax
+
+    def unpack_head(self, dgram):
+        """unpack_fec_head: (rc, sent, src, n, k, ik, is_checksum, shard bytes)."""
+        d = np.ascontiguousarray(dgram, dtype=np.uint8)
+        sent, src = C.c_uint32(), C.c_uint32()
+        n, k, ik, cs, sl = (C.c_int() for _ in range(5))
+        shard = np.zeros(max(d.size, 1), dtype=np.uint8)
+        rc = self.L.orc_unpack_head(_p(d), d.size, C.byref(sent), C.byref(src), C.byref(n), C.byref(k), C.byref(ik),
+                                    C.byref(cs), _p(shard), C.byref(sl))
+        body = shard[: sl.value].copy() if rc == 1 else None
+        return rc, sent.value, src.value, n.value, k.value, ik.value, cs.value, body
+
+    def dec_src(self, shard, dec_pkt_size, checksum):
+        sz = C.c_int()
+        s = np.ascontiguousarray(shard, dtype=np.uint8)
+        off = self.L.orc_dec_src(_p(s), dec_pkt_size, checksum, C.byref(sz))
+        return off, sz.value
+
 
 class RS(C.Structure):  # module/rs.h:7-13
     _fields_ = [("data_shards", C.c_int), ("parity_shards", C.c_int), ("shards", C.c_int),
@@ -146,3 +178,41 @@ class RefCodec:
 
     def rs_reconstruct(self, h, ptrs, marks, nshards, length):
         return self.rs.reed_solomon_reconstruct(h, ptrs, _p(marks), nshards, length)
+
+
+class FecCodecBufS(C.Structure):  # network/FecCodecBuf.h:19-36
+    _fields_ = [("enc_pkt_size", C.c_int), ("enc_kmax", C.c_int), ("is_checksum", C.c_bool),
+                ("is_send_checksum", C.c_bool), ("fec_en_buf", C.c_void_p), ("sent_buf", C.c_void_p),
+                ("en_check_pkt", C.c_void_p), ("dec_pkt_size", C.c_int), ("dec_kmax", C.c_int),
+                ("fecDecoderBuf", C.c_void_p), ("fecDecoderIndices", C.c_void_p), ("dec_buf", C.c_void_p),
+                ("dec_check_pkt", C.c_void_p)]
+
+
+class FecCodecHead(C.Structure):  # network/FecCodecBuf.h:10-17
+    _fields_ = [("sent_pkt_index", C.c_uint32), ("src_pkt_index", C.c_uint32), ("codec_n", C.c_ubyte),
+                ("codec_k", C.c_ubyte), ("ik", C.c_ubyte)]
+
+
+def load_callers(path):
+    """The reference's network/FecCodec.cpp + FecCodecBuf.cpp built by `make -C oracle ref`."""
+    L = C.CDLL(path)
+    P, vp, i, ip = C.POINTER(FecCodecBufS), C.c_void_p, C.c_int, C.POINTER(C.c_int)
+    L.init_fec_buf.argtypes = [P, i, i]
+    L.release_fec_buf.argtypes = [P]
+    L.set_fec_enc_buf.argtypes = [P, i, vp, i, ip]
+    L.set_fec_enc_buf.restype = vp
+    L.get_fec_encoded_pkt.argtypes = [P, vp, i, i, ip]
+    L.get_fec_encoded_pkt.restype = vp
+    L.pack_fec_head.argtypes = [P, C.POINTER(FecCodecHead), vp, i, ip]
+    L.pack_fec_head.restype = vp
+    L.unpack_fec_head.argtypes = [P, C.POINTER(FecCodecHead), vp, i, ip]
+    L.unpack_fec_head.restype = vp
+    L.set_fec_dec_buf.argtypes = [P, i, vp, i, i]
+    L.set_fec_dec_buf.restype = vp
+    L.reset_fec_dec_buf.argtypes = [P]
+    L.fec_decode_pkts.argtypes = [P, vp, i]
+    L.get_fec_decoded_pkt.argtypes = [P, i]
+    L.get_fec_decoded_pkt.restype = vp
+    L.dec_src_pkt_info.argtypes = [vp, P, C.POINTER(C.c_uint16)]
+    L.dec_src_pkt_info.restype = vp
+    return L

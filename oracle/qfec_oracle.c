@@ -12,7 +12,7 @@
  * library (liboracle.so), and only to check or time against. The product path lives in
  * quicknet_amd/csrc and never links or calls anything here.
  *
- * Parity of this restatement is pinned by tests/golden/*, which oracle/gen_golden.py
+ * Parity of this restatement is pinned by the tests/golden vectors, which oracle/gen_golden.py
  * produced by running the reference itself (compiled by oracle/Makefile into
  * oracle/_ref/ from /root/reference/module/{rs,fec}.c).
  *
@@ -394,6 +394,8 @@ int orc_fec_decode(int k, int n, const u8 *enc_rows_full, u8 **pkt, int *idx, in
     u8 *mat, **fresh;
     int r, c, b;
     orc_init();
+    if (k <= 0)
+        return 1;
     if (fec_shuffle(pkt, idx, k))
         return 1;
     mat = (u8 *)malloc((size_t)k * (size_t)k);
@@ -542,4 +544,118 @@ uint32_t orc_byte_sum(const u8 *p, long long len)
     long long i;
     for (i = 0; i < len; ++i) s += p[i];
     return s;
+}
+
+/* ------------------------------------------------------------------ FEC wire marshalling
+ * network/FecCodecBuf.cpp: the shard format the network layer feeds the codec, and the
+ * 11-byte (+2 checksum) FEC header on every datagram.  All integers little-endian
+ * (iencode16u_lsb / iencode32u_lsb, system/imemdata.h:805-870). */
+
+static void put16(u8 *p, unsigned v) { p[0] = (u8)v; p[1] = (u8)(v >> 8); }
+static void put32(u8 *p, uint32_t v) { p[0] = (u8)v; p[1] = (u8)(v >> 8); p[2] = (u8)(v >> 16); p[3] = (u8)(v >> 24); }
+static unsigned get16(const u8 *p) { return (unsigned)p[0] | ((unsigned)p[1] << 8); }
+static uint32_t get32(const u8 *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+
+/* set_fec_enc_buf() (FecCodecBuf.cpp:66-103): shard = [size][cksum16(payload) if checksum]
+ * [payload], zero-filled to cap bytes.  Returns en_size = size + 2 or + 4. */
+int orc_build_shard(const u8 *payload, int size, int checksum, u8 *shard, int cap)
+{
+    int head = checksum ? 4 : 2;
+    memset(shard, 0, (size_t)cap);
+    put16(shard, (unsigned)size);
+    if (checksum)
+        put16(shard + 2, orc_byte_sum(payload, size) & 0xFFFF);
+    memcpy(shard + head, payload, (size_t)size);
+    return size + head;
+}
+
+/* pack_fec_head() (FecCodecBuf.cpp:274-328): [tag 0xEC | 0xED][sent u32][src u32]
+ * [ikn u16 = n | k << 4 | ik << 8][cksum16(buf) if checksum][buf].  Returns the length. */
+int orc_pack_head(uint32_t sent, uint32_t src, int n, int k, int ik, int checksum, const u8 *buf, int len, u8 *out)
+{
+    int off = 0;
+    unsigned ikn = ((unsigned)n | ((unsigned)k << 4) | ((unsigned)ik << 8)) & 0xFFFF;
+    out[off++] = checksum ? 0xED : 0xEC;
+    put32(out + off, sent); off += 4;
+    put32(out + off, src); off += 4;
+    put16(out + off, ikn); off += 2;
+    if (checksum) { put16(out + off, orc_byte_sum(buf, len) & 0xFFFF); off += 2; }
+    memcpy(out + off, buf, (size_t)len);
+    return off + len;
+}
+
+/* unpack_fec_head() (FecCodecBuf.cpp:334-411).  Returns 1 for an FEC datagram (fields and
+ * the shard bytes [0, *shard_len) written out), 0 for a non-FEC datagram (tag not EC/ED, or
+ * shorter than 11 bytes: payload = dgram + 1), -1 when the shard checksum fails (the
+ * network layer drops the datagram, NetFecCodec.cpp:210-213).  is_checksum receives
+ * whether the tag carried a checksum (it also governs dec_src_pkt_info's check). */
+int orc_unpack_head(const u8 *d, int len, uint32_t *sent, uint32_t *src, int *n, int *k, int *ik,
+                    int *is_checksum, u8 *shard, int *shard_len)
+{
+    unsigned ikn;
+    int off = 11;
+    if (len < 1 || (d[0] != 0xEC && d[0] != 0xED) || len < 11)
+        return 0;
+    *is_checksum = d[0] == 0xED;
+    *sent = get32(d + 1);
+    *src = get32(d + 5);
+    ikn = get16(d + 9);
+    *n = (int)(ikn & 0xF);
+    *k = (int)((ikn >> 4) & 0xF);
+    *ik = (int)((ikn >> 8) & 0xF);
+    if (*is_checksum) {
+        /* rm_checksum (FecCodecBuf.cpp:42-61) over the bytes after the checksum */
+        unsigned want = get16(d + off);
+        if ((orc_byte_sum(d + off + 2, len - off - 2) & 0xFFFF) != want)
+            return -1;
+        off += 2;
+    }
+    *shard_len = len - off;
+    memcpy(shard, d + off, (size_t)(len - off));
+    return 1;
+}
+
+/* dec_src_pkt_info() (FecCodecBuf.cpp:109-133): returns the payload offset in the shard (2
+ * or 4) and its size, or -1 for a size >= dec_pkt_size or a checksum mismatch. */
+int orc_dec_src(const u8 *shard, int dec_pkt_size, int checksum, int *size)
+{
+    unsigned sz = get16(shard);
+    *size = (int)sz;
+    if ((int)sz >= dec_pkt_size)
+        return -1;
+    if (checksum) {
+        if ((orc_byte_sum(shard + 4, sz) & 0xFFFF) != get16(shard + 2))
+            return -1;
+        return 4;
+    }
+    return 2;
+}
+
+/* One full group through the send path of zfec_pack_input (NetFecCodec.cpp:96-172):
+ * k source datagrams (sent0 + i, src0 + i), then n - k check datagrams (sent0 + k + j,
+ * src0 + k - 1) whose shards are fec_encode(.., k + j, groupMax).  rows_full is the n x k
+ * fec.c matrix.  out: n datagrams at stride out_pitch, lengths in out_len.  Returns groupMax. */
+int orc_pack_group(int k, int n, const u8 *rows_full, const u8 *payload, const long long *offs, const int *sizes,
+                   uint32_t sent0, uint32_t src0, int checksum, int shard_cap, u8 *out, long long out_pitch,
+                   int *out_len)
+{
+    u8 *shards = (u8 *)calloc((size_t)k * (size_t)shard_cap, 1);
+    u8 **src = (u8 **)malloc(sizeof(u8 *) * (size_t)k);
+    u8 *par = (u8 *)calloc((size_t)shard_cap, 1);
+    int i, j, gmax = 0;
+    orc_init();
+    for (i = 0; i < k; ++i) {
+        int en = orc_build_shard(payload + offs[i], sizes[i], checksum, shards + (size_t)i * shard_cap, shard_cap);
+        src[i] = shards + (size_t)i * shard_cap;
+        gmax = i == 0 ? en : (en > gmax ? en : gmax);
+        out_len[i] = orc_pack_head(sent0 + (uint32_t)i, src0 + (uint32_t)i, n, k, i, checksum, src[i], en,
+                                   out + (size_t)i * out_pitch);
+    }
+    for (j = k; j < n; ++j) {
+        orc_fec_encode(k, n, rows_full, src, par, j, gmax);
+        out_len[j] = orc_pack_head(sent0 + (uint32_t)j, src0 + (uint32_t)k - 1, n, k, j, checksum, par, gmax,
+                                   out + (size_t)j * out_pitch);
+    }
+    free(shards); free(src); free(par);
+    return gmax;
 }

@@ -128,3 +128,43 @@ def test_fec_reconstruct_matches_rs_rule(oracle):
     bad = oracle.fec_reconstruct(rows, b, par.copy(), marks, B)
     assert bad == 0
     assert np.array_equal(a, b)
+
+
+WIRE = [(4, 5), (4, 6), (3, 5), (5, 8), (7, 8), (10, 13), (2, 4), (3, 4), (14, 15), (1, 2)]
+
+
+@pytest.mark.parametrize("k,n", WIRE)
+@pytest.mark.parametrize("checksum", [1, 0])
+def test_wire_pack_unpack(oracle, golden, k, n, checksum):
+    """The FEC wire format vs the reference's own FecCodecBuf.cpp (send: set_fec_enc_buf,
+    get_fec_encoded_pkt, pack_fec_head; receive: unpack_fec_head, dec_src_pkt_info)."""
+    z = golden("wire.npz")
+    key = f"{k}_{n}_{checksum}"
+    sizes, payload, seq = z[f"sizes_{key}"], z[f"payload_{key}"], z[f"seq_{key}"]
+    dg, dl, gmax = z[f"dgrams_{key}"], z[f"dlen_{key}"], z[f"gmax_{key}"]
+    G = dg.shape[0]
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    full = np.concatenate([np.eye(k, dtype=np.uint8), oracle.vandermonde(k, n)])
+    for g in range(G):
+        out, ln, gm = oracle.pack_group(k, n, full, payload, offs[g * k:(g + 1) * k], sizes[g * k:(g + 1) * k],
+                                        int(seq[g, 0]), int(seq[g, 1]), checksum, pitch=dg.shape[2])
+        assert gm == gmax[g]
+        assert np.array_equal(ln, dl[g])
+        assert np.array_equal(out, dg[g])
+    parsed, shards, srcinfo = z[f"parsed_{key}"], z[f"shards_{key}"], z[f"srcinfo_{key}"]
+    for g in range(G):
+        for ik in range(n):
+            for var in range(2):
+                d = dg[g, ik, :dl[g, ik]].copy()
+                if var == 1 and dl[g, ik] > 14:
+                    d[14] ^= 0x40
+                rc, sent, src, nn, kk, ii, cs, body = oracle.unpack_head(d)
+                ok = rc == 1
+                assert int(ok) == parsed[g, ik, var, 0]
+                if ok:
+                    assert [sent, src, nn, kk, ii, len(body), cs] == list(parsed[g, ik, var, 1:8])
+                    if var == 0:
+                        assert np.array_equal(body, shards[g, ik, :len(body)])
+                        if ik < k:
+                            off, sz = oracle.dec_src(body, 2068, cs)
+                            assert [off, sz] == list(srcinfo[g, ik]) or (off == -1 and srcinfo[g, ik, 0] == -1)
