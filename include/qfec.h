@@ -89,6 +89,32 @@ qfec_code *qfec_rs_code(struct _reed_solomon *rs);
 /* The n x k systematic matrix of a fec_new() handle (identity on top). */
 int qfec_fec_matrix(void *fec_handle, unsigned char *out_full);
 
+/* ---- FEC datagram batches: the network layer's shard + wire format ----
+ * Send, for `groups` full groups of k packets (zfec_pack_input, network/NetFecCodec.cpp:96-172):
+ *   shard (g, i)    = [size u16][cksum16(payload) u16 if checksum][payload], zero-filled
+ *                     (set_fec_enc_buf, network/FecCodecBuf.cpp:66-103)
+ *   check shards    = fec_encode(.., groupMax) (get_fec_encoded_pkt, FecCodecBuf.cpp:137-156)
+ *   datagram (g, j) = [0xEC|0xED][sent u32][src u32][n | k<<4 | ik<<8 u16][cksum16 if 0xED][shard]
+ *                     (pack_fec_head, FecCodecBuf.cpp:274-328); sent = seq[g][0] + j,
+ *                     src = seq[g][1] + min(j, k - 1)
+ * Receive reverses it: unpack_fec_head (:334-411; a failed shard checksum drops the
+ * datagram), reconstruct of the missing data shards from the first k valid ones, and
+ * dec_src_pkt_info (:109-133): status[g*k+i] = payload offset in the shard row (2 or 4),
+ * -1 dropped (size >= dec_pkt_size or checksum mismatch), -2 lost (group unrecoverable);
+ * psize = the payload size field.
+ * Layout: d_shards [G][n][shard_pitch], d_wire [G][n][wire_pitch] (16-B aligned, pitches
+ * multiples of 16, wire_pitch >= shard_pitch + 13), d_wire_len [G*n] (0 = not received),
+ * d_marks [G*n] rs.c-layout scratch, d_rx_size [G*n] (nullable).  n = k + m <= 15 (the
+ * header's 4-bit fields).  d_payload must stay readable 16 bytes past its last byte. */
+int qfec_pack_datagrams(qfec_code *code, const unsigned char *d_payload, const long long *d_offsets,
+                        const int *d_sizes, const unsigned int *d_seq, long long groups, int checksum,
+                        unsigned char *d_shards, long long shard_pitch, unsigned char *d_wire,
+                        long long wire_pitch, int *d_wire_len, void *stream);
+int qfec_unpack_datagrams(qfec_code *code, const unsigned char *d_wire, long long wire_pitch,
+                          const int *d_wire_len, long long groups, int checksum, int dec_pkt_size,
+                          unsigned char *d_shards, long long shard_pitch, unsigned char *d_marks,
+                          int *d_rx_size, int *d_status, int *d_psize, void *stream);
+
 /* Fill nbytes of device memory with the synthetic stream of quicknet_amd/synth.py. */
 int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long seed, void *stream);
 

@@ -133,6 +133,48 @@ class Code:
         check(lib().qfec_reconstruct(self._h, _dev_ptr(data), _dev_ptr(parity), _dev_ptr(marks), G, block_size,
                                      pitch, _dev_ptr(failed), _stream_handle(stream)), "qfec_reconstruct")
 
+    # -- FEC datagram batches (network/FecCodecBuf.cpp wire format); n = k + m <= 15
+    def pack_datagrams(self, payload, offsets, sizes, seq, checksum=True, shard_pitch=None, wire_pitch=None,
+                       stream=None):
+        """payload: uint8 device tensor (16 readable bytes past the last packet); offsets int64
+        [G*k]; sizes int32 [G*k]; seq uint32/int32 [G, 2] (sent, src index of each group's first
+        packet).  Returns (shards [G, n, pitch], wire [G, n, wire_pitch], wire_len int32 [G, n])."""
+        import torch
+        G = sizes.numel() // self.k
+        n = self.k + self.m
+        head = 4 if checksum else 2
+        if shard_pitch is None:
+            shard_pitch = (int(sizes.max().item()) + head + 15) // 16 * 16 if G else 16
+        if wire_pitch is None:
+            wire_pitch = (shard_pitch + 13 + 15) // 16 * 16
+        dev = payload.device
+        shards = torch.empty((G, n, shard_pitch), dtype=torch.uint8, device=dev)
+        wire = torch.empty((G, n, wire_pitch), dtype=torch.uint8, device=dev)
+        wire_len = torch.empty((G, n), dtype=torch.int32, device=dev)
+        check(lib().qfec_pack_datagrams(self._h, _dev_ptr(payload), _dev_ptr(offsets), _dev_ptr(sizes), _dev_ptr(seq),
+                                        G, int(bool(checksum)), _dev_ptr(shards), shard_pitch, _dev_ptr(wire),
+                                        wire_pitch, _dev_ptr(wire_len), _stream_handle(stream)), "qfec_pack_datagrams")
+        return shards, wire, wire_len
+
+    def unpack_datagrams(self, wire, wire_len, checksum=True, dec_pkt_size=2068, shard_pitch=None, stream=None):
+        """wire [G, n, wire_pitch] uint8, wire_len int32 [G, n] (0 = not received).  Returns
+        (shards [G, n, pitch], status int32 [G, k], psize int32 [G, k], rx_size int32 [G, n])."""
+        import torch
+        G, n, wire_pitch = wire.shape
+        if shard_pitch is None:
+            shard_pitch = (wire_pitch - 13) // 16 * 16
+        dev = wire.device
+        shards = torch.empty((G, n, shard_pitch), dtype=torch.uint8, device=dev)
+        marks = torch.empty(G * n, dtype=torch.uint8, device=dev)
+        rx = torch.empty((G, n), dtype=torch.int32, device=dev)
+        status = torch.empty((G, self.k), dtype=torch.int32, device=dev)
+        psize = torch.empty((G, self.k), dtype=torch.int32, device=dev)
+        check(lib().qfec_unpack_datagrams(self._h, _dev_ptr(wire), wire_pitch, _dev_ptr(wire_len), G, int(bool(checksum)),
+                                          dec_pkt_size, _dev_ptr(shards), shard_pitch, _dev_ptr(marks), _dev_ptr(rx),
+                                          _dev_ptr(status), _dev_ptr(psize), _stream_handle(stream)),
+              "qfec_unpack_datagrams")
+        return shards, status, psize, rx
+
     def decode_rows(self, marks_n):
         """Host-side decode matrix for one group-order mark vector: (e, rows[e,k], survivors[k], erased[e])."""
         marks_n = np.ascontiguousarray(marks_n, dtype=np.uint8)

@@ -38,7 +38,8 @@ struct EncodeArgs {
     const uint8_t* gf_exp;  // LDS variant: exp[512]
     const uint8_t* gf_log;  // LDS variant: log[256]
     uint64_t work;          // groups * cols lanes (< 2^32)
-    uint64_t pitch;
+    uint64_t pitch;         // bytes between rows of a group
+    uint64_t dgs, pgs;      // bytes between groups: data (k*pitch when packed), parity (m*pitch)
     DivMagic cols_div;
     uint32_t cols;          // columns per row: 16-B columns (vec16) or bytes
     int k, m;
@@ -56,6 +57,7 @@ struct ReconArgs {
     unsigned int* failed;
     uint64_t groups;
     uint64_t pitch;
+    uint64_t dgs, pgs;        // bytes between groups: data rows, parity rows
     uint32_t cols;            // 16-B columns (vec16) or bytes per row
     int k, m;
     int surv_off, lost_off, hdr;
@@ -63,6 +65,33 @@ struct ReconArgs {
     int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once
     uint32_t wpg;             // waves per group = ceil(cols / 64) (vec16 LUT kernels)
 };
+
+// FEC datagram batches (qfec_wire.hip): shards[G][n][pitch], wire[G][n][wire_pitch]
+struct WireArgs {
+    const uint8_t* payload;   // send: concatenated payloads (16 readable bytes past the last)
+    const int64_t* offsets;   // send: [G*k] payload offsets
+    const int32_t* sizes;     // send: [G*k] payload sizes
+    const uint32_t* seq;      // send: [G][2] sent / src index of the group's first packet
+    uint8_t* shards;
+    uint64_t group_stride;    // n * pitch
+    uint64_t pitch;
+    uint8_t* wire;
+    uint64_t wire_pitch;
+    int32_t* wire_len;        // [G*n] datagram lengths (receive: 0 = not received)
+    uint8_t* marks;           // receive: rs.c-layout erasure marks
+    int32_t* rx_size;         // receive: [G*n] shard size or -1 (may be NULL)
+    int32_t* status;          // receive: [G*k] payload offset (2|4), -1 dropped, -2 lost
+    int32_t* psize;           // receive: [G*k] payload size field
+    uint64_t groups;
+    int k, m;
+    int checksum;
+    int dec_pkt_size;
+};
+
+hipError_t launch_build_shards(const WireArgs& a, hipStream_t s);
+hipError_t launch_emit_wire(const WireArgs& a, hipStream_t s);
+hipError_t launch_parse_wire(const WireArgs& a, hipStream_t s);
+hipError_t launch_check_payloads(const WireArgs& a, hipStream_t s);
 
 // runtime tuning knobs (qfec_tune); defaults are the measured best
 struct Tuning {

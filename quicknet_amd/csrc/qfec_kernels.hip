@@ -135,8 +135,8 @@ __global__ void __launch_bounds__(256) k_encode_perm(EncodeArgs a) {
     if (t >= a.work) return;
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
-    const uint8_t* src = a.data + g * (uint64_t)(K * a.pitch) + (uint64_t)col * 16u;
-    uint8_t* dst = a.parity + g * (uint64_t)(M * a.pitch) + (uint64_t)col * 16u;
+    const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
+    uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
     const uint32_t* __restrict__ tab = a.tab;
 
     uint4 x[K];
@@ -176,8 +176,8 @@ __global__ void __launch_bounds__(256) k_encode_perm_rows(EncodeArgs a) {
     if (t >= a.work) return;
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
-    const uint8_t* src = a.data + g * (uint64_t)(K * a.pitch) + (uint64_t)col * 16u;
-    uint8_t* dst = a.parity + g * (uint64_t)(M * a.pitch) + (uint64_t)col * 16u;
+    const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
+    uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
     const uint32_t* __restrict__ tab = a.tab;
     uint4 x[K];
 #pragma unroll
@@ -215,8 +215,8 @@ __global__ void __launch_bounds__(256) k_encode_perm_any(EncodeArgs a) {
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
     const int k = a.k, m = a.m;
-    const uint8_t* src = a.data + g * (uint64_t)k * a.pitch + (uint64_t)col * 16u;
-    uint8_t* dst = a.parity + g * (uint64_t)m * a.pitch + (uint64_t)col * 16u;
+    const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
+    uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
     for (int r0 = 0; r0 < m; r0 += RCH) {
         uint4 acc[RCH];
 #pragma unroll
@@ -246,8 +246,8 @@ __global__ void __launch_bounds__(256) k_encode_bytes(EncodeArgs a) {
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t b = (uint32_t)(t - g * (uint64_t)a.cols);
     const int k = a.k, m = a.m;
-    const uint8_t* src = a.data + g * (uint64_t)k * a.pitch + b;
-    uint8_t* dst = a.parity + g * (uint64_t)m * a.pitch + b;
+    const uint8_t* src = a.data + g * a.dgs + b;
+    uint8_t* dst = a.parity + g * a.pgs + b;
     for (int r = 0; r < m; ++r) {
         const uint32_t* tr = a.tab + (r * k) * QFEC_TAB_STRIDE;
         uint32_t acc = tr[5] ? (uint32_t)dst[(uint64_t)r * a.pitch] : 0u;
@@ -276,8 +276,8 @@ __global__ void __launch_bounds__(256) k_encode_ldslog(EncodeArgs a) {
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
     const int k = a.k, m = a.m;
-    const uint8_t* src = a.data + g * (uint64_t)k * a.pitch + (uint64_t)col * 16u;
-    uint8_t* dst = a.parity + g * (uint64_t)m * a.pitch + (uint64_t)col * 16u;
+    const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
+    uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
     for (int r0 = 0; r0 < m; r0 += RCH) {
         uint32_t acc[RCH][4];
 #pragma unroll
@@ -322,8 +322,8 @@ __global__ void __launch_bounds__(256) k_encode_ldslog(EncodeArgs a) {
 // index, [hdr + (j*k + c)*QFEC_TAB_STRIDE] perm table; dword 5 of (j, 0) = stale flag.
 
 __device__ __forceinline__ const uint8_t* shard_ptr(const ReconArgs& a, uint64_t g, uint32_t s) {
-    return s < (uint32_t)a.k ? a.data + (g * (uint64_t)a.k + s) * a.pitch
-                             : a.parity + (g * (uint64_t)a.m + (s - a.k)) * a.pitch;
+    return s < (uint32_t)a.k ? a.data + g * a.dgs + (uint64_t)s * a.pitch
+                             : a.parity + g * a.pgs + (uint64_t)(s - a.k) * a.pitch;
 }
 
 __device__ __forceinline__ int group_record(const ReconArgs& a, uint64_t g, int lane) {
@@ -459,13 +459,14 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     const int rec = __builtin_amdgcn_readfirstlane(lut[mask]);
     const uint32_t* tab = records + rec + a.hdr;
     const uint64_t pitch = a.pitch;
-    uint8_t* data_g = data + g * K * pitch;
+    uint8_t* data_g = data + g * a.dgs;
+    const uint8_t* par_g = parity + g * a.pgs;
     const uint8_t* src[K];
 #pragma unroll
     for (int c = 0; c < K; ++c) {
         const uint32_t s = (uint32_t)__builtin_ctzll(avail);
         avail &= avail - 1;
-        src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : parity + (g * M + (s - K)) * pitch;
+        src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : par_g + (uint64_t)(s - K) * pitch;
     }
     const uint32_t col = part * 64u + lane;
     if (col < a.cols) {
@@ -502,7 +503,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_any(ReconArgs a) {
                     acc[j] = make_uint4(0, 0, 0, 0);
                     const int jj = j0 + j;
                     if (jj < e && tab[(jj * k) * QFEC_TAB_STRIDE + 5])
-                        acc[j] = *reinterpret_cast<const uint4*>(a.data + (g * (uint64_t)k + lost[jj]) * a.pitch + off);
+                        acc[j] = *reinterpret_cast<const uint4*>(a.data + g * a.dgs + (uint64_t)lost[jj] * a.pitch + off);
                 }
                 for (int c = 0; c < k; ++c) {
                     const uint4 v = ld16(shard_ptr(a, g, surv[c]) + off);
@@ -514,7 +515,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_any(ReconArgs a) {
                 }
 #pragma unroll
                 for (int j = 0; j < RCH; ++j)
-                    if (j0 + j < e) st16(a.data + (g * (uint64_t)k + lost[j0 + j]) * a.pitch + off, acc[j]);
+                    if (j0 + j < e) st16(a.data + g * a.dgs + (uint64_t)lost[j0 + j] * a.pitch + off, acc[j]);
             } else {
                 const uint64_t off = col;
                 uint32_t acc[RCH];
@@ -523,7 +524,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_any(ReconArgs a) {
                     acc[j] = 0;
                     const int jj = j0 + j;
                     if (jj < e && tab[(jj * k) * QFEC_TAB_STRIDE + 5])
-                        acc[j] = a.data[(g * (uint64_t)k + lost[jj]) * a.pitch + off];
+                        acc[j] = a.data[g * a.dgs + (uint64_t)lost[jj] * a.pitch + off];
                 }
                 for (int c = 0; c < k; ++c) {
                     const Sel s = gf_sel((uint32_t)shard_ptr(a, g, surv[c])[off]);
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_any(ReconArgs a) {
                 }
 #pragma unroll
                 for (int j = 0; j < RCH; ++j)
-                    if (j0 + j < e) a.data[(g * (uint64_t)k + lost[j0 + j]) * a.pitch + off] = (uint8_t)acc[j];
+                    if (j0 + j < e) a.data[g * a.dgs + (uint64_t)lost[j0 + j] * a.pitch + off] = (uint8_t)acc[j];
             }
         }
     }
@@ -567,8 +568,8 @@ __global__ void __launch_bounds__(256) k_probe_xor(EncodeArgs a) {
     if (t >= a.work) return;
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
-    const uint8_t* src = a.data + g * (uint64_t)a.k * a.pitch + (uint64_t)col * 16u;
-    uint8_t* dst = a.parity + g * (uint64_t)a.m * a.pitch + (uint64_t)col * 16u;
+    const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
+    uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
     uint4 acc = make_uint4(0, 0, 0, 0);
     for (int c = 0; c < a.k; ++c) {
         const uint4 v = ld16(src + (uint64_t)c * a.pitch);

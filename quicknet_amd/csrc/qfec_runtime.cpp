@@ -334,7 +334,8 @@ bool vec16_ok(const void* a, const void* b, int block, long long pitch) {
 
 // launch encode over `groups` groups with tables `tab` covering `m` rows
 int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, const uint8_t* d_data,
-               uint8_t* d_par, long long groups, int block, long long pitch, hipStream_t s) {
+               uint8_t* d_par, long long groups, int block, long long pitch, hipStream_t s,
+               long long dgs = -1, long long pgs = -1) {
     EncodeArgs a{};
     a.tab = tab;
     a.gf_exp = ctx.d_gf;
@@ -346,11 +347,18 @@ int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, cons
     a.impl = tuning().encode_impl;
     a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
     a.cols_div = make_div_magic(a.cols);
+    a.dgs = dgs >= 0 ? (uint64_t)dgs : (uint64_t)c->k * pitch;
+    a.pgs = pgs >= 0 ? (uint64_t)pgs : (uint64_t)m * pitch;
+    if (a.vec16 && ((a.dgs | a.pgs) & 15)) {
+        a.vec16 = 0;
+        a.cols = (uint32_t)block;
+        a.cols_div = make_div_magic(a.cols);
+    }
     const long long per = std::max<long long>(1, (long long)(0x7FFFFFFFll / a.cols));
     for (long long g0 = 0; g0 < groups; g0 += per) {
         const long long gn = std::min(per, groups - g0);
-        a.data = d_data + (size_t)g0 * c->k * pitch;
-        a.parity = d_par + (size_t)g0 * m * pitch;
+        a.data = d_data + (size_t)g0 * a.dgs;
+        a.parity = d_par + (size_t)g0 * a.pgs;
         a.work = (uint64_t)gn * a.cols;
         hipError_t e = launch_encode(a, g_variant.load(), s);
         if (e != hipSuccess) return hip_fail(e, "encode kernel launch");
@@ -360,7 +368,8 @@ int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, cons
 
 int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const int32_t* group_rec,
                     const uint32_t* recs, uint8_t* d_data, const uint8_t* d_par, const uint8_t* d_marks,
-                    long long groups, int block, long long pitch, unsigned* d_failed, hipStream_t s) {
+                    long long groups, int block, long long pitch, unsigned* d_failed, hipStream_t s,
+                    long long dgs = -1, long long pgs = -1) {
     ReconArgs a{};
     const RecordLayout L = record_layout(c->k, c->m);
     a.data = d_data;
@@ -377,7 +386,9 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.surv_off = L.surv_off;
     a.lost_off = L.lost_off;
     a.hdr = L.hdr;
-    a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
+    a.dgs = dgs >= 0 ? (uint64_t)dgs : (uint64_t)c->k * pitch;
+    a.pgs = pgs >= 0 ? (uint64_t)pgs : (uint64_t)c->m * pitch;
+    a.vec16 = vec16_ok(d_data, d_par, block, pitch) && !((a.dgs | a.pgs) & 15) ? 1 : 0;
     a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
     a.impl = tuning().recon_impl;
     a.wpg = (a.cols + 63) / 64;
@@ -617,9 +628,124 @@ int qfec_probe_stream(const unsigned char* d_data, unsigned char* d_parity, long
     a.cols = (uint32_t)((block_size + 15) / 16);
     a.cols_div = make_div_magic(a.cols);
     a.work = (uint64_t)groups * a.cols;
+    a.dgs = (uint64_t)k * pitch;
+    a.pgs = (uint64_t)m * pitch;
     if (a.work >= 0x80000000ull) return QFEC_EINVAL;
     hipError_t e = launch_probe_xor(a, (hipStream_t)stream);
     return e == hipSuccess ? QFEC_OK : hip_fail(e, "probe launch");
+}
+
+}  // extern "C"
+
+// ====================================================================== FEC datagram batches
+namespace {
+
+int wire_check(const qfec_code* c, long long groups, int checksum, long long pitch, long long wire_pitch,
+               const void* shards, const void* wire) {
+    if (!c || groups < 0 || (checksum != 0 && checksum != 1)) return QFEC_EINVAL;
+    if (c->k + c->m > 15 || c->k < 1) {
+        set_error("FEC datagrams carry 4-bit n and k (network/FecCodecBuf.cpp:290-299): n = %d > 15", c->k + c->m);
+        return QFEC_EUNSUP;
+    }
+    if (pitch < 16 || pitch % 16 || wire_pitch % 16 || wire_pitch < (long long)round_up((size_t)pitch + 13, 16) ||
+        ((uintptr_t)shards | (uintptr_t)wire) % 16) {
+        set_error("datagram batch: shard pitch and wire pitch must be multiples of 16, wire >= shard + 13, 16-B aligned");
+        return QFEC_EINVAL;
+    }
+    return QFEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qfec_pack_datagrams(qfec_code* code, const unsigned char* d_payload, const long long* d_offsets,
+                        const int* d_sizes, const unsigned int* d_seq, long long groups, int checksum,
+                        unsigned char* d_shards, long long shard_pitch, unsigned char* d_wire, long long wire_pitch,
+                        int* d_wire_len, void* stream) {
+    int rc = wire_check(code, groups, checksum, shard_pitch, wire_pitch, d_shards, d_wire);
+    if (rc) return rc;
+    if (groups == 0) return QFEC_OK;
+    DevCtx* ctx = nullptr;
+    if ((rc = current_ctx(&ctx))) return rc;
+    uint32_t* tab = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_enc(code, ctx->device, &tab);
+    }
+    if (rc) return rc;
+    const int k = code->k, m = code->m, n = k + m;
+    hipStream_t s = (hipStream_t)stream;
+    WireArgs a{};
+    a.payload = d_payload;
+    a.offsets = (const int64_t*)d_offsets;
+    a.sizes = d_sizes;
+    a.seq = d_seq;
+    a.shards = d_shards;
+    a.pitch = (uint64_t)shard_pitch;
+    a.group_stride = (uint64_t)n * shard_pitch;
+    a.wire = d_wire;
+    a.wire_pitch = (uint64_t)wire_pitch;
+    a.wire_len = d_wire_len;
+    a.groups = (uint64_t)groups;
+    a.k = k;
+    a.m = m;
+    a.checksum = checksum;
+    hipError_t e = launch_build_shards(a, s);
+    if (e != hipSuccess) return hip_fail(e, "build_shards launch");
+    // check shards: fec_encode(.., groupMax) over the k data shards (FecCodecBuf.cpp:151);
+    // bytes past a group's groupMax are zero in every data shard, hence in the parity.
+    if (m > 0 && (rc = run_encode(*ctx, code, tab, m, d_shards, d_shards + (size_t)k * shard_pitch, groups,
+                                  (int)shard_pitch, shard_pitch, s, (long long)a.group_stride, (long long)a.group_stride)))
+        return rc;
+    e = launch_emit_wire(a, s);
+    return e == hipSuccess ? QFEC_OK : hip_fail(e, "emit_wire launch");
+}
+
+int qfec_unpack_datagrams(qfec_code* code, const unsigned char* d_wire, long long wire_pitch, const int* d_wire_len,
+                          long long groups, int checksum, int dec_pkt_size, unsigned char* d_shards,
+                          long long shard_pitch, unsigned char* d_marks, int* d_rx_size, int* d_status, int* d_psize,
+                          void* stream) {
+    int rc = wire_check(code, groups, checksum, shard_pitch, wire_pitch, d_shards, d_wire);
+    if (rc) return rc;
+    if (groups == 0) return QFEC_OK;
+    if (!d_marks || !d_status || !d_psize || !d_wire_len) return QFEC_EINVAL;
+    DevCtx* ctx = nullptr;
+    if ((rc = current_ctx(&ctx))) return rc;
+    DevTables* d = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_lut(code, ctx->device, &d);
+    }
+    if (rc) return rc;
+    const int k = code->k, m = code->m, n = k + m;
+    hipStream_t s = (hipStream_t)stream;
+    WireArgs a{};
+    a.shards = d_shards;
+    a.pitch = (uint64_t)shard_pitch;
+    a.group_stride = (uint64_t)n * shard_pitch;
+    a.wire = const_cast<uint8_t*>(d_wire);
+    a.wire_pitch = (uint64_t)wire_pitch;
+    a.wire_len = const_cast<int32_t*>(d_wire_len);
+    a.marks = d_marks;
+    a.rx_size = d_rx_size;
+    a.status = d_status;
+    a.psize = d_psize;
+    a.groups = (uint64_t)groups;
+    a.k = k;
+    a.m = m;
+    a.checksum = checksum;
+    a.dec_pkt_size = dec_pkt_size;
+    hipError_t e = launch_parse_wire(a, s);
+    if (e != hipSuccess) return hip_fail(e, "parse_wire launch");
+    // decode the missing data shards from the first k valid ones in group order
+    // (network/NetFecCodec.cpp:504-528 == module/rs.c:620-629)
+    if ((rc = run_reconstruct(*ctx, code, d->d_lut, nullptr, d->d_rec, d_shards, d_shards + (size_t)k * shard_pitch,
+                              d_marks, groups, (int)shard_pitch, shard_pitch, nullptr, s, (long long)a.group_stride,
+                              (long long)a.group_stride)))
+        return rc;
+    e = launch_check_payloads(a, s);
+    return e == hipSuccess ? QFEC_OK : hip_fail(e, "check_payloads launch");
 }
 
 }  // extern "C"
