@@ -124,7 +124,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
                       int block_size, long long pitch, void *stream);
 
 /* Experiment knobs for interleaved A/B timing (tools/ab.py): "encode_impl" 0|1,
- * "recon_impl" -1 (auto) | 0 | 1.  Defaults are the measured best; results are identical. */
+ * "recon_impl" -1 (auto) | 0 | 1, "wire_fused" 1 (one-kernel datagram send where a (k, m)
+ * instance exists) | 0 (staged build -> encode -> emit).  Defaults are the measured best; results are identical. */
 int qfec_tune(const char *key, int value);
 
 int qfec_set_kernel_variant(int variant);

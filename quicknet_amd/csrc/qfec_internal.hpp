@@ -89,6 +89,9 @@ struct WireArgs {
 };
 
 hipError_t launch_build_shards(const WireArgs& a, hipStream_t s);
+// fused send path for templated (k, m); *launched = false when the shape has no instance
+// `part` = scratch of (lpg / 16) * ((n + 1) / 2) u32 per group, lpg ~ (pitch + 13) / 16
+hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s, bool* launched);
 hipError_t launch_emit_wire(const WireArgs& a, hipStream_t s);
 hipError_t launch_parse_wire(const WireArgs& a, hipStream_t s);
 hipError_t launch_check_payloads(const WireArgs& a, hipStream_t s);
@@ -97,6 +100,8 @@ hipError_t launch_check_payloads(const WireArgs& a, hipStream_t s);
 struct Tuning {
     int recon_impl = -1;  // -1 auto (per shape), 0 row loop, 1 all rows
     int encode_impl = 0;
+    int wire_fused = 1;
+    int wire_wpe = 1;     // experiment: waves-per-EU floor of the fused send body (1 | 4)   // fused one-kernel datagram paths where a (k, m) instance exists
 };
 Tuning& tuning();
 

@@ -493,6 +493,8 @@ int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
     if (!strcmp(key, "recon_impl") && value >= -1 && value <= 1) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_wpe") && (value == 1 || value == 4)) { tuning().wire_wpe = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
 }
@@ -691,6 +693,14 @@ int qfec_pack_datagrams(qfec_code* code, const unsigned char* d_payload, const l
     a.k = k;
     a.m = m;
     a.checksum = checksum;
+    if (tuning().wire_fused) {
+        bool launched = false;
+        // the fused path never materialises shards; their buffer holds its partial sums
+        // ((pitch + 13) / 256 + 1) * 8 u32 per group  <<  n * pitch bytes
+        hipError_t e = launch_pack_fused(a, tab, reinterpret_cast<uint32_t*>(d_shards), s, &launched);
+        if (e != hipSuccess) return hip_fail(e, "pack_fused launch");
+        if (launched) return QFEC_OK;
+    }
     hipError_t e = launch_build_shards(a, s);
     if (e != hipSuccess) return hip_fail(e, "build_shards launch");
     // check shards: fec_encode(.., groupMax) over the k data shards (FecCodecBuf.cpp:151);

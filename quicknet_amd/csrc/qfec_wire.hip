@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
+#include "qfec_device.hpp"
 #include "qfec_internal.hpp"
 
 namespace qfec {
@@ -164,7 +167,16 @@ __global__ void __launch_bounds__(256) k_emit_wire(WireArgs a) {
     const int j = (int)(slot - g * (uint32_t)n);
     const int head = a.checksum ? 4 : 2;
     int gmax = 0;
-    for (int i = 0; i < a.k; ++i) gmax = max(gmax, a.sizes[g * a.k + i] + head);
+    bool ok = true;
+    for (int i = 0; i < a.k; ++i) {
+        const int sz = a.sizes[g * a.k + i];
+        ok = ok && sz >= 0 && sz + head <= (int)a.pitch;
+        gmax = max(gmax, sz + head);
+    }
+    if (!ok) {  // a size the shard pitch cannot hold: the group is not packed
+        if (lane == 0) a.wire_len[slot] = -1;
+        return;
+    }
     const int len = j < a.k ? a.sizes[g * a.k + j] + head : gmax;
     const uint8_t* sh = a.shards + g * a.group_stride + (uint64_t)j * a.pitch;
     uint8_t* out = a.wire + slot * a.wire_pitch;
@@ -295,6 +307,231 @@ __global__ void __launch_bounds__(256) k_check_payloads(WireArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ send: fused
+// Two launches for compile-time (K, M) replace build -> encode -> emit, so the
+// [G][n][pitch] shard matrix never exists: HBM traffic is the payload in and the
+// datagrams out.  GF arithmetic is bytewise, so check-shard bytes at any shard offset
+// come from the data-shard bytes at the same offset; each lane therefore works on one
+// 16-B DATAGRAM chunk t = shard bytes [16t - HDR, 16t + 16 - HDR) of all n rows at once,
+// with no neighbour exchange.
+//  k_pack_body   lanes for t >= 2, flat over (group, t), lpg lanes per group (a multiple
+//                of 16): data chunks are straight payload loads; it stores all n datagram
+//                chunks and 16-lane partial byte sums (two rows per u32) into `part`.
+//  k_pack_head   two lanes per group for t = 0, 1: the only chunks that hold shard bytes
+//                0-3 (size, payload checksum) and the datagram header with its checksum,
+//                both of which need the whole group's sums.
+template <int K, int M>
+__device__ __forceinline__ void encode_col(const uint4 (&x)[K], uint4 (&acc)[M], const uint32_t* __restrict__ tab) {
+#pragma unroll
+    for (int r = 0; r < M; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c + 1 < K; c += 2) {
+        Sel sa[4], sb[4];
+        sel16(sa, x[c]);
+        sel16(sb, x[c + 1]);
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+            gf_mac16x2(acc[r], sa, sb, tab + (r * K + c) * QFEC_TAB_STRIDE, tab + (r * K + c + 1) * QFEC_TAB_STRIDE);
+    }
+    if (K & 1) {
+        Sel sl[4];
+        sel16(sl, x[K - 1]);
+#pragma unroll
+        for (int r = 0; r < M; ++r) gf_mac16(acc[r], sl, tab + (r * K + K - 1) * QFEC_TAB_STRIDE);
+    }
+}
+
+// sum over each aligned 16-lane row, result in every lane of the row (DPP, no LDS)
+__device__ __forceinline__ uint32_t row16_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return v;
+}
+// v + the value of lane ^ 1
+__device__ __forceinline__ uint32_t pair_sum(uint32_t v) {
+    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+}
+
+// A group is packed only if every size is in [0, shard_pitch - head]; otherwise its n
+// wire_len entries are -1 and none of its datagram bytes are written.
+template <int K, int HEAD>
+__device__ __forceinline__ bool group_sizes(const int32_t* __restrict__ sizes, uint64_t g, int pitch, int (&size)[K],
+                                            int& gmax) {
+    bool ok = true;
+    gmax = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        size[i] = sizes[g * K + i];
+        ok = ok && size[i] >= 0 && size[i] + HEAD <= pitch;
+        gmax = max(gmax, size[i] + HEAD);
+    }
+    return ok;
+}
+
+template <int K, int M, int HDR, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_pack_body(WireArgs a, const uint8_t* __restrict__ payload,
+                                                   const int64_t* __restrict__ offsets,
+                                                   const int32_t* __restrict__ sizes,
+                                                   const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
+                                                   uint64_t g0, uint32_t lanes, uint32_t lpg, DivMagic rows_div) {
+    constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
+    const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
+    const bool live = flat < lanes;  // whole 16-lane rows are live or not: lanes % 16 == 0
+    const uint32_t gl = live ? (uint32_t)fast_div(flat >> 4, rows_div) : 0;
+    const uint32_t rem = flat - gl * lpg;
+    const uint64_t g = g0 + gl;
+    const int t = 2 + (int)rem;
+    const int p = 16 * t - HDR - HEAD;  // payload offset of this chunk's first byte (>= 32 - 17)
+    int size[K], gmax = 0;
+    bool act = false;
+    if (live) act = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax) && 16 * t < HDR + gmax;
+    uint8_t* out = a.wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
+    uint32_t ps[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) ps[q] = 0;
+    uint4 acc[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) acc[r] = make_uint4(0, 0, 0, 0);
+    auto data_chunk = [&](int i) -> uint4 {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (act && p < size[i]) {
+            v = mask16(ldu16(payload + offsets[g * K + i] + p), 0, size[i] - p);
+            st16(out + (uint64_t)i * a.wire_pitch, v);
+        }
+        const uint32_t s = sum16(v, 0);
+        ps[i >> 1] += (i & 1) ? s << 16 : s;
+        return v;
+    };
+#pragma unroll
+    for (int c = 0; c + 1 < K; c += 2) {
+        const uint4 x0 = data_chunk(c), x1 = data_chunk(c + 1);
+        Sel sa[4], sb[4];
+        sel16(sa, x0);
+        sel16(sb, x1);
+#pragma unroll
+        for (int r = 0; r < M; ++r)
+            gf_mac16x2(acc[r], sa, sb, tab + (r * K + c) * QFEC_TAB_STRIDE, tab + (r * K + c + 1) * QFEC_TAB_STRIDE);
+    }
+    if (K & 1) {
+        const uint4 x = data_chunk(K - 1);
+        Sel sl[4];
+        sel16(sl, x);
+#pragma unroll
+        for (int r = 0; r < M; ++r) gf_mac16(acc[r], sl, tab + (r * K + K - 1) * QFEC_TAB_STRIDE);
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        // check-shard bytes past groupMax are zero: every data chunk is zero there
+        if (act) st16(out + (uint64_t)(K + j) * a.wire_pitch, acc[j]);
+        const uint32_t s = sum16(acc[j], 0);
+        ps[(K + j) >> 1] += ((K + j) & 1) ? s << 16 : s;
+    }
+    // per-lane sums are <= 16 * 255, a 16-lane row's <= 65280: two rows share a u32 exactly
+    const uint32_t R = lpg >> 4;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        const uint32_t v = row16_sum(ps[q]);
+        if (live && (flat & 15) == 0) part[(g * R + (rem >> 4)) * P + q] = v;
+    }
+}
+
+template <int K, int M, int HDR>
+__global__ void __launch_bounds__(256) k_pack_head(WireArgs a, const uint8_t* __restrict__ payload,
+                                                   const int64_t* __restrict__ offsets,
+                                                   const int32_t* __restrict__ sizes,
+                                                   const uint32_t* __restrict__ tab,
+                                                   const uint32_t* __restrict__ part, uint64_t g0, uint32_t lanes,
+                                                   uint32_t lpg) {
+    constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
+    const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
+    const bool live = flat < lanes;  // lanes is even: both lanes of a pair agree
+    const uint64_t g = g0 + (flat >> 1);
+    const int t = (int)(flat & 1);
+    int size[K], gmax = 0;
+    bool ok = false;
+    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+    // this lane's datagram chunk of every data row, checksum bytes still zero
+    uint4 dw[K];
+    uint32_t psum[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = make_uint4(0, 0, 0, 0);
+        if (ok) {
+            const uint8_t* src = payload + offsets[g * K + i];
+            if (size[i] > 0) c0 = mask16(window(make_uint4(0, 0, 0, 0), ldu16(src), 16 - HEAD), HEAD, HEAD + size[i]);
+            put_byte(c0, 0, (uint32_t)size[i]);
+            put_byte(c0, 1, (uint32_t)size[i] >> 8);
+            if (t == 1 && 16 - HEAD < size[i]) c1 = mask16(ldu16(src + 16 - HEAD), 0, size[i] - (16 - HEAD));
+        }
+        const int len = size[i] + HEAD;
+        dw[i] = t == 0 ? mask16(window(make_uint4(0, 0, 0, 0), c0, 16 - HDR), HDR, HDR + len)
+                       : mask16(window(c0, c1, 16 - HDR), 0, HDR + len - 16);
+        psum[i] = sum16(dw[i], 0) - (t == 0 ? ((uint32_t)size[i] & 0xFF) + (((uint32_t)size[i] >> 8) & 0xFF) : 0u);
+    }
+    uint32_t tot[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) tot[r] = 0;
+    if (ok) {
+        const uint32_t R = lpg >> 4;
+        for (uint32_t rr = 0; rr < R; ++rr) {
+#pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const uint32_t v = part[(g * R + rr) * P + q];
+                tot[2 * q] += v & 0xFFFF;
+                if (2 * q + 1 < N) tot[2 * q + 1] += v >> 16;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        psum[i] = (pair_sum(psum[i]) + tot[i]) & 0xFFFF;
+        if (HEAD == 4) put_byte(dw[i], t == 0 ? 15 : 0, t == 0 ? psum[i] : psum[i] >> 8);  // shard bytes 2, 3
+    }
+    uint4 pw[M];
+    encode_col<K, M>(dw, pw, tab);
+    uint32_t qsum[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) qsum[j] = (pair_sum(sum16(pw[j], 0)) + tot[K + j]) & 0xFFFF;
+    if (!live) return;
+    uint8_t* out = a.wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        const int len = r < K ? size[r] + HEAD : gmax;
+        uint4 v = r < K ? dw[r] : pw[r - K];
+        if (t == 0) {
+            if (!ok) {
+                a.wire_len[g * N + r] = -1;
+                continue;
+            }
+            const uint32_t sent = a.seq[2 * g] + (uint32_t)r;
+            const uint32_t srcno = a.seq[2 * g + 1] + (uint32_t)(r < K ? r : K - 1);
+            const uint32_t ikn = ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu;
+            put_byte(v, 0, HDR == 13 ? 0xED : 0xEC);
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                put_byte(v, 1 + b, sent >> (8 * b));
+                put_byte(v, 5 + b, srcno >> (8 * b));
+            }
+            put_byte(v, 9, ikn);
+            put_byte(v, 10, ikn >> 8);
+            if (HDR == 13) {
+                // datagram checksum: byte sum of shard [0, len)
+                const uint32_t d = r < K ? psum[r] + ((uint32_t)size[r] & 0xFF) + (((uint32_t)size[r] >> 8) & 0xFF) +
+                                               (psum[r] & 0xFF) + (psum[r] >> 8)
+                                         : qsum[r - K];
+                put_byte(v, 11, d);
+                put_byte(v, 12, d >> 8);
+            }
+            st16(out + (uint64_t)r * a.wire_pitch, v);
+            a.wire_len[g * N + r] = HDR + len;
+        } else if (ok && 16 < HDR + len) {
+            st16(out + (uint64_t)r * a.wire_pitch, v);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 static inline unsigned waves_grid(uint64_t waves) { return (unsigned)((waves + 3) / 4); }
 
@@ -304,6 +541,54 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_build_shards, dim3(waves_grid(rows)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
+
+template <int K, int M, int HDR>
+hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s) {
+    // lanes per group for t >= 2 cover the longest datagram the shard pitch allows
+    const uint32_t tn = (uint32_t)((HDR + a.pitch + 15) / 16);
+    const uint32_t lpg = std::max(16u, (tn - 2 + 15) / 16 * 16);
+    const DivMagic rows_div = make_div_magic(lpg / 16);
+    const uint64_t per = ((uint64_t)1 << 30) / lpg;  // groups per launch: lanes < 2^30
+    for (uint64_t g0 = 0; g0 < a.groups; g0 += per) {
+        const uint64_t gn = std::min(per, a.groups - g0);
+        const uint32_t lanes = (uint32_t)(gn * lpg);
+        if (tuning().wire_wpe == 4)
+            hipLaunchKernelGGL((k_pack_body<K, M, HDR, 4>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
+                               a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
+        else
+            hipLaunchKernelGGL((k_pack_body<K, M, HDR, 1>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
+                               a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
+        const uint32_t hl = (uint32_t)(2 * gn);
+        hipLaunchKernelGGL((k_pack_head<K, M, HDR>), dim3((hl + 255) / 256), dim3(256), 0, s, a, a.payload, a.offsets,
+                           a.sizes, tab, (const uint32_t*)part, g0, hl, lpg);
+    }
+    return hipGetLastError();
+}
+
+#define QFEC_PACK_CASE(KK, MM)                                                                              \
+    if (a.k == KK && a.m == MM) {                                                                           \
+        *launched = true;                                                                                   \
+        return a.checksum ? pack_fused_shape<KK, MM, 13>(a, tab, part, s)                                   \
+                          : pack_fused_shape<KK, MM, 11>(a, tab, part, s);                                  \
+    }
+
+// `part` needs pack_part_words(pitch, n) u32 per group; the caller's shard buffer holds it
+hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s, bool* launched) {
+    *launched = false;
+    if (!a.groups) return hipSuccess;
+    QFEC_PACK_CASE(10, 3)
+    QFEC_PACK_CASE(4, 1)
+    QFEC_PACK_CASE(4, 2)
+    QFEC_PACK_CASE(2, 2)
+    QFEC_PACK_CASE(3, 1)
+    QFEC_PACK_CASE(3, 2)
+    QFEC_PACK_CASE(5, 1)
+    QFEC_PACK_CASE(5, 3)
+    QFEC_PACK_CASE(7, 1)
+    QFEC_PACK_CASE(8, 4)
+    return hipSuccess;
+}
+#undef QFEC_PACK_CASE
 
 hipError_t launch_emit_wire(const WireArgs& a, hipStream_t s) {
     const uint64_t slots = a.groups * (uint64_t)(a.k + a.m);

@@ -24,9 +24,18 @@ def padded_payload(p):
     return dev(np.concatenate([p, np.zeros(16, np.uint8)]))  # 16 readable bytes past the end
 
 
+@pytest.fixture(params=[1, 0], ids=["fused", "staged"])
+def wire_fused(request):
+    """Both send paths: the one-kernel fused pack (templated (k, m)) and the staged
+    build -> encode -> emit pipeline every shape can take."""
+    qa.tune("wire_fused", request.param)
+    yield request.param
+    qa.tune("wire_fused", 1)
+
+
 @pytest.mark.parametrize("k,n", WIRE)
 @pytest.mark.parametrize("checksum", [1, 0])
-def test_pack_vs_reference(golden, k, n, checksum):
+def test_pack_vs_reference(golden, wire_fused, k, n, checksum):
     z = golden("wire.npz")
     key = f"{k}_{n}_{checksum}"
     sizes, payload, seq = z[f"sizes_{key}"], z[f"payload_{key}"], z[f"seq_{key}"]
@@ -80,7 +89,7 @@ def test_unpack_vs_reference(golden, k, n, checksum):
 
 
 @pytest.mark.parametrize("k,n,checksum", [(10, 13, 1), (4, 6, 1), (14, 15, 0), (5, 8, 1)])
-def test_lossy_roundtrip_vs_oracle(oracle, k, n, checksum):
+def test_lossy_roundtrip_vs_oracle(oracle, wire_fused, k, n, checksum):
     """Pack G groups, drop and corrupt datagrams, unpack: every data packet comes back exactly
     when its group has k valid datagrams; the verdicts match the reference rules (oracle)."""
     rng = np.random.default_rng(k * 100 + n)
@@ -131,3 +140,22 @@ def test_lossy_roundtrip_vs_oracle(oracle, k, n, checksum):
             sz = sizes[g * k + i]
             assert psize[g, i] == sz
             assert np.array_equal(sh[g, i, head:head + sz], payload[offs[g * k + i]:offs[g * k + i] + sz])
+
+
+def test_pack_oversize_group(wire_fused):
+    """A size the shard pitch cannot hold (or a negative one) voids its group only:
+    wire_len -1 for its n datagrams, the other groups are packed as usual."""
+    k, n, G = 4, 6, 6
+    sizes = np.full(G * k, 100, np.int32)
+    sizes[1 * k + 2] = 125  # 125 + 4 > 128
+    sizes[4 * k + 0] = -3
+    payload = np.arange(int(np.maximum(sizes, 0).sum()) + 1, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(np.maximum(sizes, 0))[:-1]]).astype(np.int64)
+    seq = np.zeros((G, 2), np.uint32)
+    code = qa.Code.vandermonde(k, n - k)
+    _, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq), True, shard_pitch=128)
+    torch.cuda.synchronize()
+    wl = wlen.cpu().numpy()
+    assert (wl[1] == -1).all() and (wl[4] == -1).all()
+    good = [0, 2, 3, 5]
+    assert (wl[good, :k] == 13 + 104).all() and (wl[good, k:] == 13 + 104).all()
