@@ -86,6 +86,7 @@ struct WireArgs {
     int k, m;
     int checksum;
     int dec_pkt_size;
+    int store_nt;             // fused send: bit 0 body, bit 1 head use non-temporal stores
 };
 
 hipError_t launch_build_shards(const WireArgs& a, hipStream_t s);
@@ -101,7 +102,9 @@ struct Tuning {
     int recon_impl = -1;  // -1 auto (per shape), 0 row loop, 1 all rows
     int encode_impl = 0;
     int wire_fused = 1;
-    int wire_wpe = 1;     // experiment: waves-per-EU floor of the fused send body (1 | 4)   // fused one-kernel datagram paths where a (k, m) instance exists
+    int wire_store_nt = 3; // fused send datagram stores: bit 0 body, bit 1 head non-temporal
+    int wire_uni = 1;     // fused send body: 0 per-lane groups, 1 wave-uniform when lpg % 64 == 0,
+                          // 2 wave-uniform always (lpg rounded up to 64)   // fused one-kernel datagram paths where a (k, m) instance exists
 };
 Tuning& tuning();
 

@@ -493,8 +493,9 @@ int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
     if (!strcmp(key, "recon_impl") && value >= -1 && value <= 1) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_wpe") && (value == 1 || value == 4)) { tuning().wire_wpe = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_uni") && value >= 0 && value <= 2) { tuning().wire_uni = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_fused") && value >= 0 && value <= 2) { tuning().wire_fused = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
 }
@@ -693,6 +694,7 @@ int qfec_pack_datagrams(qfec_code* code, const unsigned char* d_payload, const l
     a.k = k;
     a.m = m;
     a.checksum = checksum;
+    a.store_nt = tuning().wire_store_nt;
     if (tuning().wire_fused) {
         bool launched = false;
         // the fused path never materialises shards; their buffer holds its partial sums

@@ -81,6 +81,17 @@ __device__ __forceinline__ uint32_t get_byte(const uint4& v, int pos) {
     return (w >> (8 * (pos & 3))) & 0xFFu;
 }
 
+// datagram store: non-temporal or write-back (tuning "wire_store_nt"), wave-uniform flag
+__device__ __forceinline__ void stw(uint8_t* p, const uint4& v, int nt) {
+    if (nt) st16(p, v);
+    else st16a(p, v);
+}
+
+// c ? a : b per dword (a ?: on the struct is lowered through scratch memory)
+__device__ __forceinline__ uint4 pick16(bool c, const uint4& a, const uint4& b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
 // bytes [s, s + 16) of the 32-byte window (a | b), s in [0, 16)
 __device__ __forceinline__ uint4 window(const uint4& a, const uint4& b, int s) {
     const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -370,61 +381,65 @@ __device__ __forceinline__ bool group_sizes(const int32_t* __restrict__ sizes, u
     return ok;
 }
 
-template <int K, int M, int HDR, int WPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) k_pack_body(WireArgs a, const uint8_t* __restrict__ payload,
-                                                   const int64_t* __restrict__ offsets,
-                                                   const int32_t* __restrict__ sizes,
-                                                   const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
-                                                   uint64_t g0, uint32_t lanes, uint32_t lpg, DivMagic rows_div) {
+// UNI: lpg is a multiple of 64, so a wave never straddles groups and the group's sizes,
+// offsets and row addresses are wave-uniform (SGPRs); otherwise per lane.
+// One lane of the body: datagram chunk t = 2 + rem of group g (live: g exists).  PART_SC1:
+// write the partial sums write-through (agent scope), for a same-launch reader.
+template <int K, int M, int HDR, bool PART_SC1>
+__device__ __forceinline__ void body_lane(const WireArgs& a, const uint8_t* __restrict__ payload,
+                                          const int64_t* __restrict__ offsets, const int32_t* __restrict__ sizes,
+                                          const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
+                                          uint64_t g, uint32_t rem, bool live, uint32_t lpg) {
     constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
-    const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
-    const bool live = flat < lanes;  // whole 16-lane rows are live or not: lanes % 16 == 0
-    const uint32_t gl = live ? (uint32_t)fast_div(flat >> 4, rows_div) : 0;
-    const uint32_t rem = flat - gl * lpg;
-    const uint64_t g = g0 + gl;
     const int t = 2 + (int)rem;
     const int p = 16 * t - HDR - HEAD;  // payload offset of this chunk's first byte (>= 32 - 17)
     int size[K], gmax = 0;
-    bool act = false;
-    if (live) act = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax) && 16 * t < HDR + gmax;
+    bool ok = false;
+    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+    const bool act = ok && 16 * t < HDR + gmax;
     uint8_t* out = a.wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
+    // all K loads back to back (no per-row branch in between): the address is clamped to
+    // the packet's end, whose 16 following bytes are readable by contract, and masked after
+    uint4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
+    if (ok) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + offsets[g * K + i] + min(p, size[i]));
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = mask16(x[i], 0, size[i] - p);
+    }
     uint32_t ps[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) ps[q] = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        if (act && p < size[i]) stw(out + (uint64_t)i * a.wire_pitch, x[i], a.store_nt & 1);
+        const uint32_t s = sum16(x[i], 0);
+        ps[i >> 1] += (i & 1) ? s << 16 : s;
+    }
     uint4 acc[M];
 #pragma unroll
     for (int r = 0; r < M; ++r) acc[r] = make_uint4(0, 0, 0, 0);
-    auto data_chunk = [&](int i) -> uint4 {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (act && p < size[i]) {
-            v = mask16(ldu16(payload + offsets[g * K + i] + p), 0, size[i] - p);
-            st16(out + (uint64_t)i * a.wire_pitch, v);
-        }
-        const uint32_t s = sum16(v, 0);
-        ps[i >> 1] += (i & 1) ? s << 16 : s;
-        return v;
-    };
 #pragma unroll
     for (int c = 0; c + 1 < K; c += 2) {
-        const uint4 x0 = data_chunk(c), x1 = data_chunk(c + 1);
         Sel sa[4], sb[4];
-        sel16(sa, x0);
-        sel16(sb, x1);
+        sel16(sa, x[c]);
+        sel16(sb, x[c + 1]);
 #pragma unroll
         for (int r = 0; r < M; ++r)
             gf_mac16x2(acc[r], sa, sb, tab + (r * K + c) * QFEC_TAB_STRIDE, tab + (r * K + c + 1) * QFEC_TAB_STRIDE);
     }
     if (K & 1) {
-        const uint4 x = data_chunk(K - 1);
         Sel sl[4];
-        sel16(sl, x);
+        sel16(sl, x[K - 1]);
 #pragma unroll
         for (int r = 0; r < M; ++r) gf_mac16(acc[r], sl, tab + (r * K + K - 1) * QFEC_TAB_STRIDE);
     }
 #pragma unroll
     for (int j = 0; j < M; ++j) {
         // check-shard bytes past groupMax are zero: every data chunk is zero there
-        if (act) st16(out + (uint64_t)(K + j) * a.wire_pitch, acc[j]);
+        if (act) stw(out + (uint64_t)(K + j) * a.wire_pitch, acc[j], a.store_nt & 1);
         const uint32_t s = sum16(acc[j], 0);
         ps[(K + j) >> 1] += ((K + j) & 1) ? s << 16 : s;
     }
@@ -433,7 +448,138 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 #pragma unroll
     for (int q = 0; q < P; ++q) {
         const uint32_t v = row16_sum(ps[q]);
-        if (live && (flat & 15) == 0) part[(g * R + (rem >> 4)) * P + q] = v;
+        if (live && (rem & 15) == 0) {
+            uint32_t* dst = part + (g * R + (rem >> 4)) * P + q;
+            if (PART_SC1) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else *dst = v;
+        }
+    }
+}
+
+template <int K, int M, int HDR, bool UNI>
+__global__ void __launch_bounds__(256) k_pack_body(WireArgs a, const uint8_t* __restrict__ payload,
+                                                   const int64_t* __restrict__ offsets,
+                                                   const int32_t* __restrict__ sizes,
+                                                   const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
+                                                   uint64_t g0, uint32_t lanes, uint32_t lpg, DivMagic rows_div) {
+    const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
+    const bool live = flat < lanes;  // whole 16-lane rows (UNI: waves) are live or not
+    uint32_t gl;
+    if (UNI) {
+        if (!live) return;
+        gl = __builtin_amdgcn_readfirstlane((uint32_t)fast_div(flat >> 6, rows_div));
+    } else {
+        gl = live ? (uint32_t)fast_div(flat >> 4, rows_div) : 0;
+    }
+    body_lane<K, M, HDR, false>(a, payload, offsets, sizes, tab, part, g0 + gl, flat - gl * lpg, live, lpg);
+}
+
+// One lane of the head: datagram chunk t (0 or 1) of group g; lanes 2j, 2j + 1 are a pair
+// (same g, same `live`).  PART_SC1: read the partial sums write-through (agent scope).
+template <int K, int M, int HDR, bool PART_SC1>
+__device__ __forceinline__ void head_lane(const WireArgs& a, const uint8_t* __restrict__ payload,
+                                          const int64_t* __restrict__ offsets, const int32_t* __restrict__ sizes,
+                                          const uint32_t* __restrict__ tab, const uint32_t* __restrict__ part,
+                                          const uint32_t* __restrict__ seq, uint8_t* __restrict__ wire,
+                                          int32_t* __restrict__ wire_len, uint64_t g, int t, bool live, uint32_t lpg) {
+    constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
+    int size[K], gmax = 0;
+    bool ok = false;
+    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+    // every global load up front, addresses clamped to the packet (+16 readable bytes)
+    uint4 raw0[K], raw1[K];
+    uint32_t tot[N], sent0 = 0, src0 = 0;
+#pragma unroll
+    for (int r = 0; r < N; ++r) tot[r] = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) raw0[i] = raw1[i] = make_uint4(0, 0, 0, 0);
+    if (ok) {
+        sent0 = seq[2 * g];
+        src0 = seq[2 * g + 1];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const uint8_t* src = payload + offsets[g * K + i];
+            raw0[i] = ldu16(src);
+            raw1[i] = ldu16(src + min(16 - HEAD, size[i]));
+        }
+        // the body's 16-lane partial sums: R = lpg / 16 rows of P words
+        const uint32_t R = lpg >> 4;
+        const uint32_t* pg = part + g * R * P;
+        for (uint32_t r0 = 0; r0 < R; r0 += 4) {
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t rr = min(r0 + u, R - 1), use = r0 + u < R;
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    uint32_t v = 0;
+                    if (use)
+                        v = PART_SC1 ? __hip_atomic_load(pg + rr * P + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : pg[rr * P + q];
+                    tot[2 * q] += v & 0xFFFF;
+                    if (2 * q + 1 < N) tot[2 * q + 1] += v >> 16;
+                }
+            }
+        }
+    }
+    // this lane's datagram chunk of every data row (t = 0: shard bytes [0, 16 - HDR) after
+    // the header; t = 1: shard bytes [16 - HDR, 32 - HDR)), checksum bytes still zero
+    uint4 dw[K];
+    uint32_t psum[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        uint4 c0 = mask16(window(make_uint4(0, 0, 0, 0), raw0[i], 16 - HEAD), HEAD, HEAD + size[i]);
+        put_byte(c0, 0, (uint32_t)size[i]);
+        put_byte(c0, 1, (uint32_t)size[i] >> 8);
+        const uint4 c1 = mask16(raw1[i], 0, size[i] - (16 - HEAD));
+        const int len = size[i] + HEAD;
+        const uint4 d0 = mask16(window(make_uint4(0, 0, 0, 0), c0, 16 - HDR), HDR, HDR + len);
+        const uint4 d1 = mask16(window(c0, c1, 16 - HDR), 0, HDR + len - 16);
+        dw[i] = pick16(t == 0, d0, d1);
+        psum[i] = sum16(dw[i], 0) - (t == 0 ? ((uint32_t)size[i] & 0xFF) + (((uint32_t)size[i] >> 8) & 0xFF) : 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        psum[i] = (pair_sum(psum[i]) + tot[i]) & 0xFFFF;
+        if (HEAD == 4) {  // shard bytes 2, 3: datagram chunk 0 byte 15, chunk 1 byte 0
+            uint4 p0 = dw[i], p1 = dw[i];
+            put_byte(p0, 15, psum[i]);
+            put_byte(p1, 0, psum[i] >> 8);
+            dw[i] = pick16(t == 0, p0, p1);
+        }
+    }
+    uint4 pw[M];
+    encode_col<K, M>(dw, pw, tab);
+    uint32_t qsum[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) qsum[j] = (pair_sum(sum16(pw[j], 0)) + tot[K + j]) & 0xFFFF;
+    if (!live) return;
+    uint8_t* out = wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        const int len = r < K ? size[r] + HEAD : gmax;
+        const uint4 v = r < K ? dw[r] : pw[r - K];
+        uint4 h = v;
+        const uint32_t sent = sent0 + (uint32_t)r;
+        const uint32_t srcno = src0 + (uint32_t)(r < K ? r : K - 1);
+        const uint32_t ikn = ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu;
+        put_byte(h, 0, HDR == 13 ? 0xED : 0xEC);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            put_byte(h, 1 + b, sent >> (8 * b));
+            put_byte(h, 5 + b, srcno >> (8 * b));
+        }
+        put_byte(h, 9, ikn);
+        put_byte(h, 10, ikn >> 8);
+        if (HDR == 13) {
+            // datagram checksum: byte sum of shard [0, len)
+            const uint32_t d = r < K ? psum[r] + ((uint32_t)size[r] & 0xFF) + (((uint32_t)size[r] >> 8) & 0xFF) +
+                                           (psum[r] & 0xFF) + (psum[r] >> 8)
+                                     : qsum[r - K];
+            put_byte(h, 11, d);
+            put_byte(h, 12, d >> 8);
+        }
+        if (ok && (t == 0 || 16 < HDR + len)) stw(out + (uint64_t)r * a.wire_pitch, pick16(t == 0, h, v), a.store_nt & 2);
+        if (t == 0) wire_len[g * N + r] = ok ? HDR + len : -1;
     }
 }
 
@@ -442,93 +588,49 @@ __global__ void __launch_bounds__(256) k_pack_head(WireArgs a, const uint8_t* __
                                                    const int64_t* __restrict__ offsets,
                                                    const int32_t* __restrict__ sizes,
                                                    const uint32_t* __restrict__ tab,
-                                                   const uint32_t* __restrict__ part, uint64_t g0, uint32_t lanes,
+                                                   const uint32_t* __restrict__ part,
+                                                   const uint32_t* __restrict__ seq, uint8_t* __restrict__ wire,
+                                                   int32_t* __restrict__ wire_len, uint64_t g0, uint32_t lanes,
                                                    uint32_t lpg) {
-    constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
     const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
-    const bool live = flat < lanes;  // lanes is even: both lanes of a pair agree
-    const uint64_t g = g0 + (flat >> 1);
-    const int t = (int)(flat & 1);
-    int size[K], gmax = 0;
-    bool ok = false;
-    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
-    // this lane's datagram chunk of every data row, checksum bytes still zero
-    uint4 dw[K];
-    uint32_t psum[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        uint4 c0 = make_uint4(0, 0, 0, 0), c1 = make_uint4(0, 0, 0, 0);
-        if (ok) {
-            const uint8_t* src = payload + offsets[g * K + i];
-            if (size[i] > 0) c0 = mask16(window(make_uint4(0, 0, 0, 0), ldu16(src), 16 - HEAD), HEAD, HEAD + size[i]);
-            put_byte(c0, 0, (uint32_t)size[i]);
-            put_byte(c0, 1, (uint32_t)size[i] >> 8);
-            if (t == 1 && 16 - HEAD < size[i]) c1 = mask16(ldu16(src + 16 - HEAD), 0, size[i] - (16 - HEAD));
-        }
-        const int len = size[i] + HEAD;
-        dw[i] = t == 0 ? mask16(window(make_uint4(0, 0, 0, 0), c0, 16 - HDR), HDR, HDR + len)
-                       : mask16(window(c0, c1, 16 - HDR), 0, HDR + len - 16);
-        psum[i] = sum16(dw[i], 0) - (t == 0 ? ((uint32_t)size[i] & 0xFF) + (((uint32_t)size[i] >> 8) & 0xFF) : 0u);
-    }
-    uint32_t tot[N];
-#pragma unroll
-    for (int r = 0; r < N; ++r) tot[r] = 0;
-    if (ok) {
-        const uint32_t R = lpg >> 4;
-        for (uint32_t rr = 0; rr < R; ++rr) {
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const uint32_t v = part[(g * R + rr) * P + q];
-                tot[2 * q] += v & 0xFFFF;
-                if (2 * q + 1 < N) tot[2 * q + 1] += v >> 16;
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        psum[i] = (pair_sum(psum[i]) + tot[i]) & 0xFFFF;
-        if (HEAD == 4) put_byte(dw[i], t == 0 ? 15 : 0, t == 0 ? psum[i] : psum[i] >> 8);  // shard bytes 2, 3
-    }
-    uint4 pw[M];
-    encode_col<K, M>(dw, pw, tab);
-    uint32_t qsum[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) qsum[j] = (pair_sum(sum16(pw[j], 0)) + tot[K + j]) & 0xFFFF;
-    if (!live) return;
-    uint8_t* out = a.wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-        const int len = r < K ? size[r] + HEAD : gmax;
-        uint4 v = r < K ? dw[r] : pw[r - K];
-        if (t == 0) {
-            if (!ok) {
-                a.wire_len[g * N + r] = -1;
-                continue;
-            }
-            const uint32_t sent = a.seq[2 * g] + (uint32_t)r;
-            const uint32_t srcno = a.seq[2 * g + 1] + (uint32_t)(r < K ? r : K - 1);
-            const uint32_t ikn = ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu;
-            put_byte(v, 0, HDR == 13 ? 0xED : 0xEC);
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                put_byte(v, 1 + b, sent >> (8 * b));
-                put_byte(v, 5 + b, srcno >> (8 * b));
-            }
-            put_byte(v, 9, ikn);
-            put_byte(v, 10, ikn >> 8);
-            if (HDR == 13) {
-                // datagram checksum: byte sum of shard [0, len)
-                const uint32_t d = r < K ? psum[r] + ((uint32_t)size[r] & 0xFF) + (((uint32_t)size[r] >> 8) & 0xFF) +
-                                               (psum[r] & 0xFF) + (psum[r] >> 8)
-                                         : qsum[r - K];
-                put_byte(v, 11, d);
-                put_byte(v, 12, d >> 8);
-            }
-            st16(out + (uint64_t)r * a.wire_pitch, v);
-            a.wire_len[g * N + r] = HDR + len;
-        } else if (ok && 16 < HDR + len) {
-            st16(out + (uint64_t)r * a.wire_pitch, v);
-        }
+    head_lane<K, M, HDR, false>(a, payload, offsets, sizes, tab, part, seq, wire, wire_len, g0 + (flat >> 1),
+                                (int)(flat & 1), flat < lanes, lpg);
+}
+
+// One launch: body lanes in batches of 8 blocks dealt to one XCD (blocks b, b + 8, ...,
+// b + 56 of each 64); a batch holds gpb whole groups (gpb * lpg <= 2048 lanes).  Each block
+// publishes its partial sums write-through, waits for its stores, and bumps the batch
+// counter; the block whose add is the batch's last runs the batch's heads (2 lanes per
+// group) while the payload lines they re-read are still in that XCD's L2.
+template <int K, int M, int HDR, bool UNI>
+__global__ void __launch_bounds__(256) k_pack_one(WireArgs a, const uint8_t* __restrict__ payload,
+                                                  const int64_t* __restrict__ offsets,
+                                                  const int32_t* __restrict__ sizes,
+                                                  const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
+                                                  uint32_t* __restrict__ counters, uint32_t lpg, DivMagic rows_div,
+                                                  uint32_t gpb, uint64_t nbatch) {
+    __shared__ uint32_t s_last;
+    const uint32_t b = blockIdx.x;
+    const uint64_t beta = (uint64_t)(b >> 6) * 8 + (b & 7);
+    const uint32_t lib = ((b >> 3) & 7) * 256u + threadIdx.x;  // lane in batch
+    const uint32_t gib = UNI ? __builtin_amdgcn_readfirstlane((uint32_t)fast_div(lib >> 6, rows_div))
+                             : (uint32_t)fast_div(lib >> 4, rows_div);
+    const uint64_t g = beta * gpb + gib;
+    const bool live = beta < nbatch && gib < gpb && g < a.groups;
+    body_lane<K, M, HDR, true>(a, payload, offsets, sizes, tab, part, live ? g : 0, lib - gib * lpg, live, lpg);
+    if (beta >= nbatch) return;  // whole block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_last = __hip_atomic_fetch_add(counters + beta, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 7;
+    __syncthreads();
+    if (!s_last || threadIdx.x >= 64) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint64_t gend = min((uint64_t)gpb, a.groups - beta * gpb);
+    for (uint32_t h0 = 0; h0 < 2 * gend; h0 += 64) {
+        const uint32_t h = h0 + threadIdx.x;
+        head_lane<K, M, HDR, true>(a, payload, offsets, sizes, tab, part, a.seq, a.wire, a.wire_len,
+                                   beta * gpb + (h >> 1), (int)(h & 1), h < 2 * gend, lpg);
     }
 }
 
@@ -546,21 +648,41 @@ template <int K, int M, int HDR>
 hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s) {
     // lanes per group for t >= 2 cover the longest datagram the shard pitch allows
     const uint32_t tn = (uint32_t)((HDR + a.pitch + 15) / 16);
-    const uint32_t lpg = std::max(16u, (tn - 2 + 15) / 16 * 16);
-    const DivMagic rows_div = make_div_magic(lpg / 16);
+    uint32_t lpg = std::max(16u, (tn - 2 + 15) / 16 * 16);
+    const int uni_mode = tuning().wire_uni;
+    if (uni_mode == 2) lpg = (lpg + 63) / 64 * 64;
+    const bool uni = uni_mode != 0 && lpg % 64 == 0;
+    const DivMagic rows_div = make_div_magic(uni ? lpg / 64 : lpg / 16);
+    const uint32_t gpb = 2048 / lpg;
+    if (tuning().wire_fused == 2 && gpb >= 1) {
+        const uint64_t nbatch = (a.groups + gpb - 1) / gpb;
+        const uint32_t P = (uint32_t)(a.k + a.m + 1) / 2;
+        uint32_t* counters = part + a.groups * (lpg / 16) * P;
+        hipError_t e = hipMemsetAsync(counters, 0, nbatch * 4, s);
+        if (e != hipSuccess) return e;
+        const uint64_t blocks = (nbatch + 7) / 8 * 64;
+        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
+        if (uni)
+            hipLaunchKernelGGL((k_pack_one<K, M, HDR, true>), dim3((unsigned)blocks), dim3(256), 0, s, a, a.payload,
+                               a.offsets, a.sizes, tab, part, counters, lpg, rows_div, gpb, nbatch);
+        else
+            hipLaunchKernelGGL((k_pack_one<K, M, HDR, false>), dim3((unsigned)blocks), dim3(256), 0, s, a, a.payload,
+                               a.offsets, a.sizes, tab, part, counters, lpg, rows_div, gpb, nbatch);
+        return hipGetLastError();
+    }
     const uint64_t per = ((uint64_t)1 << 30) / lpg;  // groups per launch: lanes < 2^30
     for (uint64_t g0 = 0; g0 < a.groups; g0 += per) {
         const uint64_t gn = std::min(per, a.groups - g0);
         const uint32_t lanes = (uint32_t)(gn * lpg);
-        if (tuning().wire_wpe == 4)
-            hipLaunchKernelGGL((k_pack_body<K, M, HDR, 4>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
-                               a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
+        if (uni)
+            hipLaunchKernelGGL((k_pack_body<K, M, HDR, true>), dim3((lanes + 255) / 256), dim3(256), 0, s, a,
+                               a.payload, a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
         else
-            hipLaunchKernelGGL((k_pack_body<K, M, HDR, 1>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
-                               a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
+            hipLaunchKernelGGL((k_pack_body<K, M, HDR, false>), dim3((lanes + 255) / 256), dim3(256), 0, s, a,
+                               a.payload, a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
         const uint32_t hl = (uint32_t)(2 * gn);
         hipLaunchKernelGGL((k_pack_head<K, M, HDR>), dim3((hl + 255) / 256), dim3(256), 0, s, a, a.payload, a.offsets,
-                           a.sizes, tab, (const uint32_t*)part, g0, hl, lpg);
+                           a.sizes, tab, (const uint32_t*)part, a.seq, a.wire, a.wire_len, g0, hl, lpg);
     }
     return hipGetLastError();
 }

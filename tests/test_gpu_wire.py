@@ -24,10 +24,10 @@ def padded_payload(p):
     return dev(np.concatenate([p, np.zeros(16, np.uint8)]))  # 16 readable bytes past the end
 
 
-@pytest.fixture(params=[1, 0], ids=["fused", "staged"])
+@pytest.fixture(params=[1, 2, 0], ids=["fused2", "fused1", "staged"])
 def wire_fused(request):
-    """Both send paths: the one-kernel fused pack (templated (k, m)) and the staged
-    build -> encode -> emit pipeline every shape can take."""
+    """Every send path: fused body + head launches, the one-launch fused pack (templated
+    (k, m)), and the staged build -> encode -> emit pipeline every shape can take."""
     qa.tune("wire_fused", request.param)
     yield request.param
     qa.tune("wire_fused", 1)

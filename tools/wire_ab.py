@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of the fused datagram send's tuning knobs (qfec_tune) in one
+process, on the same buffers; every variant's wire output is checked identical.
+
+  python tools/wire_ab.py [--k 10 --n 13 --size 1024 --groups 100000 --rounds 10 --reps 10]
+"""
+import argparse
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import quicknet_amd as qa  # noqa: E402
+
+KNOBS = {"wire_fused": 1, "wire_uni": 1, "wire_store_nt": 3}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--n", type=int, default=13)
+    p.add_argument("--size", type=int, default=1024)
+    p.add_argument("--groups", type=int, default=100_000)
+    p.add_argument("--rounds", type=int, default=10)
+    p.add_argument("--reps", type=int, default=10)
+    p.add_argument("--variants", default="base;wire_store_nt=0;wire_store_nt=1;wire_store_nt=2;wire_uni=0;wire_fused=0")
+    a = p.parse_args()
+    k, n, G, S = a.k, a.n, a.groups, a.size
+    dev = torch.device("cuda:0")
+    code = qa.Code.vandermonde(k, n - k)
+    sizes = torch.full((G * k,), S, dtype=torch.int32, device=dev)
+    offs = torch.arange(G * k, dtype=torch.int64, device=dev) * S
+    payload = torch.empty(G * k * S + 16, dtype=torch.uint8, device=dev)
+    qa.synth_fill(payload, 77)
+    seq = torch.stack([torch.arange(G, dtype=torch.int32, device=dev) * n,
+                       torch.arange(G, dtype=torch.int32, device=dev) * k], 1).contiguous()
+    head = 4
+    pitch = (S + head + 15) // 16 * 16
+    wpitch = (pitch + 13 + 15) // 16 * 16
+    shards = torch.empty((G, n, pitch), dtype=torch.uint8, device=dev)
+    wire = torch.zeros((G, n, wpitch), dtype=torch.uint8, device=dev)
+    wlen = torch.empty((G, n), dtype=torch.int32, device=dev)
+
+    def pack():
+        qa.lib().qfec_pack_datagrams(code._h, payload.data_ptr(), offs.data_ptr(), sizes.data_ptr(), seq.data_ptr(), G, 1,
+                                     shards.data_ptr(), pitch, wire.data_ptr(), wpitch, wlen.data_ptr(), None)
+
+    def setup(spec):
+        for kk, v in KNOBS.items():
+            qa.tune(kk, v)
+        if spec != "base":
+            for kv in spec.split(","):
+                kk, v = kv.split("=")
+                qa.tune(kk, int(v))
+
+    variants = a.variants.split(";")
+    setup("base")
+    pack()
+    torch.cuda.synchronize()
+    ref = wire.clone()
+    ref_len = wlen.clone()
+    times = {v: [] for v in variants}
+    s = torch.cuda.current_stream()
+    for _ in range(a.rounds):
+        for v in variants:
+            setup(v)
+            pack()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(a.reps):
+                pack()
+            e1.record(s)
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / a.reps)
+            L = ref_len.max().item()
+            assert torch.equal(wlen, ref_len), v
+            assert torch.equal(wire[..., :L], ref[..., :L]) or v.startswith("wire_fused=0"), v
+    setup("base")
+    nbytes = G * k * S + int(ref_len.sum().item())
+    print(f"pack RS({k},{n}) payload {S} B, G={G}: {a.rounds} rounds x {a.reps}")
+    for v in variants:
+        t = times[v]
+        med = statistics.median(t)
+        print(f"  {v:36s} median {med*1e3:8.1f} us  min {min(t)*1e3:8.1f} us -> {nbytes/(med*1e-3)/1e9:7.1f} GB/s min-traffic")
+
+
+if __name__ == "__main__":
+    main()
