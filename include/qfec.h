@@ -115,6 +115,26 @@ int qfec_unpack_datagrams(qfec_code *code, const unsigned char *d_wire, long lon
                           unsigned char *d_shards, long long shard_pitch, unsigned char *d_marks,
                           int *d_rx_size, int *d_status, int *d_psize, void *stream);
 
+/* ---- ProtocolUdp framing of datagram batches ----
+ * The byte stage below FEC.  Row r of d_out = Session::PacketOutput + ProtocolUdp::SendPacket
+ * (network/SessionDesc.cpp:69-77, network/ProtocolBasic.cpp:111-150) applied to d_in row r:
+ *   [mask][c][(cmd & 0x1f) | 0xA0][protocol]([conv u32 LE][hid u32 LE])[d_in[r][0, len)]
+ * with bytes 1.. XORed by mask ^ gmask ^ 0x5a, mask = d_mask[r] (the session's _mask++),
+ * c = CheckSum(bytes 2..) & 0xff, CheckSum(x) = ~(fold16(byte sum)) (ProtocolBasic.cpp:56-87).
+ * The 8-byte Session prefix is present iff d_conv_hid ([rows][2] conv, hid) is non-NULL.
+ * d_out_len[r] = framed length, or -1 when it does not fit out_pitch.
+ * qfec_unframe_udp reverses it (ProtocolUdp::RecvPacket, ProtocolBasic.cpp:152-210):
+ * d_status[r] = 0 ok, 1 short, 2 bad checksum, 3 bad cmd, 4 too long; d_out row = the data,
+ * d_out_len = len - 4 (- 8 with session = 1); d_info [rows][4] = xor mask, c, cmd & 0x1f,
+ * protocol (nullable); d_conv_hid receives the Session prefix when session = 1 (nullable).
+ * Pitches multiples of 16, rows 16-B aligned. */
+int qfec_frame_udp(const unsigned char *d_in, long long in_pitch, const int *d_len, long long rows,
+                   const unsigned char *d_mask, const unsigned int *d_conv_hid, int gmask, int cmd, int protocol,
+                   unsigned char *d_out, long long out_pitch, int *d_out_len, void *stream);
+int qfec_unframe_udp(const unsigned char *d_in, long long in_pitch, const int *d_len, long long rows, int gmask,
+                     int session, unsigned char *d_out, long long out_pitch, int *d_out_len, int *d_status,
+                     unsigned char *d_info, unsigned int *d_conv_hid, void *stream);
+
 /* Fill nbytes of device memory with the synthetic stream of quicknet_amd/synth.py. */
 int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long seed, void *stream);
 
@@ -123,9 +143,9 @@ int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long s
 int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long long groups, int k, int m,
                       int block_size, long long pitch, void *stream);
 
-/* Experiment knobs for interleaved A/B timing (tools/ab.py): "encode_impl" 0|1,
- * "recon_impl" -1 (auto) | 0 | 1, "wire_fused" 1 (one-kernel datagram send where a (k, m)
- * instance exists) | 0 (staged build -> encode -> emit).  Defaults are the measured best; results are identical. */
+/* Experiment knobs for interleaved A/B timing (tools/ab.py, tools/wire_ab.py): "encode_impl"
+ * 0|1, "recon_impl" -1 (auto) | 0 | 1, "wire_fused" 1 (fused datagram send where a (k, m)
+ * instance exists) | 0 (staged build -> encode -> emit), "wire_store_nt" 0-3.  Defaults are the measured best; results are identical. */
 int qfec_tune(const char *key, int value);
 
 int qfec_set_kernel_variant(int variant);

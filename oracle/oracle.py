@@ -47,6 +47,8 @@ class Oracle:
         L.orc_pack_group.argtypes = [i, i, vp, vp, vp, vp, C.c_uint32, C.c_uint32, i, i, vp, ll, vp]
         L.orc_unpack_head.argtypes = [vp, i] + [C.POINTER(C.c_uint32)] * 2 + [C.POINTER(i)] * 4 + [vp, C.POINTER(i)]
         L.orc_dec_src.argtypes = [vp, i, i, C.POINTER(i)]
+        L.orc_frame_udp.argtypes = [vp, i, i, i, i, i, i, C.c_uint32, C.c_uint32, vp]
+        L.orc_unframe_udp.argtypes = [vp, i, i, i, vp, vp]
         self.L = L
 
     # -- matrices
@@ -117,6 +119,24 @@ class Oracle:
         gmax = self.L.orc_pack_group(k, n, _p(np.ascontiguousarray(rows_full)), _p(pl), _p(offs), _p(sizes),
                                      sent0, src0, checksum, shard_cap, _p(out), pitch, _p(ln))
         return out, ln, gmax
+
+    def frame_udp(self, data, mask, gmask=0, cmd=0x11, protocol=0xFF, conv_hid=None):
+        """ProtocolUdp framing of one datagram (parity unpinned: ProtocolBasic.cpp does not build)."""
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        out = np.zeros(len(d) + 12, np.uint8)
+        sess = conv_hid is not None
+        conv, hid = (int(conv_hid[0]) & 0xFFFFFFFF, int(conv_hid[1]) & 0xFFFFFFFF) if sess else (0, 0)
+        n = self.L.orc_frame_udp(_p(d), len(d), int(mask), int(gmask), int(cmd), int(protocol), int(sess), conv, hid,
+                                 _p(out))
+        return out[:n]
+
+    def unframe_udp(self, frame, gmask=0, session=False):
+        """-> (status, un-XORed frame bytes, info[4])."""
+        f = np.ascontiguousarray(frame, dtype=np.uint8)
+        work = np.zeros(max(len(f), 1), np.uint8)
+        info = np.zeros(4, np.uint8)
+        st = self.L.orc_unframe_udp(_p(f), len(f), int(gmask), int(bool(session)), _p(work), _p(info))
+        return st, work[:len(f)], info
 
     def unpack_head(self, dgram):
         """unpack_fec_head: (rc, sent, src, n, k, ik, is_checksum, shard bytes)."""

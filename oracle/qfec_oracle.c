@@ -659,3 +659,62 @@ int orc_pack_group(int k, int n, const u8 *rows_full, const u8 *payload, const l
     free(shards); free(src); free(par);
     return gmax;
 }
+
+/* ---------------------------------------------------------------- ProtocolUdp framing
+ * Restated from network/ProtocolBasic.cpp (which does not build here: ../system/option.h is
+ * absent from the reference tree), so this part of the oracle is PARITY UNPINNED: no
+ * reference output exists to check it against.
+ *   CheckSum2 / CheckSum (ProtocolBasic.cpp:65-87): s = byte sum; ~((s >> 16) + (s & 0xffff))
+ *   SendPacket (:111-150): push protocol, push (cmd & 0x1f) | 0xA0, push CheckSum & 0xff,
+ *                           XOR everything with mask ^ gmask ^ 0x5a, push mask
+ *   Session::PacketOutput (SessionDesc.cpp:69-77): push hid, push conv (u32 LE) first. */
+static uint32_t udp_checksum(const u8 *p, int n)
+{
+    uint32_t s = 0;
+    int i;
+    for (i = 0; i < n; ++i) s += p[i];
+    s = (s >> 16) + (s & 0xffffu);
+    return ~s;
+}
+
+/* returns the framed length; out holds at least len + 12 bytes */
+int orc_frame_udp(const u8 *data, int len, int mask, int gmask, int cmd, int protocol, int session, uint32_t conv,
+                  uint32_t hid, u8 *out)
+{
+    int P = session ? 12 : 4, i;
+    u8 x = (u8)((mask ^ gmask ^ 0x5a) & 0xff);
+    out[2] = (u8)((cmd & 0x1f) | 0xa0);
+    out[3] = (u8)protocol;
+    if (session) {
+        for (i = 0; i < 4; ++i) {
+            out[4 + i] = (u8)(conv >> (8 * i));
+            out[8 + i] = (u8)(hid >> (8 * i));
+        }
+    }
+    memcpy(out + P, data, (size_t)len);
+    out[1] = (u8)(udp_checksum(out + 2, P - 2 + len) & 0xff);
+    for (i = 1; i < P + len; ++i) out[i] ^= x;
+    out[0] = (u8)mask;
+    return P + len;
+}
+
+/* RecvPacket (:152-210).  Returns 0 ok, 1 short, 2 checksum, 3 cmd; the un-XORed frame goes
+ * to work (len bytes); info = xor mask, check, cmd & 0x1f, protocol */
+int orc_unframe_udp(const u8 *frame, int len, int gmask, int session, u8 *work, u8 *info)
+{
+    int P = session ? 12 : 4, i;
+    u8 x;
+    uint32_t c;
+    if (len < P) return 1;
+    x = (u8)((frame[0] ^ gmask ^ 0x5a) & 0xff);
+    work[0] = frame[0];
+    for (i = 1; i < len; ++i) work[i] = frame[i] ^ x;
+    c = udp_checksum(work + 2, len - 2) & 0xff;
+    info[0] = x;
+    info[1] = work[1];
+    info[2] = (u8)(work[2] & 0x1f);
+    info[3] = work[3];
+    if (c != work[1]) return 2;
+    if ((work[2] & 0xe0) != 0xa0) return 3;
+    return 0;
+}

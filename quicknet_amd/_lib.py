@@ -17,7 +17,7 @@ EXPORTS = {
     "qfec.h": ["qfec_code_new", "qfec_code_from_rows", "qfec_code_free", "qfec_code_rows", "qfec_code_shape",
                "qfec_encode", "qfec_reconstruct", "qfec_prepare_reconstruct", "qfec_decode_rows",
                "qfec_fec_code", "qfec_rs_code", "qfec_fec_matrix", "qfec_pack_datagrams", "qfec_unpack_datagrams",
-               "qfec_synth_fill", "qfec_probe_stream",
+               "qfec_frame_udp", "qfec_unframe_udp", "qfec_synth_fill", "qfec_probe_stream",
                "qfec_tune", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
                "qfec_last_error", "qfec_version"],
 }
@@ -60,6 +60,8 @@ def lib():
         "qfec_fec_matrix": (i, [vp, vp]),
         "qfec_pack_datagrams": (i, [vp, vp, vp, vp, vp, ll, i, vp, ll, vp, ll, vp, vp]),
         "qfec_unpack_datagrams": (i, [vp, vp, ll, vp, ll, i, i, vp, ll, vp, vp, vp, vp, vp]),
+        "qfec_frame_udp": (i, [vp, ll, vp, ll, vp, vp, i, i, i, vp, ll, vp, vp]),
+        "qfec_unframe_udp": (i, [vp, ll, vp, ll, i, i, vp, ll, vp, vp, vp, vp, vp]),
         "qfec_synth_fill": (i, [vp, ll, u64, vp]),
         "qfec_probe_stream": (i, [vp, vp, ll, i, i, i, ll, vp]),
         "qfec_tune": (i, [C.c_char_p, i]),

@@ -17,7 +17,7 @@ import numpy as np
 from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
 
 __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
-           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count"]
+           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count", "frame_udp", "unframe_udp"]
 
 
 def _stream_handle(stream):
@@ -64,6 +64,44 @@ def probe_stream(data, parity, block_size, stream=None):
     m = parity.shape[1]
     check(lib().qfec_probe_stream(_dev_ptr(data), _dev_ptr(parity), G, k, m, block_size, pitch,
                                   _stream_handle(stream)), "qfec_probe_stream")
+
+
+def frame_udp(rows, lengths, masks, gmask=0, cmd=0x11, protocol=0xFF, conv_hid=None, out_pitch=None, stream=None):
+    """ProtocolUdp framing of a datagram batch (include/qfec.h qfec_frame_udp): rows uint8
+    [R, pitch] device tensor, lengths int32 [R], masks uint8 [R] (per-packet Session _mask),
+    conv_hid uint32/int32 [R, 2] or None.  Defaults: QUICKNET_CMD_DATA, QUICKNET_PROTOCOL_FEC
+    (network/ProtocolBasic.h:82,95), as Session::TransmissionOutput sets them for FEC datagrams
+    (network/SessionDesc.cpp:513-519).  Returns (framed [R, out_pitch], framed_len [R])."""
+    import torch
+    R, pitch = rows.shape
+    P = 12 if conv_hid is not None else 4
+    if out_pitch is None:
+        out_pitch = (pitch + P + 15) // 16 * 16
+    out = torch.empty((R, out_pitch), dtype=torch.uint8, device=rows.device)
+    out_len = torch.empty(R, dtype=torch.int32, device=rows.device)
+    check(lib().qfec_frame_udp(_dev_ptr(rows), pitch, _dev_ptr(lengths), R, _dev_ptr(masks),
+                               _dev_ptr(conv_hid) if conv_hid is not None else None, int(gmask), int(cmd), int(protocol),
+                               _dev_ptr(out), out_pitch, _dev_ptr(out_len), _stream_handle(stream)), "qfec_frame_udp")
+    return out, out_len
+
+
+def unframe_udp(frames, lengths, gmask=0, session=False, out_pitch=None, stream=None):
+    """Reverse of frame_udp (qfec_unframe_udp).  Returns (data [R, out_pitch], data_len [R],
+    status [R], info uint8 [R, 4], conv_hid int32 [R, 2] or None)."""
+    import torch
+    R, pitch = frames.shape
+    if out_pitch is None:
+        out_pitch = pitch
+    dev = frames.device
+    out = torch.empty((R, out_pitch), dtype=torch.uint8, device=dev)
+    out_len = torch.empty(R, dtype=torch.int32, device=dev)
+    status = torch.empty(R, dtype=torch.int32, device=dev)
+    info = torch.empty((R, 4), dtype=torch.uint8, device=dev)
+    ch = torch.zeros((R, 2), dtype=torch.int32, device=dev) if session else None
+    check(lib().qfec_unframe_udp(_dev_ptr(frames), pitch, _dev_ptr(lengths), R, int(gmask), int(bool(session)),
+                                 _dev_ptr(out), out_pitch, _dev_ptr(out_len), _dev_ptr(status), _dev_ptr(info),
+                                 _dev_ptr(ch) if ch is not None else None, _stream_handle(stream)), "qfec_unframe_udp")
+    return out, out_len, status, info, ch
 
 
 class Code:

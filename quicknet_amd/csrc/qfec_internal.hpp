@@ -93,6 +93,21 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s);
 // fused send path for templated (k, m); *launched = false when the shape has no instance
 // `part` = scratch of (lpg / 16) * ((n + 1) / 2) u32 per group, lpg ~ (pitch + 13) / 16
 hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s, bool* launched);
+struct FrameArgs {
+    const uint8_t* in;        // [rows][in_pitch]
+    const int32_t* in_len;    // [rows]
+    uint8_t* out;             // [rows][out_pitch]
+    int32_t* out_len;         // [rows] (frame: framed length, -1 if it does not fit)
+    const uint8_t* mask;      // frame: [rows] raw mask byte (Session::PacketOutput's _mask++)
+    uint32_t* conv_hid;       // [rows][2] Session prefix (frame: in, unframe: out); may be NULL
+    int32_t* status;          // unframe: [rows]
+    uint8_t* info;            // unframe: [rows][4] mask, check, cmd & 0x1f, protocol; may be NULL
+    uint64_t rows, in_pitch, out_pitch;
+    uint32_t gmask, cmd, protocol;
+    int session;              // 1: the 8-byte conv/hid prefix is part of the frame
+};
+hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s);
+hipError_t launch_unframe_udp(const FrameArgs& a, hipStream_t s);
 hipError_t launch_emit_wire(const WireArgs& a, hipStream_t s);
 hipError_t launch_parse_wire(const WireArgs& a, hipStream_t s);
 hipError_t launch_check_payloads(const WireArgs& a, hipStream_t s);
@@ -101,10 +116,8 @@ hipError_t launch_check_payloads(const WireArgs& a, hipStream_t s);
 struct Tuning {
     int recon_impl = -1;  // -1 auto (per shape), 0 row loop, 1 all rows
     int encode_impl = 0;
-    int wire_fused = 1;
-    int wire_store_nt = 3; // fused send datagram stores: bit 0 body, bit 1 head non-temporal
-    int wire_uni = 1;     // fused send body: 0 per-lane groups, 1 wave-uniform when lpg % 64 == 0,
-                          // 2 wave-uniform always (lpg rounded up to 64)   // fused one-kernel datagram paths where a (k, m) instance exists
+    int wire_fused = 1;     // fused datagram send where a (k, m) instance exists (0: staged)
+    int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
 };
 Tuning& tuning();
 

@@ -494,8 +494,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "recon_impl") && value >= -1 && value <= 1) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_uni") && value >= 0 && value <= 2) { tuning().wire_uni = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_fused") && value >= 0 && value <= 2) { tuning().wire_fused = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
 }
@@ -758,6 +757,66 @@ int qfec_unpack_datagrams(qfec_code* code, const unsigned char* d_wire, long lon
         return rc;
     e = launch_check_payloads(a, s);
     return e == hipSuccess ? QFEC_OK : hip_fail(e, "check_payloads launch");
+}
+
+
+int qfec_frame_udp(const unsigned char* d_in, long long in_pitch, const int* d_len, long long rows,
+                   const unsigned char* d_mask, const unsigned int* d_conv_hid, int gmask, int cmd, int protocol,
+                   unsigned char* d_out, long long out_pitch, int* d_out_len, void* stream) {
+    if (rows < 0 || !d_len || !d_mask || !d_out_len || in_pitch < 16 || out_pitch < 16 || in_pitch % 16 ||
+        out_pitch % 16 || ((uintptr_t)d_in | (uintptr_t)d_out) % 16) {
+        set_error("frame_udp: pitches must be multiples of 16 and rows 16-B aligned");
+        return QFEC_EINVAL;
+    }
+    if (rows == 0) return QFEC_OK;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    FrameArgs a{};
+    a.in = d_in;
+    a.in_len = d_len;
+    a.out = d_out;
+    a.out_len = d_out_len;
+    a.mask = d_mask;
+    a.conv_hid = const_cast<uint32_t*>(d_conv_hid);
+    a.rows = (uint64_t)rows;
+    a.in_pitch = (uint64_t)in_pitch;
+    a.out_pitch = (uint64_t)out_pitch;
+    a.gmask = (uint32_t)gmask & 0xFFu;
+    a.cmd = (uint32_t)cmd;
+    a.protocol = (uint32_t)protocol;
+    a.session = d_conv_hid != nullptr;
+    const hipError_t e = launch_frame_udp(a, (hipStream_t)stream);
+    return e == hipSuccess ? QFEC_OK : hip_fail(e, "frame_udp launch");
+}
+
+int qfec_unframe_udp(const unsigned char* d_in, long long in_pitch, const int* d_len, long long rows, int gmask,
+                     int session, unsigned char* d_out, long long out_pitch, int* d_out_len, int* d_status,
+                     unsigned char* d_info, unsigned int* d_conv_hid, void* stream) {
+    if (rows < 0 || !d_len || !d_out_len || !d_status || (session != 0 && session != 1) || in_pitch < 16 ||
+        out_pitch < 16 || in_pitch % 16 || out_pitch % 16 || ((uintptr_t)d_in | (uintptr_t)d_out) % 16) {
+        set_error("unframe_udp: pitches must be multiples of 16 and rows 16-B aligned");
+        return QFEC_EINVAL;
+    }
+    if (rows == 0) return QFEC_OK;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    FrameArgs a{};
+    a.in = d_in;
+    a.in_len = d_len;
+    a.out = d_out;
+    a.out_len = d_out_len;
+    a.conv_hid = d_conv_hid;
+    a.status = d_status;
+    a.info = d_info;
+    a.rows = (uint64_t)rows;
+    a.in_pitch = (uint64_t)in_pitch;
+    a.out_pitch = (uint64_t)out_pitch;
+    a.gmask = (uint32_t)gmask & 0xFFu;
+    a.session = session;
+    const hipError_t e = launch_unframe_udp(a, (hipStream_t)stream);
+    return e == hipSuccess ? QFEC_OK : hip_fail(e, "unframe_udp launch");
 }
 
 }  // extern "C"

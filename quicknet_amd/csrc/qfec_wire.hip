@@ -319,20 +319,23 @@ __global__ void __launch_bounds__(256) k_check_payloads(WireArgs a) {
 }
 
 // ------------------------------------------------------------------ send: fused
-// Two launches for compile-time (K, M) replace build -> encode -> emit, so the
-// [G][n][pitch] shard matrix never exists: HBM traffic is the payload in and the
-// datagrams out.  GF arithmetic is bytewise, so check-shard bytes at any shard offset
-// come from the data-shard bytes at the same offset; each lane therefore works on one
-// 16-B DATAGRAM chunk t = shard bytes [16t - HDR, 16t + 16 - HDR) of all n rows at once,
-// with no neighbour exchange.
-//  k_pack_body   lanes for t >= 2, flat over (group, t), lpg lanes per group (a multiple
-//                of 16): data chunks are straight payload loads; it stores all n datagram
-//                chunks and 16-lane partial byte sums (two rows per u32) into `part`.
-//  k_pack_head   two lanes per group for t = 0, 1: the only chunks that hold shard bytes
-//                0-3 (size, payload checksum) and the datagram header with its checksum,
-//                both of which need the whole group's sums.
+// For compile-time (K, M), build -> encode -> emit collapse into one body launch (plus a
+// tiny head launch with checksums), so the [G][n][pitch] shard matrix never exists: HBM
+// traffic is the payload in and the datagrams out.  GF arithmetic is bytewise, so check-shard
+// bytes at any shard offset come from the data-shard bytes at the same offset; each lane
+// works on one 16-B DATAGRAM chunk t = shard bytes [16t - HDR, 16t + 16 - HDR) of all n
+// rows at once, with no neighbour exchange.
+//
+//  k_pack_body  flat over (group, t), lpg lanes per group (a multiple of 16).  HDR 11 (no
+//               checksums): every chunk, header included.  HDR 13: every chunk but 0, with
+//               shard byte 3 (the high checksum byte, datagram byte 16) left zero; 16-lane
+//               partial byte sums (two rows per u32) go to `part`.
+//  k_pack_head  HDR 13 only, one lane per group: shard bytes 0-3 are the sizes and payload
+//               checksums, so check-shard bytes 0-3 are a K-term GF dot product of those
+//               dwords -- no payload is read.  Writes chunk 0 (header, datagram checksum,
+//               shard bytes 0-2) and byte 16 of every datagram.
 template <int K, int M>
-__device__ __forceinline__ void encode_col(const uint4 (&x)[K], uint4 (&acc)[M], const uint32_t* __restrict__ tab) {
+__device__ __forceinline__ void encode_cols(const uint4 (&x)[K], uint4 (&acc)[M], const uint32_t* __restrict__ tab) {
 #pragma unroll
     for (int r = 0; r < M; ++r) acc[r] = make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -360,10 +363,6 @@ __device__ __forceinline__ uint32_t row16_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
     return v;
 }
-// v + the value of lane ^ 1
-__device__ __forceinline__ uint32_t pair_sum(uint32_t v) {
-    return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
-}
 
 // A group is packed only if every size is in [0, shard_pitch - head]; otherwise its n
 // wire_len entries are -1 and none of its datagram bytes are written.
@@ -381,256 +380,325 @@ __device__ __forceinline__ bool group_sizes(const int32_t* __restrict__ sizes, u
     return ok;
 }
 
-// UNI: lpg is a multiple of 64, so a wave never straddles groups and the group's sizes,
-// offsets and row addresses are wave-uniform (SGPRs); otherwise per lane.
-// One lane of the body: datagram chunk t = 2 + rem of group g (live: g exists).  PART_SC1:
-// write the partial sums write-through (agent scope), for a same-launch reader.
-template <int K, int M, int HDR, bool PART_SC1>
-__device__ __forceinline__ void body_lane(const WireArgs& a, const uint8_t* __restrict__ payload,
-                                          const int64_t* __restrict__ offsets, const int32_t* __restrict__ sizes,
-                                          const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
-                                          uint64_t g, uint32_t rem, bool live, uint32_t lpg) {
+// datagram header bytes 0-10 (+ 11-12 with HDR 13) into chunk 0 of row r
+template <int HDR>
+__device__ __forceinline__ void put_header(uint4& v, uint32_t sent, uint32_t srcno, uint32_t ikn, uint32_t dsum) {
+    put_byte(v, 0, HDR == 13 ? 0xED : 0xEC);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        put_byte(v, 1 + b, sent >> (8 * b));
+        put_byte(v, 5 + b, srcno >> (8 * b));
+    }
+    put_byte(v, 9, ikn);
+    put_byte(v, 10, ikn >> 8);
+    if (HDR == 13) {
+        put_byte(v, 11, dsum);
+        put_byte(v, 12, dsum >> 8);
+    }
+}
+
+template <int K, int M, int HDR>
+__global__ void __launch_bounds__(256) k_pack_body(WireArgs a, const uint8_t* __restrict__ payload,
+                                                   const int64_t* __restrict__ offsets,
+                                                   const int32_t* __restrict__ sizes,
+                                                   const uint32_t* __restrict__ seq,
+                                                   const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
+                                                   uint64_t g0, uint32_t lanes, uint32_t lpg, DivMagic lpg_div,
+                                                   uint64_t row0) {
     constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
-    const int t = 2 + (int)rem;
-    const int p = 16 * t - HDR - HEAD;  // payload offset of this chunk's first byte (>= 32 - 17)
+    constexpr int TS = HDR == 13 ? 1 : 0;            // first chunk of the body
+    constexpr int PS = 16 * TS - HDR - HEAD;          // its payload offset (< 0)
+    const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
+    const bool live = flat < lanes;  // dead lanes still join the row sums (with zeros)
+    const uint32_t gl = (uint32_t)fast_div(flat, lpg_div);
+    const uint32_t rem = flat - gl * lpg;
+    const uint64_t g = g0 + gl;
+    const int t = TS + (int)rem;
+    const bool first = t == TS;          // holds shard byte 0 (HDR 11) / byte 3 (HDR 13)
+    const int p = 16 * t - HDR - HEAD;   // payload offset of this chunk's first byte
     int size[K], gmax = 0;
     bool ok = false;
     if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
     const bool act = ok && 16 * t < HDR + gmax;
     uint8_t* out = a.wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
-    // all K loads back to back (no per-row branch in between): the address is clamped to
-    // the packet's end, whose 16 following bytes are readable by contract, and masked after
+    // all K loads back to back, addresses clamped into the packet (+16 readable bytes)
     uint4 x[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
     if (ok) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + offsets[g * K + i] + min(p, size[i]));
+        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + offsets[g * K + i] + min(max(p, 0), size[i]));
 #pragma unroll
-        for (int i = 0; i < K; ++i) x[i] = mask16(x[i], 0, size[i] - p);
+        for (int i = 0; i < K; ++i) {
+            // the first chunk's payload starts -PS bytes in: shift it up
+            const uint4 sh = window(make_uint4(0, 0, 0, 0), x[i], 16 + PS);
+            x[i] = mask16(pick16(first, sh, x[i]), first ? -PS : 0, size[i] - p);
+            if (HDR == 11) {  // shard bytes 0-1 (size) at chunk bytes 11-12 of the first chunk
+                uint4 y = x[i];
+                put_byte(y, 11, (uint32_t)size[i]);
+                put_byte(y, 12, (uint32_t)size[i] >> 8);
+                x[i] = pick16(first, y, x[i]);
+            }
+        }
     }
     uint32_t ps[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) ps[q] = 0;
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        if (act && p < size[i]) stw(out + (uint64_t)i * a.wire_pitch, x[i], a.store_nt & 1);
-        const uint32_t s = sum16(x[i], 0);
-        ps[i >> 1] += (i & 1) ? s << 16 : s;
-    }
-    uint4 acc[M];
-#pragma unroll
-    for (int r = 0; r < M; ++r) acc[r] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int c = 0; c + 1 < K; c += 2) {
-        Sel sa[4], sb[4];
-        sel16(sa, x[c]);
-        sel16(sb, x[c + 1]);
-#pragma unroll
-        for (int r = 0; r < M; ++r)
-            gf_mac16x2(acc[r], sa, sb, tab + (r * K + c) * QFEC_TAB_STRIDE, tab + (r * K + c + 1) * QFEC_TAB_STRIDE);
-    }
-    if (K & 1) {
-        Sel sl[4];
-        sel16(sl, x[K - 1]);
-#pragma unroll
-        for (int r = 0; r < M; ++r) gf_mac16(acc[r], sl, tab + (r * K + K - 1) * QFEC_TAB_STRIDE);
-    }
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        // check-shard bytes past groupMax are zero: every data chunk is zero there
-        if (act) stw(out + (uint64_t)(K + j) * a.wire_pitch, acc[j], a.store_nt & 1);
-        const uint32_t s = sum16(acc[j], 0);
-        ps[(K + j) >> 1] += ((K + j) & 1) ? s << 16 : s;
-    }
-    // per-lane sums are <= 16 * 255, a 16-lane row's <= 65280: two rows share a u32 exactly
-    const uint32_t R = lpg >> 4;
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-        const uint32_t v = row16_sum(ps[q]);
-        if (live && (rem & 15) == 0) {
-            uint32_t* dst = part + (g * R + (rem >> 4)) * P + q;
-            if (PART_SC1) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else *dst = v;
-        }
-    }
-}
-
-template <int K, int M, int HDR, bool UNI>
-__global__ void __launch_bounds__(256) k_pack_body(WireArgs a, const uint8_t* __restrict__ payload,
-                                                   const int64_t* __restrict__ offsets,
-                                                   const int32_t* __restrict__ sizes,
-                                                   const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
-                                                   uint64_t g0, uint32_t lanes, uint32_t lpg, DivMagic rows_div) {
-    const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
-    const bool live = flat < lanes;  // whole 16-lane rows (UNI: waves) are live or not
-    uint32_t gl;
-    if (UNI) {
-        if (!live) return;
-        gl = __builtin_amdgcn_readfirstlane((uint32_t)fast_div(flat >> 6, rows_div));
-    } else {
-        gl = live ? (uint32_t)fast_div(flat >> 4, rows_div) : 0;
-    }
-    body_lane<K, M, HDR, false>(a, payload, offsets, sizes, tab, part, g0 + gl, flat - gl * lpg, live, lpg);
-}
-
-// One lane of the head: datagram chunk t (0 or 1) of group g; lanes 2j, 2j + 1 are a pair
-// (same g, same `live`).  PART_SC1: read the partial sums write-through (agent scope).
-template <int K, int M, int HDR, bool PART_SC1>
-__device__ __forceinline__ void head_lane(const WireArgs& a, const uint8_t* __restrict__ payload,
-                                          const int64_t* __restrict__ offsets, const int32_t* __restrict__ sizes,
-                                          const uint32_t* __restrict__ tab, const uint32_t* __restrict__ part,
-                                          const uint32_t* __restrict__ seq, uint8_t* __restrict__ wire,
-                                          int32_t* __restrict__ wire_len, uint64_t g, int t, bool live, uint32_t lpg) {
-    constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
-    int size[K], gmax = 0;
-    bool ok = false;
-    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
-    // every global load up front, addresses clamped to the packet (+16 readable bytes)
-    uint4 raw0[K], raw1[K];
-    uint32_t tot[N], sent0 = 0, src0 = 0;
-#pragma unroll
-    for (int r = 0; r < N; ++r) tot[r] = 0;
-#pragma unroll
-    for (int i = 0; i < K; ++i) raw0[i] = raw1[i] = make_uint4(0, 0, 0, 0);
-    if (ok) {
-        sent0 = seq[2 * g];
-        src0 = seq[2 * g + 1];
+    if (HDR == 13) {
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            const uint8_t* src = payload + offsets[g * K + i];
-            raw0[i] = ldu16(src);
-            raw1[i] = ldu16(src + min(16 - HEAD, size[i]));
-        }
-        // the body's 16-lane partial sums: R = lpg / 16 rows of P words
-        const uint32_t R = lpg >> 4;
-        const uint32_t* pg = part + g * R * P;
-        for (uint32_t r0 = 0; r0 < R; r0 += 4) {
-#pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
-                const uint32_t rr = min(r0 + u, R - 1), use = r0 + u < R;
-#pragma unroll
-                for (int q = 0; q < P; ++q) {
-                    uint32_t v = 0;
-                    if (use)
-                        v = PART_SC1 ? __hip_atomic_load(pg + rr * P + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : pg[rr * P + q];
-                    tot[2 * q] += v & 0xFFFF;
-                    if (2 * q + 1 < N) tot[2 * q + 1] += v >> 16;
-                }
-            }
+            const uint32_t s = sum16(x[i], 0);  // payload bytes only
+            ps[i >> 1] += (i & 1) ? s << 16 : s;
         }
     }
-    // this lane's datagram chunk of every data row (t = 0: shard bytes [0, 16 - HDR) after
-    // the header; t = 1: shard bytes [16 - HDR, 32 - HDR)), checksum bytes still zero
-    uint4 dw[K];
-    uint32_t psum[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        uint4 c0 = mask16(window(make_uint4(0, 0, 0, 0), raw0[i], 16 - HEAD), HEAD, HEAD + size[i]);
-        put_byte(c0, 0, (uint32_t)size[i]);
-        put_byte(c0, 1, (uint32_t)size[i] >> 8);
-        const uint4 c1 = mask16(raw1[i], 0, size[i] - (16 - HEAD));
-        const int len = size[i] + HEAD;
-        const uint4 d0 = mask16(window(make_uint4(0, 0, 0, 0), c0, 16 - HDR), HDR, HDR + len);
-        const uint4 d1 = mask16(window(c0, c1, 16 - HDR), 0, HDR + len - 16);
-        dw[i] = pick16(t == 0, d0, d1);
-        psum[i] = sum16(dw[i], 0) - (t == 0 ? ((uint32_t)size[i] & 0xFF) + (((uint32_t)size[i] >> 8) & 0xFF) : 0u);
+    uint4 acc[M];
+    encode_cols<K, M>(x, acc, tab);
+    uint32_t sent0 = 0, src0 = 0;
+    if (HDR == 11 && act && first) {
+        sent0 = seq[2 * g];
+        src0 = seq[2 * g + 1];
     }
-#pragma unroll
-    for (int i = 0; i < K; ++i) {
-        psum[i] = (pair_sum(psum[i]) + tot[i]) & 0xFFFF;
-        if (HEAD == 4) {  // shard bytes 2, 3: datagram chunk 0 byte 15, chunk 1 byte 0
-            uint4 p0 = dw[i], p1 = dw[i];
-            put_byte(p0, 15, psum[i]);
-            put_byte(p1, 0, psum[i] >> 8);
-            dw[i] = pick16(t == 0, p0, p1);
-        }
-    }
-    uint4 pw[M];
-    encode_col<K, M>(dw, pw, tab);
-    uint32_t qsum[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) qsum[j] = (pair_sum(sum16(pw[j], 0)) + tot[K + j]) & 0xFFFF;
-    if (!live) return;
-    uint8_t* out = wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
 #pragma unroll
     for (int r = 0; r < N; ++r) {
+        uint4 v = r < K ? x[r] : acc[r - K];
         const int len = r < K ? size[r] + HEAD : gmax;
-        const uint4 v = r < K ? dw[r] : pw[r - K];
-        uint4 h = v;
-        const uint32_t sent = sent0 + (uint32_t)r;
-        const uint32_t srcno = src0 + (uint32_t)(r < K ? r : K - 1);
-        const uint32_t ikn = ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu;
-        put_byte(h, 0, HDR == 13 ? 0xED : 0xEC);
+        if (HDR == 11 && first) {
+            uint4 h = v;
+            put_header<11>(h, sent0 + (uint32_t)r, src0 + (uint32_t)(r < K ? r : K - 1),
+                           ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu, 0);
+            v = pick16(true, h, v);
+        }
+        if (act && 16 * t < HDR + len) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
+        if (HDR == 11 && act && first) a.wire_len[g * N + r] = HDR + len;
+        if (HDR == 13 && r >= K) {
+            const uint32_t s = sum16(v, 0);  // check-shard bytes 0-3 are the head's: zero here
+            ps[r >> 1] += (r & 1) ? s << 16 : s;
+        }
+    }
+    if (HDR == 11) {
+        if (live && !ok && first)
+            for (int r = 0; r < N; ++r) a.wire_len[g * N + r] = -1;
+        return;
+    }
+    // Per-lane sums are <= 16 * 255, a 16-lane row's <= 65280: two rows share a u32 exactly.
+    // lpg >= 16 lanes per group, so a 16-lane row holds at most two groups (its first and
+    // its last): one sum for each, slot 0 and slot 1 of the row's record.
+    const uint32_t gf = (uint32_t)fast_div(flat & ~15u, lpg_div), gla = (uint32_t)fast_div(flat | 15u, lpg_div);
+    uint32_t* rec = part + (row0 + (flat >> 4)) * 2 * P;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            put_byte(h, 1 + b, sent >> (8 * b));
-            put_byte(h, 5 + b, srcno >> (8 * b));
+    for (int q = 0; q < P; ++q) {
+        const uint32_t v0 = row16_sum(gl == gf ? ps[q] : 0u);
+        const uint32_t v1 = row16_sum(gl == gla && gla != gf ? ps[q] : 0u);
+        if (live && (flat & 15) == 0) {
+            rec[q] = v0;
+            rec[P + q] = v1;
         }
-        put_byte(h, 9, ikn);
-        put_byte(h, 10, ikn >> 8);
-        if (HDR == 13) {
-            // datagram checksum: byte sum of shard [0, len)
-            const uint32_t d = r < K ? psum[r] + ((uint32_t)size[r] & 0xFF) + (((uint32_t)size[r] >> 8) & 0xFF) +
-                                           (psum[r] & 0xFF) + (psum[r] >> 8)
-                                     : qsum[r - K];
-            put_byte(h, 11, d);
-            put_byte(h, 12, d >> 8);
-        }
-        if (ok && (t == 0 || 16 < HDR + len)) stw(out + (uint64_t)r * a.wire_pitch, pick16(t == 0, h, v), a.store_nt & 2);
-        if (t == 0) wire_len[g * N + r] = ok ? HDR + len : -1;
     }
 }
 
-template <int K, int M, int HDR>
-__global__ void __launch_bounds__(256) k_pack_head(WireArgs a, const uint8_t* __restrict__ payload,
-                                                   const int64_t* __restrict__ offsets,
-                                                   const int32_t* __restrict__ sizes,
+// HDR 13 only.  One lane per group, no payload reads (see the section comment).
+template <int K, int M>
+__global__ void __launch_bounds__(256) k_pack_head(WireArgs a, const int32_t* __restrict__ sizes,
                                                    const uint32_t* __restrict__ tab,
                                                    const uint32_t* __restrict__ part,
                                                    const uint32_t* __restrict__ seq, uint8_t* __restrict__ wire,
                                                    int32_t* __restrict__ wire_len, uint64_t g0, uint32_t lanes,
-                                                   uint32_t lpg) {
+                                                   uint32_t lpg, uint64_t row0) {
+    constexpr int N = K + M, HDR = 13, HEAD = 4, P = (N + 1) / 2;
     const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
-    head_lane<K, M, HDR, false>(a, payload, offsets, sizes, tab, part, seq, wire, wire_len, g0 + (flat >> 1),
-                                (int)(flat & 1), flat < lanes, lpg);
+    if (flat >= lanes) return;
+    const uint64_t g = g0 + flat;
+    int size[K], gmax = 0;
+    const bool ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+    if (!ok) {
+#pragma unroll
+        for (int r = 0; r < N; ++r) wire_len[g * N + r] = -1;
+        return;
+    }
+    uint32_t tot[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) tot[r] = 0;
+    // the body's 16-lane rows holding this group's lanes [flat0, flat0 + lpg)
+    const uint64_t flat0 = (uint64_t)flat * lpg;
+    for (uint64_t row = flat0 >> 4; row <= (flat0 + lpg - 1) >> 4; ++row) {
+        const uint32_t* rec = part + (row0 + row) * 2 * P + ((row << 4) >= flat0 ? 0 : P);
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const uint32_t v = rec[q];
+            tot[2 * q] += v & 0xFFFF;
+            if (2 * q + 1 < N) tot[2 * q + 1] += v >> 16;
+        }
+    }
+    const uint32_t sent0 = seq[2 * g], src0 = seq[2 * g + 1];
+    // shard bytes 0-3 of the data rows: [size lo][size hi][cksum lo][cksum hi]
+    uint32_t d[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) d[i] = ((uint32_t)size[i] & 0xFFFFu) | ((tot[i] & 0xFFFFu) << 16);
+    uint8_t* out = wire + g * (uint64_t)N * a.wire_pitch;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        uint32_t w;  // shard bytes 0-3 of row r
+        uint32_t dsum;
+        if (r < K) {
+            w = d[r];
+            dsum = tot[r] + (w & 0xFF) + ((w >> 8) & 0xFF) + ((w >> 16) & 0xFF) + (w >> 24);
+        } else {
+            w = 0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const uint32_t* e = tab + ((r - K) * K + i) * QFEC_TAB_STRIDE;
+                w ^= gf_mul4(gf_sel(d[i]), e[0], e[1], e[2], e[3], e[4]);
+            }
+            dsum = tot[r] + (w & 0xFF) + ((w >> 8) & 0xFF) + ((w >> 16) & 0xFF) + (w >> 24);
+        }
+        const int len = r < K ? size[r] + HEAD : gmax;
+        // chunk 0 = header (13) + shard bytes 0-2, masked to the datagram length
+        uint4 v = make_uint4(0, 0, 0, w << 8);
+        put_header<HDR>(v, sent0 + (uint32_t)r, src0 + (uint32_t)(r < K ? r : K - 1),
+                        ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu, dsum);
+        v = mask16(v, 0, HDR + len);
+        stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 2);
+        if (HDR + len > 16) out[(uint64_t)r * a.wire_pitch + 16] = (uint8_t)(w >> 24);
+        wire_len[g * N + r] = HDR + len;
+    }
 }
 
-// One launch: body lanes in batches of 8 blocks dealt to one XCD (blocks b, b + 8, ...,
-// b + 56 of each 64); a batch holds gpb whole groups (gpb * lpg <= 2048 lanes).  Each block
-// publishes its partial sums write-through, waits for its stores, and bumps the batch
-// counter; the block whose add is the batch's last runs the batch's heads (2 lanes per
-// group) while the payload lines they re-read are still in that XCD's L2.
-template <int K, int M, int HDR, bool UNI>
-__global__ void __launch_bounds__(256) k_pack_one(WireArgs a, const uint8_t* __restrict__ payload,
-                                                  const int64_t* __restrict__ offsets,
-                                                  const int32_t* __restrict__ sizes,
-                                                  const uint32_t* __restrict__ tab, uint32_t* __restrict__ part,
-                                                  uint32_t* __restrict__ counters, uint32_t lpg, DivMagic rows_div,
-                                                  uint32_t gpb, uint64_t nbatch) {
-    __shared__ uint32_t s_last;
-    const uint32_t b = blockIdx.x;
-    const uint64_t beta = (uint64_t)(b >> 6) * 8 + (b & 7);
-    const uint32_t lib = ((b >> 3) & 7) * 256u + threadIdx.x;  // lane in batch
-    const uint32_t gib = UNI ? __builtin_amdgcn_readfirstlane((uint32_t)fast_div(lib >> 6, rows_div))
-                             : (uint32_t)fast_div(lib >> 4, rows_div);
-    const uint64_t g = beta * gpb + gib;
-    const bool live = beta < nbatch && gib < gpb && g < a.groups;
-    body_lane<K, M, HDR, true>(a, payload, offsets, sizes, tab, part, live ? g : 0, lib - gib * lpg, live, lpg);
-    if (beta >= nbatch) return;  // whole block
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-        s_last = __hip_atomic_fetch_add(counters + beta, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 7;
-    __syncthreads();
-    if (!s_last || threadIdx.x >= 64) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const uint64_t gend = min((uint64_t)gpb, a.groups - beta * gpb);
-    for (uint32_t h0 = 0; h0 < 2 * gend; h0 += 64) {
-        const uint32_t h = h0 + threadIdx.x;
-        head_lane<K, M, HDR, true>(a, payload, offsets, sizes, tab, part, a.seq, a.wire, a.wire_len,
-                                   beta * gpb + (h >> 1), (int)(h & 1), h < 2 * gend, lpg);
+// ------------------------------------------------------------------ ProtocolUdp framing
+// The byte stage below FEC on every datagram:
+//   Session::PacketOutput (network/SessionDesc.cpp:69-77): mask = _mask++, push hid, push conv
+//   ProtocolUdp::SendPacket (network/ProtocolBasic.cpp:111-150): push protocol, push
+//     (cmd & 0x1f) | 0xA0, push c = CheckSum(all of it) & 0xff, XOR all of it with
+//     mask ^ gmask ^ 0x5a, push mask
+// so frame = [mask][c][cmd][proto]([conv LE][hid LE])[data], bytes 1.. XORed, with
+// CheckSum(x) = ~((s >> 16) + (s & 0xffff)), s = byte sum (ProtocolBasic.cpp:56-87).
+// One wave per row, 32 bytes per lane per pass; chunk 0 (which holds c) is written last.
+__device__ __forceinline__ uint4 xor16(uint4 v, uint32_t mm) {
+    return make_uint4(v.x ^ mm, v.y ^ mm, v.z ^ mm, v.w ^ mm);
+}
+
+__global__ void __launch_bounds__(256) k_frame_udp(FrameArgs a) {
+    const uint64_t row = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (row >= a.rows) return;
+    const int lane = threadIdx.x & 63;
+    const int P = a.session ? 12 : 4;
+    const int len = a.in_len[row];
+    const int total = P + len;
+    const uint8_t* in = a.in + row * a.in_pitch;
+    uint8_t* out = a.out + row * a.out_pitch;
+    if (len < 0 || total > (int)a.out_pitch || len > (int)a.in_pitch) {
+        if (lane == 0) a.out_len[row] = -1;
+        return;
+    }
+    const uint32_t m = a.mask[row];
+    const uint32_t x = (m ^ a.gmask ^ 0x5Au) & 0xFFu;
+    const uint32_t mm = x * 0x01010101u;
+    const int in_chunks = (int)(a.in_pitch / 16);
+    uint32_t sum = 0;
+    uint4 first = make_uint4(0, 0, 0, 0);
+    for (int q0 = 2 * lane; 16 * q0 < total; q0 += 128) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = q0 + h;
+            if (16 * q >= total) break;
+            // frame bytes [16q, 16q + 16) = data bytes [16q - P, 16q + 16 - P)
+            const uint4 lo = q >= 1 ? *reinterpret_cast<const uint4*>(in + 16 * (q - 1)) : make_uint4(0, 0, 0, 0);
+            const uint4 hi = q < in_chunks ? *reinterpret_cast<const uint4*>(in + 16 * q) : make_uint4(0, 0, 0, 0);
+            uint4 v = mask16(window(lo, hi, 16 - P), q == 0 ? P : 0, total - 16 * q);
+            sum = sum16(v, sum);
+            if (q == 0) {
+                first = v;
+            } else {
+                st16a(out + 16 * q, xor16(v, mm));
+            }
+        }
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) {
+        const uint32_t cmd = (a.cmd & 0x1Fu) | 0xA0u, proto = a.protocol & 0xFFu;
+        put_byte(first, 2, cmd);
+        put_byte(first, 3, proto);
+        uint32_t s2 = sum + cmd + proto;
+        if (a.session) {
+            const uint32_t conv = a.conv_hid[2 * row], hid = a.conv_hid[2 * row + 1];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                put_byte(first, 4 + b, conv >> (8 * b));
+                put_byte(first, 8 + b, hid >> (8 * b));
+                s2 += ((conv >> (8 * b)) & 0xFFu) + ((hid >> (8 * b)) & 0xFFu);
+            }
+        }
+        const uint32_t c = ~((s2 >> 16) + (s2 & 0xFFFFu)) & 0xFFu;
+        put_byte(first, 1, c);
+        first = xor16(first, mm);
+        put_byte(first, 0, m);
+        st16a(out, first);
+        a.out_len[row] = total;
+    }
+}
+
+// Reverse (ProtocolUdp::RecvPacket, ProtocolBasic.cpp:152-210): status 0 ok, 1 shorter than 4
+// bytes (or than the 12 with the Session prefix), 2 checksum, 3 cmd (& 0xe0 != 0xA0), 4 does
+// not fit the output pitch.  The data (frame bytes [P, len), un-XORed) is written for every
+// status but 1 and 4; out_len = len - P.
+__global__ void __launch_bounds__(256) k_unframe_udp(FrameArgs a) {
+    const uint64_t row = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (row >= a.rows) return;
+    const int lane = threadIdx.x & 63;
+    const int P = a.session ? 12 : 4;
+    const int len = a.in_len[row];
+    const uint8_t* in = a.in + row * a.in_pitch;
+    uint8_t* out = a.out + row * a.out_pitch;
+    if (len < P || len > (int)a.in_pitch || len - P > (int)a.out_pitch) {
+        if (lane == 0) {
+            a.status[row] = len < P ? 1 : 4;
+            a.out_len[row] = -1;
+        }
+        return;
+    }
+    const uint4 h0 = *reinterpret_cast<const uint4*>(in);
+    const uint32_t x = (get_byte(h0, 0) ^ a.gmask ^ 0x5Au) & 0xFFu;
+    const uint32_t mm = x * 0x01010101u;
+    const int in_chunks = (int)(a.in_pitch / 16);
+    const int dlen = len - P;
+    uint32_t sum = 0;  // frame bytes [2, len), un-XORed
+    for (int q0 = 2 * lane; 16 * q0 < len; q0 += 128) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = q0 + h;
+            if (16 * q >= len) break;
+            const uint4 f = xor16(*reinterpret_cast<const uint4*>(in + 16 * q), mm);
+            sum = sum16(mask16(f, 2 - 16 * q, len - 16 * q), sum);
+            // data chunk q = frame bytes [16q + P, 16q + P + 16)
+            if (16 * q < dlen) {
+                const uint4 nx = q + 1 < in_chunks ? xor16(*reinterpret_cast<const uint4*>(in + 16 * (q + 1)), mm)
+                                                   : make_uint4(0, 0, 0, 0);
+                st16a(out + 16 * q, mask16(window(f, nx, P), 0, dlen - 16 * q));
+            }
+        }
+    }
+    sum = wave_sum(sum);
+    if (lane == 0) {
+        const uint4 f0 = xor16(h0, mm);
+        const uint32_t check = get_byte(f0, 1), cmd = get_byte(f0, 2);
+        const uint32_t c = ~((sum >> 16) + (sum & 0xFFFFu)) & 0xFFu;
+        a.status[row] = c != check ? 2 : (cmd & 0xE0u) != 0xA0u ? 3 : 0;
+        a.out_len[row] = dlen;
+        if (a.info) {
+            a.info[4 * row + 0] = (uint8_t)x;
+            a.info[4 * row + 1] = (uint8_t)check;
+            a.info[4 * row + 2] = (uint8_t)(cmd & 0x1Fu);
+            a.info[4 * row + 3] = (uint8_t)get_byte(f0, 3);
+        }
+        if (a.session && a.conv_hid) {
+            uint32_t conv = 0, hid = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                conv |= get_byte(f0, 4 + b) << (8 * b);
+                hid |= get_byte(f0, 8 + b) << (8 * b);
+            }
+            a.conv_hid[2 * row] = conv;
+            a.conv_hid[2 * row + 1] = hid;
+        }
     }
 }
 
@@ -646,43 +714,22 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s) {
 
 template <int K, int M, int HDR>
 hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s) {
-    // lanes per group for t >= 2 cover the longest datagram the shard pitch allows
+    // body lanes per group cover chunks [TS, tn): the longest datagram the shard pitch allows;
+    // groups are packed back to back (no rounding), partial sums go per 16-lane row
+    constexpr uint32_t TS = HDR == 13 ? 1 : 0;
     const uint32_t tn = (uint32_t)((HDR + a.pitch + 15) / 16);
-    uint32_t lpg = std::max(16u, (tn - 2 + 15) / 16 * 16);
-    const int uni_mode = tuning().wire_uni;
-    if (uni_mode == 2) lpg = (lpg + 63) / 64 * 64;
-    const bool uni = uni_mode != 0 && lpg % 64 == 0;
-    const DivMagic rows_div = make_div_magic(uni ? lpg / 64 : lpg / 16);
-    const uint32_t gpb = 2048 / lpg;
-    if (tuning().wire_fused == 2 && gpb >= 1) {
-        const uint64_t nbatch = (a.groups + gpb - 1) / gpb;
-        const uint32_t P = (uint32_t)(a.k + a.m + 1) / 2;
-        uint32_t* counters = part + a.groups * (lpg / 16) * P;
-        hipError_t e = hipMemsetAsync(counters, 0, nbatch * 4, s);
-        if (e != hipSuccess) return e;
-        const uint64_t blocks = (nbatch + 7) / 8 * 64;
-        if (blocks >= (1ull << 31)) return hipErrorInvalidValue;
-        if (uni)
-            hipLaunchKernelGGL((k_pack_one<K, M, HDR, true>), dim3((unsigned)blocks), dim3(256), 0, s, a, a.payload,
-                               a.offsets, a.sizes, tab, part, counters, lpg, rows_div, gpb, nbatch);
-        else
-            hipLaunchKernelGGL((k_pack_one<K, M, HDR, false>), dim3((unsigned)blocks), dim3(256), 0, s, a, a.payload,
-                               a.offsets, a.sizes, tab, part, counters, lpg, rows_div, gpb, nbatch);
-        return hipGetLastError();
-    }
-    const uint64_t per = ((uint64_t)1 << 30) / lpg;  // groups per launch: lanes < 2^30
+    const uint32_t lpg = std::max(16u, tn - TS);
+    const DivMagic lpg_div = make_div_magic(lpg);
+    const uint64_t per = (((uint64_t)1 << 30) / lpg) & ~(uint64_t)15;  // keeps g0 * lpg % 16 == 0
     for (uint64_t g0 = 0; g0 < a.groups; g0 += per) {
         const uint64_t gn = std::min(per, a.groups - g0);
-        const uint32_t lanes = (uint32_t)(gn * lpg);
-        if (uni)
-            hipLaunchKernelGGL((k_pack_body<K, M, HDR, true>), dim3((lanes + 255) / 256), dim3(256), 0, s, a,
-                               a.payload, a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
-        else
-            hipLaunchKernelGGL((k_pack_body<K, M, HDR, false>), dim3((lanes + 255) / 256), dim3(256), 0, s, a,
-                               a.payload, a.offsets, a.sizes, tab, part, g0, lanes, lpg, rows_div);
-        const uint32_t hl = (uint32_t)(2 * gn);
-        hipLaunchKernelGGL((k_pack_head<K, M, HDR>), dim3((hl + 255) / 256), dim3(256), 0, s, a, a.payload, a.offsets,
-                           a.sizes, tab, (const uint32_t*)part, a.seq, a.wire, a.wire_len, g0, hl, lpg);
+        const uint32_t lanes = (uint32_t)(gn * lpg);  // the grid covers whole 16-lane rows past it
+        const uint64_t row0 = g0 * lpg / 16;
+        hipLaunchKernelGGL((k_pack_body<K, M, HDR>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
+                           a.offsets, a.sizes, a.seq, tab, part, g0, lanes, lpg, lpg_div, row0);
+        if (HDR == 13)
+            hipLaunchKernelGGL((k_pack_head<K, M>), dim3((unsigned)((gn + 255) / 256)), dim3(256), 0, s, a, a.sizes,
+                               tab, (const uint32_t*)part, a.seq, a.wire, a.wire_len, g0, (uint32_t)gn, lpg, row0);
     }
     return hipGetLastError();
 }
@@ -711,6 +758,18 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
     return hipSuccess;
 }
 #undef QFEC_PACK_CASE
+
+hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s) {
+    if (!a.rows) return hipSuccess;
+    hipLaunchKernelGGL(k_frame_udp, dim3(waves_grid(a.rows)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_unframe_udp(const FrameArgs& a, hipStream_t s) {
+    if (!a.rows) return hipSuccess;
+    hipLaunchKernelGGL(k_unframe_udp, dim3(waves_grid(a.rows)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_emit_wire(const WireArgs& a, hipStream_t s) {
     const uint64_t slots = a.groups * (uint64_t)(a.k + a.m);

@@ -24,11 +24,11 @@ def padded_payload(p):
     return dev(np.concatenate([p, np.zeros(16, np.uint8)]))  # 16 readable bytes past the end
 
 
-@pytest.fixture(params=[1, 2, 0], ids=["fused2", "fused1", "staged"])
+@pytest.fixture(params=[(1, 0), (0, 0)], ids=["fused", "staged"])
 def wire_fused(request):
-    """Every send path: fused body + head launches, the one-launch fused pack (templated
-    (k, m)), and the staged build -> encode -> emit pipeline every shape can take."""
-    qa.tune("wire_fused", request.param)
+    """Both send paths: the fused body + head launches (templated (k, m)) and the staged
+    build -> encode -> emit pipeline every shape can take."""
+    qa.tune("wire_fused", request.param[0])
     yield request.param
     qa.tune("wire_fused", 1)
 

@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 import quicknet_amd as qa  # noqa: E402
 
-KNOBS = {"wire_fused": 1, "wire_uni": 1, "wire_store_nt": 3}
+KNOBS = {"wire_fused": 1, "wire_store_nt": 3}
 
 
 def main():
@@ -27,7 +27,7 @@ def main():
     p.add_argument("--groups", type=int, default=100_000)
     p.add_argument("--rounds", type=int, default=10)
     p.add_argument("--reps", type=int, default=10)
-    p.add_argument("--variants", default="base;wire_store_nt=0;wire_store_nt=1;wire_store_nt=2;wire_uni=0;wire_fused=0")
+    p.add_argument("--variants", default="base;wire_store_nt=0;wire_store_nt=1;wire_fused=0")
     a = p.parse_args()
     k, n, G, S = a.k, a.n, a.groups, a.size
     dev = torch.device("cuda:0")

@@ -28,10 +28,8 @@ def main():
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--cpu-seconds", type=float, default=5.0)
     p.add_argument("--staged", action="store_true", help="force the 3-kernel send pipeline")
-    p.add_argument("--uni", type=int, default=1, help="fused body group mapping (qfec_tune wire_uni 0|1|2)")
     a = p.parse_args()
     qa.tune("wire_fused", 0 if a.staged else 1)
-    qa.tune("wire_uni", a.uni)
     k, n, G, S = a.k, a.n, a.groups, a.size
     dev = torch.device("cuda:0")
     code = qa.Code.vandermonde(k, n - k)
@@ -82,7 +80,7 @@ def main():
         cpu = json.loads(r.stdout) if r.returncode == 0 else {"error": r.stderr[-200:]}
         cpu["kind"] = "reference (network/FecCodecBuf.cpp + system/fec.c, 1 thread)"
     print(json.dumps({
-        "send_path": "staged" if a.staged else f"fused(uni={a.uni})",
+        "send_path": "staged" if a.staged else "fused",
         "workload": f"{G} groups x RS({k},{n}) x {S}-B payloads, checksum on, {n - k} random losses/group",
         "pack_ms": round(t_pack, 4), "pack_payload_gibs": round(gib / (t_pack * 1e-3), 1),
         "unpack_ms": round(t_unpack, 4), "unpack_payload_gibs": round(gib / (t_unpack * 1e-3), 1),
