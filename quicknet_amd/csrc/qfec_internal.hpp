@@ -107,6 +107,9 @@ struct FrameArgs {
     int session;              // 1: the 8-byte conv/hid prefix is part of the frame
 };
 hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s);
+// fused receive for templated (k, m); *launched = false when the shape has no instance
+hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
+                               hipStream_t s, bool* launched);
 hipError_t launch_unframe_udp(const FrameArgs& a, hipStream_t s);
 hipError_t launch_emit_wire(const WireArgs& a, hipStream_t s);
 hipError_t launch_parse_wire(const WireArgs& a, hipStream_t s);
@@ -117,6 +120,7 @@ struct Tuning {
     int recon_impl = -1;  // -1 auto (per shape), 0 row loop, 1 all rows
     int encode_impl = 0;
     int wire_fused = 1;     // fused datagram send where a (k, m) instance exists (0: staged)
+    int wire_fused_rx = 1;  // fused datagram receive likewise
     int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
 };
 Tuning& tuning();

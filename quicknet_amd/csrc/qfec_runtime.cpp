@@ -494,6 +494,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "recon_impl") && value >= -1 && value <= 1) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
@@ -747,6 +748,13 @@ int qfec_unpack_datagrams(qfec_code* code, const unsigned char* d_wire, long lon
     a.m = m;
     a.checksum = checksum;
     a.dec_pkt_size = dec_pkt_size;
+    if (tuning().wire_fused_rx && d->d_lut) {
+        bool launched = false;
+        const hipError_t ef =
+            launch_unpack_fused(a, d->d_lut, d->d_rec, (uint32_t)record_layout(k, m).hdr, s, &launched);
+        if (ef != hipSuccess) return hip_fail(ef, "unpack_fused launch");
+        if (launched) return QFEC_OK;
+    }
     hipError_t e = launch_parse_wire(a, s);
     if (e != hipSuccess) return hip_fail(e, "parse_wire launch");
     // decode the missing data shards from the first k valid ones in group order

@@ -563,6 +563,331 @@ __global__ void __launch_bounds__(256) k_pack_head(WireArgs a, const int32_t* __
     }
 }
 
+// ------------------------------------------------------------------ receive: fused
+// For compile-time (K, M), parse -> reconstruct -> check collapse into one launch, one wave
+// per group: HBM traffic is the received datagrams in and the k data rows out (check-shard
+// rows of d_shards are not written on this path).
+//  1. lanes j < n parse datagram j's header (unpack_fec_head's tests, FecCodecBuf.cpp:334-411)
+//  2. survivors = the first k rows in group order whose header is good -- optimistic: their
+//     shard checksums are verified in step 4 and a bad one restarts the group without it,
+//     so the final survivors are the first k VALID rows (NetFecCodec.cpp:504-528).
+//  3. passes over the shard columns (16 B per lane, then one 4-B-per-lane tail pass when
+//     fewer than 17 chunks remain): survivor chunks are loaded straight from the datagrams
+//     (unaligned), lost data rows decoded with the record's perm tables, the k data rows
+//     stored, and shard / payload byte sums accumulated.
+//  4. wave sums -> datagram checksum verdicts, then dec_src_pkt_info's status per data row.
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+template <int NV>
+__device__ __forceinline__ void ld_vec(uint32_t (&v)[NV], const uint8_t* p) {
+    __builtin_memcpy(v, p, 4 * NV);
+}
+template <int NV>
+__device__ __forceinline__ void st_vec(uint8_t* p, const uint32_t (&v)[NV]) {
+    if (NV == 4) st16(p, make_uint4(v[0], v[1], v[2], v[3]));
+    else *reinterpret_cast<uint32_t*>(p) = v[0];
+}
+template <int NV>
+__device__ __forceinline__ void mask_vec(uint32_t (&v)[NV], int lo, int hi) {
+#pragma unroll
+    for (int d = 0; d < NV; ++d) v[d] &= byte_mask(lo, hi, d);
+}
+template <int NV>
+__device__ __forceinline__ uint32_t sum_vec(const uint32_t (&v)[NV]) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int d = 0; d < NV; ++d) s = __builtin_amdgcn_sad_u8(v[d], 0u, s);
+    return s;
+}
+
+// the group's plan, wave-uniform
+template <int K, int M>
+struct UnpackPlan {
+    uint32_t sv_off[K];   // survivor c: datagram row offset + its header length
+    int sv_row[K], sv_size[K];
+    int ns;               // survivors loaded (K when recoverable, else the valid data rows)
+    int lost_row[M], e;   // decoded rows
+    const uint32_t* tab;
+    uint32_t zero_rows;   // data rows to zero (lost, group not recoverable)
+    uint32_t ex_off[M];   // rows only checksummed (first round)
+    int ex_row[M], ex_size[M], nx;
+};
+
+template <int K, int M, int NV>
+__device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const uint8_t* __restrict__ wire_g,
+                                            uint8_t* __restrict__ out_g, uint64_t pitch, int pos, bool active,
+                                            bool first_pass, int checksum, uint32_t (&dsum)[K],
+                                            uint32_t (&xsum)[M], uint32_t (&ps_s)[K], uint32_t (&ps_l)[M],
+                                            uint32_t (&w0_s)[K], uint32_t (&w0_l)[M]) {
+    uint32_t x[K][NV];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+#pragma unroll
+        for (int d = 0; d < NV; ++d) x[c][d] = 0;
+        if (c < pl.ns && active) ld_vec<NV>(x[c], wire_g + pl.sv_off[c] + pos);
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        mask_vec<NV>(x[c], 0, pl.sv_size[c] - pos);
+        dsum[c] += sum_vec<NV>(x[c]);
+    }
+    uint32_t acc[M][NV];
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int d = 0; d < NV; ++d) acc[j][d] = 0;
+    if (pl.e > 0) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            Sel sc[NV];
+#pragma unroll
+            for (int d = 0; d < NV; ++d) sc[d] = gf_sel(x[c][d]);
+#pragma unroll
+            for (int j = 0; j < M; ++j) {
+                if (j < pl.e) {
+                    const uint32_t* t = pl.tab + (j * K + c) * QFEC_TAB_STRIDE;
+                    const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
+#pragma unroll
+                    for (int d = 0; d < NV; ++d)
+                        acc[j][d] = xor3(acc[j][d], pp0(sc[d], t0, t1), pp1(sc[d], t2, t3)) ^ pp2(sc[d], t4);
+                }
+            }
+        }
+    }
+    // the first shard chunk of every output row: size (bytes 0-1) and payload checksum (2-3)
+    if (first_pass) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) w0_s[c] = (uint32_t)__builtin_amdgcn_readlane((int)x[c][0], 0);
+#pragma unroll
+        for (int j = 0; j < M; ++j) w0_l[j] = (uint32_t)__builtin_amdgcn_readlane((int)acc[j][0], 0);
+    }
+    const int head = checksum ? 4 : 2;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        if (c < pl.ns && pl.sv_row[c] < K) {
+            if (active) st_vec<NV>(out_g + (uint64_t)pl.sv_row[c] * pitch + pos, x[c]);
+            uint32_t y[NV];
+#pragma unroll
+            for (int d = 0; d < NV; ++d) y[d] = x[c][d];
+            mask_vec<NV>(y, head - pos, head + (int)(w0_s[c] & 0xFFFF) - pos);
+            ps_s[c] += sum_vec<NV>(y);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        if (j < pl.e) {
+            if (active) st_vec<NV>(out_g + (uint64_t)pl.lost_row[j] * pitch + pos, acc[j]);
+            mask_vec<NV>(acc[j], head - pos, head + (int)(w0_l[j] & 0xFFFF) - pos);
+            ps_l[j] += sum_vec<NV>(acc[j]);
+        }
+    }
+    if (pl.zero_rows && active) {
+        uint32_t z[NV];
+#pragma unroll
+        for (int d = 0; d < NV; ++d) z[d] = 0;
+        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1)
+            st_vec<NV>(out_g + (uint64_t)__builtin_ctz(zr) * pitch + pos, z);
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        if (r < pl.nx) {
+            uint32_t y[NV];
+#pragma unroll
+            for (int d = 0; d < NV; ++d) y[d] = 0;
+            if (active) ld_vec<NV>(y, wire_g + pl.ex_off[r] + pos);
+            mask_vec<NV>(y, 0, pl.ex_size[r] - pos);
+            xsum[r] += sum_vec<NV>(y);
+        }
+    }
+}
+
+template <int K, int M>
+__global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t* __restrict__ wire,
+                                                      const int32_t* __restrict__ wire_len,
+                                                      const int32_t* __restrict__ lut,
+                                                      const uint32_t* __restrict__ records, uint32_t rec_hdr,
+                                                      uint8_t* __restrict__ shards) {
+    constexpr int N = K + M;
+    const int lane = threadIdx.x & 63;
+    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (g >= a.groups) return;
+    const uint64_t wp = a.wire_pitch, pitch = a.pitch;
+    const uint8_t* wire_g = wire + g * (uint64_t)N * wp;
+    uint8_t* out_g = shards + g * a.group_stride;
+    // ---- 1. headers
+    int len = 0, hdr = 11, size = 0;
+    uint32_t stated = 0;
+    bool okh = false;
+    if (lane < N) {
+        len = wire_len[g * N + lane];
+        uint4 h = make_uint4(0, 0, 0, 0);
+        if (len >= 11 && len <= (int)wp) h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
+        const uint32_t tag = get_byte(h, 0);
+        hdr = tag == 0xED ? 13 : 11;
+        const uint32_t ikn = get_byte(h, 9) | (get_byte(h, 10) << 8);
+        okh = len >= 11 && len <= (int)wp && (tag == 0xEC || tag == 0xED) && len >= hdr &&
+              (int)(ikn & 0xF) == N && (int)((ikn >> 4) & 0xF) == K && (int)((ikn >> 8) & 0xF) == lane &&
+              len - hdr <= (int)pitch;
+        size = okh ? len - hdr : 0;
+        stated = get_byte(h, 11) | (get_byte(h, 12) << 8);
+    }
+    const uint32_t rowmask = (1u << N) - 1u;
+    uint32_t good = (uint32_t)__ballot(okh) & rowmask;           // header fine
+    const uint32_t summed13 = (uint32_t)__ballot(okh && hdr == 13) & rowmask;
+    // per-row values for a wave-uniform row r: v_readlane with an SGPR lane index
+    auto r_hdr = [&](int r) { return __builtin_amdgcn_readlane(hdr, r); };
+    auto r_size = [&](int r) { return __builtin_amdgcn_readlane(size, r); };
+    auto r_stated = [&](int r) { return (uint32_t)__builtin_amdgcn_readlane((int)stated, r); };
+    // ---- 2-4, repeated without any survivor whose shard checksum fails
+    uint32_t verified = 0;    // rows whose checksum is known good
+    uint32_t bad = 0;         // rows whose checksum failed
+    uint32_t w0_s[K], w0_l[M], ps_s[K], ps_l[M];
+    UnpackPlan<K, M> pl;
+    bool recoverable = false;
+    uint32_t lost_data = 0;
+    for (int round = 0; round <= N; ++round) {
+        const uint32_t avail = good & ~bad;
+        lost_data = ~avail & ((1u << K) - 1u);
+        recoverable = __builtin_popcount(avail) >= K;
+        pl.ns = 0;
+        pl.e = 0;
+        pl.zero_rows = 0;
+        pl.tab = records;
+        uint32_t take = avail;
+        // survivors: the lowest K available rows; unrecoverable: just the available data rows
+        if (!recoverable) {
+            take = avail & ((1u << K) - 1u);
+            pl.zero_rows = lost_data;
+        }
+        uint32_t svmask = 0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            pl.sv_row[c] = 0;
+            if (take) {
+                pl.sv_row[c] = __builtin_ctz(take);
+                take &= take - 1;
+                pl.ns = c + 1;
+                svmask |= 1u << pl.sv_row[c];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) pl.lost_row[j] = 0;
+        if (recoverable && lost_data) {
+            const int rec = lut[(~avail) & rowmask];
+            pl.tab = records + rec + rec_hdr;
+            pl.e = (int)records[rec];
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+                if (j < pl.e) pl.lost_row[j] = (int)records[rec + 4 + K + j];
+        }
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const int r = pl.sv_row[c];
+            pl.sv_off[c] = (uint32_t)((uint64_t)r * wp + (uint64_t)r_hdr(r));
+            pl.sv_size[c] = c < pl.ns ? r_size(r) : 0;
+        }
+        // rows only checksummed: good headers with a checksum, not loaded as survivors, not yet known
+        uint32_t extra = good & summed13 & ~svmask & ~verified & ~bad;
+        pl.nx = 0;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            pl.ex_row[r] = 0;
+            pl.ex_off[r] = 0;
+            pl.ex_size[r] = 0;
+            if (extra) {
+                const int rr = __builtin_ctz(extra);
+                extra &= extra - 1;
+                pl.ex_row[r] = rr;
+                pl.ex_off[r] = (uint32_t)((uint64_t)rr * wp + 13u);
+                pl.ex_size[r] = r_size(rr);
+                pl.nx = r + 1;
+            }
+        }
+        uint32_t dsum[K], xsum[M];
+#pragma unroll
+        for (int c = 0; c < K; ++c) dsum[c] = ps_s[c] = 0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) xsum[j] = ps_l[j] = 0;
+        const int chunks = (int)(pitch / 16);
+        int q0 = 0;
+        for (; chunks - q0 > 16; q0 += 64)
+            unpack_pass<K, M, 4>(pl, wire_g, out_g, pitch, 16 * (q0 + lane), q0 + lane < chunks, q0 == 0,
+                                 a.checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
+        if (q0 < chunks)  // <= 16 chunks left: 4 bytes per lane
+            unpack_pass<K, M, 1>(pl, wire_g, out_g, pitch, 16 * q0 + 4 * lane, 4 * lane < 16 * (chunks - q0),
+                                 q0 == 0, a.checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
+        // ---- verdicts
+        uint32_t newbad = 0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const uint32_t t = wave_total(dsum[c]);
+            ps_s[c] = wave_total(ps_s[c]);
+            if (c < pl.ns) {
+                const int r = pl.sv_row[c];
+                if ((summed13 >> r) & 1u) {
+                    if ((t & 0xFFFFu) != r_stated(r)) newbad |= 1u << r;
+                    else verified |= 1u << r;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const uint32_t t = wave_total(xsum[j]);
+            ps_l[j] = wave_total(ps_l[j]);
+            if (j < pl.nx) {
+                const int r = pl.ex_row[j];
+                if ((t & 0xFFFFu) != r_stated(r)) bad |= 1u << r;
+                else verified |= 1u << r;
+            }
+        }
+        if (!(newbad & svmask)) break;
+        bad |= newbad;
+    }
+    // ---- per-row results
+    const uint32_t okrows = good & ~bad;
+    if (lane < N) {
+        const bool ok = (okrows >> lane) & 1u;
+        if (lane < K) a.marks[g * K + lane] = ok ? 0 : 1;
+        else a.marks[a.groups * K + g * M + (lane - K)] = ok ? 0 : 1;
+        if (a.rx_size) a.rx_size[g * N + lane] = ok ? size : -1;
+    }
+    // dec_src_pkt_info per data row (k_check_payloads' rules)
+    int st = 0, psz = 0;
+    const int head = a.checksum ? 4 : 2;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        if (c < pl.ns && pl.sv_row[c] < K && lane == pl.sv_row[c]) {
+            psz = (int)(w0_s[c] & 0xFFFF);
+            st = psz >= a.dec_pkt_size || head + psz > (int)pitch ? -1
+                 : a.checksum && (ps_s[c] & 0xFFFFu) != (w0_s[c] >> 16) ? -1 : head;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        if (j < pl.e && lane == pl.lost_row[j]) {
+            psz = (int)(w0_l[j] & 0xFFFF);
+            st = psz >= a.dec_pkt_size || head + psz > (int)pitch ? -1
+                 : a.checksum && (ps_l[j] & 0xFFFFu) != (w0_l[j] >> 16) ? -1 : head;
+        }
+    }
+    if (lane < K && !recoverable && ((lost_data >> lane) & 1u)) {
+        st = -2;
+        psz = 0;
+    }
+    if (lane < K) {
+        a.status[g * K + lane] = st;
+        a.psize[g * K + lane] = psz;
+    }
+}
+
 // ------------------------------------------------------------------ ProtocolUdp framing
 // The byte stage below FEC on every datagram:
 //   Session::PacketOutput (network/SessionDesc.cpp:69-77): mask = _mask++, push hid, push conv
@@ -758,6 +1083,32 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
     return hipSuccess;
 }
 #undef QFEC_PACK_CASE
+
+#define QFEC_UNPACK_CASE(KK, MM)                                                                        \
+    if (a.k == KK && a.m == MM) {                                                                       \
+        hipLaunchKernelGGL((k_unpack_fused<KK, MM>), dim3(waves_grid(a.groups)), dim3(256), 0, s, a, a.wire, \
+                           (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);                \
+        *launched = true;                                                                               \
+        return hipGetLastError();                                                                       \
+    }
+
+hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
+                               hipStream_t s, bool* launched) {
+    *launched = false;
+    if (!a.groups) return hipSuccess;
+    QFEC_UNPACK_CASE(10, 3)
+    QFEC_UNPACK_CASE(4, 1)
+    QFEC_UNPACK_CASE(4, 2)
+    QFEC_UNPACK_CASE(2, 2)
+    QFEC_UNPACK_CASE(3, 1)
+    QFEC_UNPACK_CASE(3, 2)
+    QFEC_UNPACK_CASE(5, 1)
+    QFEC_UNPACK_CASE(5, 3)
+    QFEC_UNPACK_CASE(7, 1)
+    QFEC_UNPACK_CASE(8, 4)
+    return hipSuccess;
+}
+#undef QFEC_UNPACK_CASE
 
 hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s) {
     if (!a.rows) return hipSuccess;
