@@ -586,20 +586,40 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-template <int NV>
-__device__ __forceinline__ void ld_vec(uint32_t (&v)[NV], const uint8_t* p) {
-    __builtin_memcpy(v, p, 4 * NV);
-}
-template <int NV>
-__device__ __forceinline__ void st_vec(uint8_t* p, const uint32_t (&v)[NV]) {
-    if (NV == 4) st16(p, make_uint4(v[0], v[1], v[2], v[3]));
-    else *reinterpret_cast<uint32_t*>(p) = v[0];
-}
-template <int NV>
-__device__ __forceinline__ void mask_vec(uint32_t (&v)[NV], int lo, int hi) {
+// A lane's slice of a shard row in one pass: NV16 = 4 -> one 16-B chunk at pos16, then NVT
+// tail dwords at tail + 4 * (lane + 64 t) (coalesced per instruction).  Dword d sits at
+// byte pos(d) of the row.
+template <int NV16, int NVT>
+struct Slice {
+    static constexpr int NV = NV16 + NVT;
+    int pos16, tail, lane;
+    bool act16;
+    int tail_end;  // tail dwords past this byte are inactive
+    __device__ __forceinline__ int pos(int d) const { return d < NV16 ? pos16 + 4 * d : tail + 4 * (lane + 64 * (d - NV16)); }
+    __device__ __forceinline__ bool act(int d) const { return d < NV16 ? act16 : pos(d) < tail_end; }
+    __device__ __forceinline__ void load(uint32_t (&v)[NV], const uint8_t* row) const {
+        if (NV16 && act16) {
+            uint4 w;
+            __builtin_memcpy(&w, row + pos16, 16);
+            v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+        }
 #pragma unroll
-    for (int d = 0; d < NV; ++d) v[d] &= byte_mask(lo, hi, d);
-}
+        for (int d = NV16; d < NV; ++d)
+            if (act(d)) __builtin_memcpy(&v[d], row + pos(d), 4);
+    }
+    __device__ __forceinline__ void store(uint8_t* row, const uint32_t (&v)[NV]) const {
+        if (NV16 && act16) st16(row + pos16, make_uint4(v[0], v[1], v[2], v[3]));
+#pragma unroll
+        for (int d = NV16; d < NV; ++d)
+            if (act(d)) *reinterpret_cast<uint32_t*>(row + pos(d)) = v[d];
+    }
+    // keep the bytes of row positions [lo, hi)
+    __device__ __forceinline__ void mask(uint32_t (&v)[NV], int lo, int hi) const {
+#pragma unroll
+        for (int d = 0; d < NV; ++d) v[d] &= byte_mask(lo - pos(d), hi - pos(d), 0);
+    }
+};
+
 template <int NV>
 __device__ __forceinline__ uint32_t sum_vec(const uint32_t (&v)[NV]) {
     uint32_t s = 0;
@@ -621,22 +641,23 @@ struct UnpackPlan {
     int ex_row[M], ex_size[M], nx;
 };
 
-template <int K, int M, int NV>
+template <int K, int M, int NV16, int NVT>
 __device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const uint8_t* __restrict__ wire_g,
-                                            uint8_t* __restrict__ out_g, uint64_t pitch, int pos, bool active,
-                                            bool first_pass, int checksum, uint32_t (&dsum)[K],
-                                            uint32_t (&xsum)[M], uint32_t (&ps_s)[K], uint32_t (&ps_l)[M],
-                                            uint32_t (&w0_s)[K], uint32_t (&w0_l)[M]) {
+                                            uint8_t* __restrict__ out_g, uint64_t pitch,
+                                            const Slice<NV16, NVT>& sl, bool first_pass, int checksum,
+                                            uint32_t (&dsum)[K], uint32_t (&xsum)[M], uint32_t (&ps_s)[K],
+                                            uint32_t (&ps_l)[M], uint32_t (&w0_s)[K], uint32_t (&w0_l)[M]) {
+    constexpr int NV = NV16 + NVT;
     uint32_t x[K][NV];
 #pragma unroll
     for (int c = 0; c < K; ++c) {
 #pragma unroll
         for (int d = 0; d < NV; ++d) x[c][d] = 0;
-        if (c < pl.ns && active) ld_vec<NV>(x[c], wire_g + pl.sv_off[c] + pos);
+        if (c < pl.ns) sl.load(x[c], wire_g + pl.sv_off[c]);
     }
 #pragma unroll
     for (int c = 0; c < K; ++c) {
-        mask_vec<NV>(x[c], 0, pl.sv_size[c] - pos);
+        sl.mask(x[c], 0, pl.sv_size[c]);
         dsum[c] += sum_vec<NV>(x[c]);
     }
     uint32_t acc[M][NV];
@@ -650,19 +671,20 @@ __device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const ui
             Sel sc[NV];
 #pragma unroll
             for (int d = 0; d < NV; ++d) sc[d] = gf_sel(x[c][d]);
+            // all M rows, no branch on e: records are padded to M rows (zero tables), and
+            // unconditional scalar loads batch instead of one s_load round trip per entry
 #pragma unroll
             for (int j = 0; j < M; ++j) {
-                if (j < pl.e) {
-                    const uint32_t* t = pl.tab + (j * K + c) * QFEC_TAB_STRIDE;
-                    const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
+                const uint32_t* t = pl.tab + (j * K + c) * QFEC_TAB_STRIDE;
+                const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
 #pragma unroll
-                    for (int d = 0; d < NV; ++d)
-                        acc[j][d] = xor3(acc[j][d], pp0(sc[d], t0, t1), pp1(sc[d], t2, t3)) ^ pp2(sc[d], t4);
-                }
+                for (int d = 0; d < NV; ++d)
+                    acc[j][d] = xor3(acc[j][d], pp0(sc[d], t0, t1), pp1(sc[d], t2, t3)) ^ pp2(sc[d], t4);
             }
         }
     }
-    // the first shard chunk of every output row: size (bytes 0-1) and payload checksum (2-3)
+    // the first shard dword of every output row (lane 0, dword 0 of the first pass):
+    // size (bytes 0-1) and payload checksum (2-3)
     if (first_pass) {
 #pragma unroll
         for (int c = 0; c < K; ++c) w0_s[c] = (uint32_t)__builtin_amdgcn_readlane((int)x[c][0], 0);
@@ -673,28 +695,24 @@ __device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const ui
 #pragma unroll
     for (int c = 0; c < K; ++c) {
         if (c < pl.ns && pl.sv_row[c] < K) {
-            if (active) st_vec<NV>(out_g + (uint64_t)pl.sv_row[c] * pitch + pos, x[c]);
-            uint32_t y[NV];
-#pragma unroll
-            for (int d = 0; d < NV; ++d) y[d] = x[c][d];
-            mask_vec<NV>(y, head - pos, head + (int)(w0_s[c] & 0xFFFF) - pos);
-            ps_s[c] += sum_vec<NV>(y);
+            sl.store(out_g + (uint64_t)pl.sv_row[c] * pitch, x[c]);
+            sl.mask(x[c], head, head + (int)(w0_s[c] & 0xFFFF));
+            ps_s[c] += sum_vec<NV>(x[c]);
         }
     }
 #pragma unroll
     for (int j = 0; j < M; ++j) {
         if (j < pl.e) {
-            if (active) st_vec<NV>(out_g + (uint64_t)pl.lost_row[j] * pitch + pos, acc[j]);
-            mask_vec<NV>(acc[j], head - pos, head + (int)(w0_l[j] & 0xFFFF) - pos);
+            sl.store(out_g + (uint64_t)pl.lost_row[j] * pitch, acc[j]);
+            sl.mask(acc[j], head, head + (int)(w0_l[j] & 0xFFFF));
             ps_l[j] += sum_vec<NV>(acc[j]);
         }
     }
-    if (pl.zero_rows && active) {
+    if (pl.zero_rows) {
         uint32_t z[NV];
 #pragma unroll
         for (int d = 0; d < NV; ++d) z[d] = 0;
-        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1)
-            st_vec<NV>(out_g + (uint64_t)__builtin_ctz(zr) * pitch + pos, z);
+        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) sl.store(out_g + (uint64_t)__builtin_ctz(zr) * pitch, z);
     }
 #pragma unroll
     for (int r = 0; r < M; ++r) {
@@ -702,14 +720,48 @@ __device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const ui
             uint32_t y[NV];
 #pragma unroll
             for (int d = 0; d < NV; ++d) y[d] = 0;
-            if (active) ld_vec<NV>(y, wire_g + pl.ex_off[r] + pos);
-            mask_vec<NV>(y, 0, pl.ex_size[r] - pos);
+            sl.load(y, wire_g + pl.ex_off[r]);
+            sl.mask(y, 0, pl.ex_size[r]);
             xsum[r] += sum_vec<NV>(y);
         }
     }
 }
 
-template <int K, int M>
+// all passes over a row of `chunks` 16-B chunks: 16-B passes, <= 16 chunks left over as one
+// dword per lane -- in a pass of its own, or (FUSE_TAIL) riding on the last 16-B pass
+template <int K, int M, bool FUSE_TAIL>
+__device__ __forceinline__ void unpack_row_passes(const UnpackPlan<K, M>& pl, const uint8_t* __restrict__ wire_g,
+                                                  uint8_t* __restrict__ out_g, uint64_t pitch, int lane,
+                                                  int checksum, uint32_t (&dsum)[K], uint32_t (&xsum)[M],
+                                                  uint32_t (&ps_s)[K], uint32_t (&ps_l)[M], uint32_t (&w0_s)[K],
+                                                  uint32_t (&w0_l)[M]) {
+    const int chunks = (int)(pitch / 16);
+    int q0 = 0;
+    for (;;) {
+        const int left = chunks - q0;
+        Slice<4, 0> s0{16 * (q0 + lane), 0, lane, q0 + lane < chunks, 0};
+        if (left <= 0) break;
+        if (left <= 64 && left > 16) {  // a last, partly filled 16-B pass
+            unpack_pass<K, M, 4, 0>(pl, wire_g, out_g, pitch, s0, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
+            break;
+        }
+        const int rest = left - 64;  // chunks after a full 16-B pass
+        if (left <= 16) {  // tail only: 4 bytes per lane
+            Slice<0, 1> st{0, 16 * q0, lane, false, (int)pitch};
+            unpack_pass<K, M, 0, 1>(pl, wire_g, out_g, pitch, st, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
+            break;
+        }
+        if (rest > 0 && rest <= 16 && FUSE_TAIL) {
+            Slice<4, 1> sc{16 * (q0 + lane), 16 * (q0 + 64), lane, true, (int)pitch};
+            unpack_pass<K, M, 4, 1>(pl, wire_g, out_g, pitch, sc, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
+            break;
+        }
+        unpack_pass<K, M, 4, 0>(pl, wire_g, out_g, pitch, s0, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
+        q0 += 64;
+    }
+}
+
+template <int K, int M, bool FUSE_TAIL>
 __global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t* __restrict__ wire,
                                                       const int32_t* __restrict__ wire_len,
                                                       const int32_t* __restrict__ lut,
@@ -785,8 +837,10 @@ __global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t*
             pl.tab = records + rec + rec_hdr;
             pl.e = (int)records[rec];
 #pragma unroll
-            for (int j = 0; j < M; ++j)
-                if (j < pl.e) pl.lost_row[j] = (int)records[rec + 4 + K + j];
+            for (int j = 0; j < M; ++j) {  // the record header has room for M lost ids
+                const int lr = (int)records[rec + 4 + K + j];
+                pl.lost_row[j] = j < pl.e ? lr : 0;
+            }
         }
 #pragma unroll
         for (int c = 0; c < K; ++c) {
@@ -816,14 +870,8 @@ __global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t*
         for (int c = 0; c < K; ++c) dsum[c] = ps_s[c] = 0;
 #pragma unroll
         for (int j = 0; j < M; ++j) xsum[j] = ps_l[j] = 0;
-        const int chunks = (int)(pitch / 16);
-        int q0 = 0;
-        for (; chunks - q0 > 16; q0 += 64)
-            unpack_pass<K, M, 4>(pl, wire_g, out_g, pitch, 16 * (q0 + lane), q0 + lane < chunks, q0 == 0,
-                                 a.checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
-        if (q0 < chunks)  // <= 16 chunks left: 4 bytes per lane
-            unpack_pass<K, M, 1>(pl, wire_g, out_g, pitch, 16 * q0 + 4 * lane, 4 * lane < 16 * (chunks - q0),
-                                 q0 == 0, a.checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
+        unpack_row_passes<K, M, FUSE_TAIL>(pl, wire_g, out_g, pitch, lane, a.checksum, dsum, xsum, ps_s, ps_l, w0_s,
+                                           w0_l);
         // ---- verdicts
         uint32_t newbad = 0;
 #pragma unroll
@@ -1086,8 +1134,12 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
 
 #define QFEC_UNPACK_CASE(KK, MM)                                                                        \
     if (a.k == KK && a.m == MM) {                                                                       \
-        hipLaunchKernelGGL((k_unpack_fused<KK, MM>), dim3(waves_grid(a.groups)), dim3(256), 0, s, a, a.wire, \
-                           (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);                \
+        if (tuning().wire_rx_tail)                                                                      \
+            hipLaunchKernelGGL((k_unpack_fused<KK, MM, true>), dim3(waves_grid(a.groups)), dim3(256), 0, s, a, \
+                               a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);    \
+        else                                                                                            \
+            hipLaunchKernelGGL((k_unpack_fused<KK, MM, false>), dim3(waves_grid(a.groups)), dim3(256), 0, s, a, \
+                               a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);    \
         *launched = true;                                                                               \
         return hipGetLastError();                                                                       \
     }

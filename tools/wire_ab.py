@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 import quicknet_amd as qa  # noqa: E402
 
-KNOBS = {"wire_fused": 1, "wire_store_nt": 3}
+KNOBS = {"wire_fused": 1, "wire_store_nt": 3, "wire_fused_rx": 1, "wire_rx_tail": 0}
 
 
 def main():
@@ -28,6 +28,7 @@ def main():
     p.add_argument("--rounds", type=int, default=10)
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--variants", default="base;wire_store_nt=0;wire_store_nt=1;wire_fused=0")
+    p.add_argument("--unpack", action="store_true", help="time qfec_unpack_datagrams (n - k losses per group)")
     a = p.parse_args()
     k, n, G, S = a.k, a.n, a.groups, a.size
     dev = torch.device("cuda:0")
@@ -49,6 +50,26 @@ def main():
         qa.lib().qfec_pack_datagrams(code._h, payload.data_ptr(), offs.data_ptr(), sizes.data_ptr(), seq.data_ptr(), G, 1,
                                      shards.data_ptr(), pitch, wire.data_ptr(), wpitch, wlen.data_ptr(), None)
 
+    if a.unpack:
+        import numpy as np
+        pack()
+        torch.cuda.synchronize()
+        rng = np.random.default_rng(5)
+        lost = np.zeros((G, n), bool)
+        for g in range(G):
+            lost[g, rng.choice(n, n - k, replace=False)] = True
+        rx_len = torch.where(torch.from_numpy(lost).to(dev), torch.zeros_like(wlen), wlen).contiguous()
+        marks = torch.empty(G * n, dtype=torch.uint8, device=dev)
+        rx = torch.empty((G, n), dtype=torch.int32, device=dev)
+        status = torch.empty((G, k), dtype=torch.int32, device=dev)
+        psize = torch.empty((G, k), dtype=torch.int32, device=dev)
+        wire_in = wire.clone()
+
+        def pack():  # noqa: F811 -- the timed call is the receive path
+            qa.lib().qfec_unpack_datagrams(code._h, wire_in.data_ptr(), wpitch, rx_len.data_ptr(), G, 1, 2068,
+                                           shards.data_ptr(), pitch, marks.data_ptr(), rx.data_ptr(),
+                                           status.data_ptr(), psize.data_ptr(), None)
+
     def setup(spec):
         for kk, v in KNOBS.items():
             qa.tune(kk, v)
@@ -61,8 +82,9 @@ def main():
     setup("base")
     pack()
     torch.cuda.synchronize()
-    ref = wire.clone()
-    ref_len = wlen.clone()
+    out_t, len_t = (shards, status) if a.unpack else (wire, wlen)
+    ref = out_t.clone()
+    ref_len = len_t.clone()
     times = {v: [] for v in variants}
     s = torch.cuda.current_stream()
     for _ in range(a.rounds):
@@ -76,12 +98,18 @@ def main():
             e1.record(s)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / a.reps)
-            L = ref_len.max().item()
-            assert torch.equal(wlen, ref_len), v
-            assert torch.equal(wire[..., :L], ref[..., :L]) or v.startswith("wire_fused=0"), v
+            if a.unpack:
+                assert torch.equal(status, ref_len), v
+                assert torch.equal(shards[:, :k], ref[:, :k]), v
+            else:
+                L = ref_len.max().item()
+                assert torch.equal(wlen, ref_len), v
+                assert torch.equal(wire[..., :L], ref[..., :L]) or v.startswith("wire_fused=0"), v
     setup("base")
-    nbytes = G * k * S + int(ref_len.sum().item())
-    print(f"pack RS({k},{n}) payload {S} B, G={G}: {a.rounds} rounds x {a.reps}")
+    nbytes = G * k * S + int(wlen.sum().item())
+    if a.unpack:  # received datagrams in, data rows out
+        nbytes = int(rx_len.sum().item()) + G * k * pitch
+    print(f"{'unpack' if a.unpack else 'pack'} RS({k},{n}) payload {S} B, G={G}: {a.rounds} rounds x {a.reps}")
     for v in variants:
         t = times[v]
         med = statistics.median(t)
