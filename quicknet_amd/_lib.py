@@ -20,6 +20,8 @@ EXPORTS = {
                "qfec_frame_udp", "qfec_unframe_udp", "qfec_synth_fill", "qfec_probe_stream",
                "qfec_tune", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
                "qfec_last_error", "qfec_version"],
+    "qfec_net.h": ["qfec_net_new", "qfec_net_free", "qfec_net_session", "qfec_net_pack_input", "qfec_net_flush_pack",
+                   "qfec_net_unpack_input", "qfec_net_flush_unpack", "qfec_net_stats"],
 }
 
 QFEC_CAUCHY = 0
@@ -61,6 +63,14 @@ def lib():
         "qfec_pack_datagrams": (i, [vp, vp, vp, vp, vp, ll, i, vp, ll, vp, ll, vp, vp]),
         "qfec_unpack_datagrams": (i, [vp, vp, ll, vp, ll, i, i, vp, ll, vp, vp, vp, vp, vp]),
         "qfec_frame_udp": (i, [vp, ll, vp, ll, vp, vp, i, i, i, vp, ll, vp, vp]),
+        "qfec_net_new": (vp, [i, i, i, i]),
+        "qfec_net_free": (None, [vp]),
+        "qfec_net_session": (i, [vp, vp]),
+        "qfec_net_pack_input": (i, [vp, i, vp, C.c_uint]),
+        "qfec_net_flush_pack": (i, [vp, vp, vp]),
+        "qfec_net_unpack_input": (i, [vp, i, vp, C.c_uint]),
+        "qfec_net_flush_unpack": (i, [vp, vp, i, vp]),
+        "qfec_net_stats": (i, [vp, vp]),
         "qfec_unframe_udp": (i, [vp, ll, vp, ll, i, i, vp, ll, vp, vp, vp, vp, vp]),
         "qfec_synth_fill": (i, [vp, ll, u64, vp]),
         "qfec_probe_stream": (i, [vp, vp, ll, i, i, i, ll, vp]),

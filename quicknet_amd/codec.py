@@ -17,7 +17,8 @@ import numpy as np
 from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
 
 __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
-           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count", "frame_udp", "unframe_udp"]
+           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count", "frame_udp", "unframe_udp",
+           "NetFec"]
 
 
 def _stream_handle(stream):
@@ -320,3 +321,81 @@ class ReedSolomon:
         marks = np.ascontiguousarray(marks, dtype=np.uint8)
         return lib().reed_solomon_reconstruct(self._h, self._ptrs(data, parity), C.c_void_p(marks.ctypes.data),
                                               G * (self.k + self.m), block_size)
+
+
+_PACK_OUT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_char), C.c_uint)
+_UNPACK_OUT = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_char), C.c_uint, C.c_uint)
+
+
+class NetFec:
+    """Batched NetFecCodec layer (include/qfec_net.h): sessions keep zfec_pack_input's
+    numbering; complete groups of all sessions go out in one device launch per flush, and
+    received groups come back the same way.  Callbacks get (session, bytes[, src index])."""
+
+    def __init__(self, k, n, max_pkt_size=2048, checksum=True):
+        self._h = lib().qfec_net_new(k, n, max_pkt_size, int(bool(checksum)))
+        if not self._h:
+            raise QfecError(f"qfec_net_new({k}, {n}, {max_pkt_size}) failed")
+        self.k, self.n = k, n
+
+    def close(self):
+        if self._h:
+            lib().qfec_net_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def session(self):
+        """A new session; its id is also its callback peer (id + 1)."""
+        self._nsess = getattr(self, "_nsess", 0)
+        s = lib().qfec_net_session(self._h, C.c_void_p(self._nsess + 1))
+        check(min(s, 0), "qfec_net_session")
+        self._nsess += 1
+        return s
+
+    def pack_input(self, session, data):
+        b = bytes(data)
+        check(lib().qfec_net_pack_input(self._h, session, b, len(b)), "qfec_net_pack_input")
+
+    def flush_pack(self, stream=None):
+        """-> [(session, datagram bytes)] in emission order (each session's in sent order)."""
+        out = []
+
+        def cb(peer, p, size):
+            out.append((int(peer) - 1, C.string_at(p, size)))
+            return 0
+
+        f = _PACK_OUT(cb)
+        rc = lib().qfec_net_flush_pack(self._h, f, _stream_handle(stream))
+        check(min(rc, 0), "qfec_net_flush_pack")
+        return out
+
+    def unpack_input(self, session, datagram):
+        b = bytes(datagram)
+        rc = lib().qfec_net_unpack_input(self._h, session, b, len(b))
+        check(min(rc, 0), "qfec_net_unpack_input")
+        return rc
+
+    def flush_unpack(self, all_groups=False, stream=None):
+        """-> [(session, payload bytes, src index)] delivered, group by group in source order."""
+        out = []
+
+        def cb(peer, p, size, src):
+            out.append((int(peer) - 1, C.string_at(p, size), src))
+            return 0
+
+        f = _UNPACK_OUT(cb)
+        rc = lib().qfec_net_flush_unpack(self._h, f, int(bool(all_groups)), _stream_handle(stream))
+        check(min(rc, 0), "qfec_net_flush_unpack")
+        return out
+
+    def stats(self):
+        a = (C.c_longlong * 8)()
+        check(lib().qfec_net_stats(self._h, a), "qfec_net_stats")
+        keys = ["groups_packed", "datagrams_out", "groups_unpacked", "delivered", "recovered", "undecodable",
+                "foreign", "late"]
+        return dict(zip(keys, list(a)))

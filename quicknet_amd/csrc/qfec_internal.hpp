@@ -121,7 +121,7 @@ struct Tuning {
     int encode_impl = 0;
     int wire_fused = 1;     // fused datagram send where a (k, m) instance exists (0: staged)
     int wire_fused_rx = 1;  // fused datagram receive likewise
-    int wire_rx_tail = 0;   // fused receive: 1 = tail dwords ride on the last 16-B pass
+    int wire_rx_tail = 1;   // fused receive: 1 = tail dwords ride on the last 16-B pass (0: own pass)
     int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
 };
 Tuning& tuning();

@@ -119,3 +119,29 @@ def test_no_gpu_fails_loudly():
     data = np.zeros((1, 4, 16), np.uint8)
     par = np.zeros((1, 2, 16), np.uint8)
     assert rs.encode(data, par, 16) != 0
+
+
+def test_net_layer_host_side():
+    """qfec_net (include/qfec_net.h): argument checks and session numbering run on the host;
+    a flush without a device fails loudly (QFEC_ENODEV), it does not fall back."""
+    import ctypes as C
+    L = qa.lib()
+    assert not L.qfec_net_new(4, 16, 1400, 1)      # n > 15: the header's 4-bit field
+    assert not L.qfec_net_new(4, 4, 1400, 1)       # no check packets
+    h = L.qfec_net_new(4, 6, 1400, 1)
+    assert h
+    s0, s1 = L.qfec_net_session(h, None), L.qfec_net_session(h, None)
+    assert (s0, s1) == (0, 1)
+    assert L.qfec_net_pack_input(h, 0, b"x" * 1401, 1401) < 0     # > max_pkt_size
+    assert L.qfec_net_pack_input(h, 7, b"x", 1) < 0               # no such session
+    for i in range(4):
+        assert L.qfec_net_pack_input(h, s1, bytes([i]) * 10, 10) == 0
+    # foreign datagrams are dropped on the host: too short, not FEC, another (k, n)
+    assert L.qfec_net_unpack_input(h, 0, b"\xed" * 5, 5) == 0
+    other = bytes([0xED]) + bytes(8) + bytes([5 | 3 << 4, 0]) + bytes(20)
+    assert L.qfec_net_unpack_input(h, 0, other, len(other)) == 0
+    st = (C.c_longlong * 8)()
+    assert L.qfec_net_stats(h, st) == 0 and st[6] == 2
+    if L.qfec_device_count() <= 0:
+        assert L.qfec_net_flush_pack(h, None, None) == -2   # QFEC_ENODEV
+    L.qfec_net_free(h)
