@@ -123,6 +123,7 @@ struct Tuning {
     int wire_fused_rx = 1;  // fused datagram receive likewise
     int wire_rx_tail = 1;   // fused receive: 1 = tail dwords ride on the last 16-B pass (0: own pass)
     int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
+    int wire_chunk = 0;     // fused send: groups per body + head launch pair (0: as many as fit)
 };
 Tuning& tuning();
 

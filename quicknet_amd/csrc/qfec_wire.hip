@@ -1093,7 +1093,11 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
     const uint32_t tn = (uint32_t)((HDR + a.pitch + 15) / 16);
     const uint32_t lpg = std::max(16u, tn - TS);
     const DivMagic lpg_div = make_div_magic(lpg);
-    const uint64_t per = (((uint64_t)1 << 30) / lpg) & ~(uint64_t)15;  // keeps g0 * lpg % 16 == 0
+    // groups per body + head launch pair (keeps g0 * lpg % 16 == 0); tuning "wire_chunk"
+    // bounds it so that a head launch rewrites lines its body launch wrote only just before
+    uint64_t per = (((uint64_t)1 << 30) / lpg) & ~(uint64_t)15;
+    if (tuning().wire_chunk > 0) per = std::min(per, (uint64_t)tuning().wire_chunk & ~(uint64_t)15);
+    per = std::max(per, (uint64_t)16);
     for (uint64_t g0 = 0; g0 < a.groups; g0 += per) {
         const uint64_t gn = std::min(per, a.groups - g0);
         const uint32_t lanes = (uint32_t)(gn * lpg);  // the grid covers whole 16-lane rows past it
