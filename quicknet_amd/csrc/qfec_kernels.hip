@@ -331,6 +331,10 @@ __device__ __forceinline__ void recon_column_allrows(const uint8_t* const (&src)
 #pragma unroll
         for (int j = 0; j < M; ++j) gf_mac16(acc[j], sl, tab + (j * K + K - 1) * QFEC_TAB_STRIDE);
     }
+    // materialise every row here: left alone, the compiler sinks each row's MAC into its
+    // `j < e` store branch, which keeps all K inputs' selector words live across the rows
+#pragma unroll
+    for (int j = 0; j < M; ++j) pin16(acc[j]);
 #pragma unroll
     for (int j = 0; j < M; ++j)
         if (j < e) st16(dst[j], acc[j]);
@@ -546,9 +550,9 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 
 #define QFEC_REC_CASE(KK, MM)                                                  \
     if (a.k == KK && a.m == MM) {                                              \
-        /* auto: all rows at once while the register budget allows (measured: */ \
-        /* (10,3) 5.69 vs 5.31 TB/s; (16,4) 1.31 vs 3.01 TB/s, tools/ab.py)   */ \
-        const bool ar = a.impl < 0 ? (KK * MM <= 30) : a.impl == 1;           \
+        /* auto: all rows at once up to k*m = 64 (measured, tools/ab.py: (10,3) */ \
+        /* 5.73 vs 5.44 TB/s, (16,4) B=1400 3.57 vs 3.12 TB/s)                   */ \
+        const bool ar = a.impl < 0 ? (KK * MM <= 64) : a.impl == 1;           \
         if (ar) QFEC_REC_LAUNCH(KK, MM, true);                                 \
         else QFEC_REC_LAUNCH(KK, MM, false);                                   \
         return hipGetLastError();                                              \

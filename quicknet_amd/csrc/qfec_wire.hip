@@ -453,6 +453,8 @@ __global__ void __launch_bounds__(256) k_pack_body(WireArgs a, const uint8_t* __
     }
     uint4 acc[M];
     encode_cols<K, M>(x, acc, tab);
+#pragma unroll
+    for (int r = 0; r < M; ++r) pin16(acc[r]);  // no sinking of a row's MAC into its store branch
     uint32_t sent0 = 0, src0 = 0;
     if (HDR == 11 && act && first) {
         sent0 = seq[2 * g];
@@ -683,6 +685,11 @@ __device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const ui
             }
         }
     }
+    // materialise the rows before the per-row branches below (keeps the selectors short-lived)
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int d = 0; d < NV; ++d) asm volatile("" : "+v"(acc[j][d]));
     // the first shard dword of every output row (lane 0, dword 0 of the first pass):
     // size (bytes 0-1) and payload checksum (2-3)
     if (first_pass) {
