@@ -340,13 +340,66 @@ __device__ __forceinline__ void recon_column_allrows(const uint8_t* const (&src)
         if (j < e) st16(dst[j], acc[j]);
 }
 
+// Exactly E rows (E = the group's erased-data count, wave-uniform): the ALLROWS schedule
+// without the M - E rows a group does not need.  3 random erasures of 13 give e = 1, 2, 3
+// with probability 0.10, 0.47, 0.42, so RS(10,3) does 77 % of the all-rows VALU work.
+template <int K, int E>
+__device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
+                                               uint64_t lost_bits, const uint32_t* __restrict__ tab,
+                                               uint64_t pitch, uint64_t off) {
+    uint4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = ld16(src[c] + off);
+    uint8_t* dst[E];
+    uint4 acc[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(lost_bits);
+        lost_bits &= lost_bits - 1;
+        dst[j] = data_g + (uint64_t)l * pitch + off;
+        acc[j] = make_uint4(0, 0, 0, 0);
+        if (tab[(j * K) * QFEC_TAB_STRIDE + 5]) acc[j] = *reinterpret_cast<const uint4*>(dst[j]);
+    }
+#pragma unroll
+    for (int c = 0; c + 1 < K; c += 2) {
+        Sel sa[4], sb[4];
+        sel16(sa, x[c]);
+        sel16(sb, x[c + 1]);
+#pragma unroll
+        for (int j = 0; j < E; ++j)
+            gf_mac16x2(acc[j], sa, sb, tab + (j * K + c) * QFEC_TAB_STRIDE, tab + (j * K + c + 1) * QFEC_TAB_STRIDE);
+    }
+    if (K & 1) {
+        Sel sl[4];
+        sel16(sl, x[K - 1]);
+#pragma unroll
+        for (int j = 0; j < E; ++j) gf_mac16(acc[j], sl, tab + (j * K + K - 1) * QFEC_TAB_STRIDE);
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) st16(dst[j], acc[j]);
+}
+
+// wave-uniform dispatch on e to the exact-row-count body
+template <int K, int M, int E = M>
+__device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
+                                                  uint64_t lost_bits, const uint32_t* __restrict__ tab, int e,
+                                                  uint64_t pitch, uint64_t off) {
+    if constexpr (E > 1) {
+        if (e < E) {
+            recon_column_by_e<K, M, E - 1>(src, data_g, lost_bits, tab, e, pitch, off);
+            return;
+        }
+    }
+    recon_column_e<K, E>(src, data_g, lost_bits, tab, pitch, off);
+}
+
 // LUT mode, compile-time K, M.  The survivor set follows from the erasure mask alone --
 // it is the lowest K non-erased shard ids (all surviving data, then the first e surviving
 // parity rows: module/rs.c:620-629) -- so the shard loads issue right after the ballot,
 // while the decode record (coefficients only) is still in flight.
 // One wave per 64 16-B columns of a group: a group of `cols` columns gets
 // wpg = ceil(cols / 64) waves (B = 1400 -> 2), all in flight together, no column loop.
-template <int K, int M, bool ALLROWS>
+template <int K, int M, int IMPL>
 __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ parity,
                                                           const uint8_t* __restrict__ marks,
@@ -387,7 +440,8 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     }
     const uint32_t col = part * 64u + lane;
     if (col < a.cols) {
-        if (ALLROWS) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+        if (IMPL == 2) recon_column_by_e<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+        else if (IMPL == 1) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
         else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
     }
 }
@@ -550,11 +604,12 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 
 #define QFEC_REC_CASE(KK, MM)                                                  \
     if (a.k == KK && a.m == MM) {                                              \
-        /* auto: all rows at once up to k*m = 64 (measured, tools/ab.py: (10,3) */ \
-        /* 5.73 vs 5.44 TB/s, (16,4) B=1400 3.57 vs 3.12 TB/s)                   */ \
-        const bool ar = a.impl < 0 ? (KK * MM <= 64) : a.impl == 1;           \
-        if (ar) QFEC_REC_LAUNCH(KK, MM, true);                                 \
-        else QFEC_REC_LAUNCH(KK, MM, false);                                   \
+        /* auto: exact-e rows (impl 2) up to k*m = 64, else the row loop (0);   */ \
+        /* tools/ab.py times all three                                          */ \
+        const int im = a.impl < 0 ? (KK * MM <= 64 ? 2 : 0) : a.impl;         \
+        if (im == 2) QFEC_REC_LAUNCH(KK, MM, 2);                               \
+        else if (im == 1) QFEC_REC_LAUNCH(KK, MM, 1);                          \
+        else QFEC_REC_LAUNCH(KK, MM, 0);                                       \
         return hipGetLastError();                                              \
     }
 

@@ -66,6 +66,7 @@ def main():
         ("probe xor (traffic only)", lambda: None, probe, enc_bytes),
         ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
         ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
+        ("recon impl2 (exact e rows)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),
     ]
     if a.pairs:
         variants = []
@@ -86,20 +87,34 @@ def main():
     if a.pairs:
         qa.tune("recon_impl", -1)
         scratch = torch.empty_like(par)
-        befores = [("after encode", enc), ("after XOR probe (same traffic, light VALU)", lambda: qa.probe_stream(data, scratch, B)),
+
+        def enc_other():  # same encode, parity into a buffer reconstruct does not read
+            code.encode(data, scratch, B)
+
+        def enc_sleep():
+            code.encode(data, par, B)
+            torch.cuda._sleep(100000)
+
+        befores = [("after encode", enc), ("after encode into another buffer", enc_other),
+                   ("after encode + ~50us sleep", enc_sleep),
+                   ("after XOR probe (same traffic, light VALU)", lambda: qa.probe_stream(data, scratch, B)),
                    ("after 200us sleep", lambda: torch.cuda._sleep(400000)), ("after reconstruct", rec)]
-        for label, before in befores:
-            tr = []
-            for r in range(a.rounds * a.reps):
-                e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
-                before()
-                e1.record(s)
-                rec()
-                e2.record(s)
-                torch.cuda.synchronize()
-                tr.append(e1.elapsed_time(e2))
-            med = statistics.median(tr)
-            print(f"  reconstruct {label:44s} median {med*1e3:7.1f} us -> {dec_bytes/(med*1e-3)/1e9:7.1f} GB/s")
+        for impl in (1, 2):
+            qa.tune("recon_impl", impl)
+            for label, before in befores:
+                tr = []
+                for r in range(a.rounds * a.reps):
+                    e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
+                    before()
+                    e1.record(s)
+                    rec()
+                    e2.record(s)
+                    torch.cuda.synchronize()
+                    tr.append(e1.elapsed_time(e2))
+                med = statistics.median(tr)
+                print(f"  reconstruct impl{impl} {label:44s} median {med*1e3:7.1f} us -> "
+                      f"{dec_bytes/(med*1e-3)/1e9:7.1f} GB/s")
+        qa.tune("recon_impl", -1)
     qa.set_kernel_variant(0)
     qa.tune("encode_impl", 0)
     qa.tune("recon_impl", 0)

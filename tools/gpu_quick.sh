@@ -6,7 +6,7 @@ TAG=${1:-quick}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
 tail -3 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || { grep -E "Error|assert|FAIL" $OUT/pytest_gpu.log | head -30; exit $rc; }
 timeout -k 10 300 python bench.py --no-cpu > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 4; }
