@@ -82,6 +82,7 @@ __device__ __forceinline__ void sel16(Sel (&s)[4], const uint4& v) {
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // streamed once: non-temporal (the shards are not re-read by this launch)
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) {

@@ -62,8 +62,10 @@ struct ReconArgs {
     int k, m;
     int surv_off, lost_off, hdr;
     int vec16;
-    int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once
+    int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once,
+                              // 2 exact-e rows (16-B lanes), 3 exact-e rows (8-B lanes)
     uint32_t wpg;             // waves per group = ceil(cols / 64) (vec16 LUT kernels)
+    uint32_t cols8, wpg8;     // the same at 8-B columns: ceil(B / 8), ceil(cols8 / 64)
 };
 
 // FEC datagram batches (qfec_wire.hip): shards[G][n][pitch], wire[G][n][wire_pitch]

@@ -343,54 +343,97 @@ __device__ __forceinline__ void recon_column_allrows(const uint8_t* const (&src)
 // Exactly E rows (E = the group's erased-data count, wave-uniform): the ALLROWS schedule
 // without the M - E rows a group does not need.  3 random erasures of 13 give e = 1, 2, 3
 // with probability 0.10, 0.47, 0.42, so RS(10,3) does 77 % of the all-rows VALU work.
-template <int K, int E>
+// D = dwords per lane (4: 16-B columns, 2: 8-B columns for rows whose 16-B column count
+// leaves a wave mostly idle, e.g. B = 1400: 88 16-B columns on 2 waves, 175 8-B on 3).
+template <int D>
+__device__ __forceinline__ void ldv(uint32_t (&v)[D], const uint8_t* p) {
+    if constexpr (D == 4) {
+        const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+        static_assert(D == 2, "4 or 2 dwords per lane");
+        const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+        v[0] = t.x; v[1] = t.y;
+    }
+}
+template <int D>
+__device__ __forceinline__ void stv(uint8_t* p, const uint32_t (&v)[D]) {
+    if constexpr (D == 4) {
+        const u32x4 t = {v[0], v[1], v[2], v[3]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(p));
+    } else {
+        const u32x2 t = {v[0], v[1]};
+        __builtin_nontemporal_store(t, reinterpret_cast<u32x2*>(p));
+    }
+}
+template <int D>
+__device__ __forceinline__ void ldv_plain(uint32_t (&v)[D], const uint8_t* p) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) v[d] = reinterpret_cast<const uint32_t*>(p)[d];
+}
+
+template <int K, int E, int D>
 __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
                                                uint64_t lost_bits, const uint32_t* __restrict__ tab,
                                                uint64_t pitch, uint64_t off) {
-    uint4 x[K];
+    uint32_t x[K][D];
 #pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = ld16(src[c] + off);
+    for (int c = 0; c < K; ++c) ldv<D>(x[c], src[c] + off);
     uint8_t* dst[E];
-    uint4 acc[E];
+    uint32_t acc[E][D];
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         const uint32_t l = (uint32_t)__builtin_ctzll(lost_bits);
         lost_bits &= lost_bits - 1;
         dst[j] = data_g + (uint64_t)l * pitch + off;
-        acc[j] = make_uint4(0, 0, 0, 0);
-        if (tab[(j * K) * QFEC_TAB_STRIDE + 5]) acc[j] = *reinterpret_cast<const uint4*>(dst[j]);
+#pragma unroll
+        for (int d = 0; d < D; ++d) acc[j][d] = 0;
+        if (tab[(j * K) * QFEC_TAB_STRIDE + 5]) ldv_plain<D>(acc[j], dst[j]);  // rs.c column-0 quirk
     }
 #pragma unroll
     for (int c = 0; c + 1 < K; c += 2) {
-        Sel sa[4], sb[4];
-        sel16(sa, x[c]);
-        sel16(sb, x[c + 1]);
+        Sel sa[D], sb[D];
 #pragma unroll
-        for (int j = 0; j < E; ++j)
-            gf_mac16x2(acc[j], sa, sb, tab + (j * K + c) * QFEC_TAB_STRIDE, tab + (j * K + c + 1) * QFEC_TAB_STRIDE);
+        for (int d = 0; d < D; ++d) { sa[d] = gf_sel(x[c][d]); sb[d] = gf_sel(x[c + 1][d]); }
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const uint32_t* ta = tab + (j * K + c) * QFEC_TAB_STRIDE;
+            const uint32_t* tb = ta + QFEC_TAB_STRIDE;
+            uint32_t a5[5], b5[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) { a5[i] = ta[i]; b5[i] = tb[i]; }
+#pragma unroll
+            for (int d = 0; d < D; ++d) acc[j][d] = mac2(acc[j][d], sa[d], sb[d], a5, b5);
+        }
     }
     if (K & 1) {
-        Sel sl[4];
-        sel16(sl, x[K - 1]);
+        Sel sl[D];
 #pragma unroll
-        for (int j = 0; j < E; ++j) gf_mac16(acc[j], sl, tab + (j * K + K - 1) * QFEC_TAB_STRIDE);
+        for (int d = 0; d < D; ++d) sl[d] = gf_sel(x[K - 1][d]);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            const uint32_t* t = tab + (j * K + K - 1) * QFEC_TAB_STRIDE;
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+                acc[j][d] = xor3(acc[j][d], pp0(sl[d], t[0], t[1]), pp1(sl[d], t[2], t[3])) ^ pp2(sl[d], t[4]);
+        }
     }
 #pragma unroll
-    for (int j = 0; j < E; ++j) st16(dst[j], acc[j]);
+    for (int j = 0; j < E; ++j) stv<D>(dst[j], acc[j]);
 }
 
 // wave-uniform dispatch on e to the exact-row-count body
-template <int K, int M, int E = M>
+template <int K, int M, int D, int E = M>
 __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
                                                   uint64_t lost_bits, const uint32_t* __restrict__ tab, int e,
                                                   uint64_t pitch, uint64_t off) {
     if constexpr (E > 1) {
         if (e < E) {
-            recon_column_by_e<K, M, E - 1>(src, data_g, lost_bits, tab, e, pitch, off);
+            recon_column_by_e<K, M, D, E - 1>(src, data_g, lost_bits, tab, e, pitch, off);
             return;
         }
     }
-    recon_column_e<K, E>(src, data_g, lost_bits, tab, pitch, off);
+    recon_column_e<K, E, D>(src, data_g, lost_bits, tab, pitch, off);
 }
 
 // LUT mode, compile-time K, M.  The survivor set follows from the erasure mask alone --
@@ -410,7 +453,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const uint32_t wpg = a.wpg;
+    const uint32_t wpg = IMPL == 3 ? a.wpg8 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
     if (g >= a.groups) return;
@@ -439,8 +482,9 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
         src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : par_g + (uint64_t)(s - K) * pitch;
     }
     const uint32_t col = part * 64u + lane;
-    if (col < a.cols) {
-        if (IMPL == 2) recon_column_by_e<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+    if (col < (IMPL == 3 ? a.cols8 : a.cols)) {
+        if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+        else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 8u);
         else if (IMPL == 1) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
         else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
     }
@@ -602,15 +646,17 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
     hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR>), dim3(pgrid), dim3(256), 0, stream, a, a.data, a.parity, \
                        a.marks, a.lut, a.records)
 
-#define QFEC_REC_CASE(KK, MM)                                                  \
-    if (a.k == KK && a.m == MM) {                                              \
-        /* auto: exact-e rows (impl 2) up to k*m = 64, else the row loop (0);   */ \
-        /* tools/ab.py times all three                                          */ \
-        const int im = a.impl < 0 ? (KK * MM <= 64 ? 2 : 0) : a.impl;         \
-        if (im == 2) QFEC_REC_LAUNCH(KK, MM, 2);                               \
-        else if (im == 1) QFEC_REC_LAUNCH(KK, MM, 1);                          \
-        else QFEC_REC_LAUNCH(KK, MM, 0);                                       \
-        return hipGetLastError();                                              \
+#define QFEC_REC_CASE(KK, MM)                                                      \
+    if (a.k == KK && a.m == MM) {                                                  \
+        /* auto: exact-e rows up to k*m = 64 (8-B lanes when that fills the      */ \
+        /* waves better, e.g. B = 1400), else the row loop; tools/ab.py times all */ \
+        const int im = a.impl < 0 ? (KK * MM <= 64 ? (lanes8 ? 3 : 2) : 0) : a.impl; \
+        const unsigned pgrid = im == 3 ? pgrid8 : pgrid16;                         \
+        if (im == 3) QFEC_REC_LAUNCH(KK, MM, 3);                                   \
+        else if (im == 2) QFEC_REC_LAUNCH(KK, MM, 2);                              \
+        else if (im == 1) QFEC_REC_LAUNCH(KK, MM, 1);                              \
+        else QFEC_REC_LAUNCH(KK, MM, 0);                                           \
+        return hipGetLastError();                                                  \
     }
 
 hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
@@ -624,9 +670,12 @@ hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
         hipLaunchKernelGGL((k_reconstruct_any<true>), dim3(grid), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
-    const uint64_t waves = a.groups * (uint64_t)a.wpg;
+    const uint64_t waves = a.groups * (uint64_t)std::max(a.wpg, a.wpg8);
     if (waves > 0xFFFFFFFFull) return hipErrorInvalidValue;  // caller chunks batches
-    const unsigned pgrid = grid_for(waves, 4);
+    const unsigned pgrid16 = grid_for(a.groups * (uint64_t)a.wpg, 4);
+    const unsigned pgrid8 = grid_for(a.groups * (uint64_t)a.wpg8, 4);
+    // 8-B lanes when they fill the group's waves clearly better than 16-B lanes
+    const bool lanes8 = (double)a.cols8 / (64.0 * a.wpg8) > (double)a.cols / (64.0 * a.wpg) + 0.1;
     QFEC_REC_CASE(10, 3)
     QFEC_REC_CASE(16, 4)
     QFEC_REC_CASE(4, 2)

@@ -211,6 +211,40 @@ def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
     assert rc_ref in (0, -1)
 
 
+@pytest.mark.parametrize("impl", [0, 1, 2, 3])
+@pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (4, 2, 100), (12, 4, 40), (3, 2, 1400)])
+def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
+    """Every LUT reconstruct body (row loop, all rows, exact-e rows on 16-B and on 8-B
+    lanes) against the oracle's rs.c restatement, on random erasure patterns (0..m+1
+    erasures, so unrecoverable groups too) with random, inconsistent parity: the survivor
+    rule and the stale-row quirk have to match byte for byte."""
+    G = 700
+    code = qa.Code.cauchy(k, m)
+    rng = np.random.default_rng(k * 100 + B)
+    data = synth_bytes(k * 7 + B, G * k * B).reshape(G, k, B)
+    par = synth_bytes(k * 11 + B, G * m * B).reshape(G, m, B)
+    gm = np.zeros((G, k + m), np.uint8)
+    for g in range(G):
+        gm[g, rng.choice(k + m, size=int(rng.integers(0, m + 2)), replace=False)] = 1
+    marks = marks_to_rs_layout(gm, k)
+    expect = data.copy()
+    expect.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+    damaged = expect.copy()
+    oracle.rs_reconstruct(code.rows, expect, par.copy(), marks, B)
+    pitch = round16(B)
+    dd = to_dev(padded(damaged, pitch))
+    failed = torch.zeros(1, dtype=torch.int32, device=DEV)
+    qa.tune("recon_impl", impl)
+    try:
+        code.reconstruct(dd, to_dev(padded(par, pitch)), to_dev(marks), B, failed)
+        torch.cuda.synchronize()
+    finally:
+        qa.tune("recon_impl", -1)
+    assert np.array_equal(dd.cpu().numpy()[..., :B], expect)
+    unrecoverable = int(((gm[:, :k].sum(1) > 0) & (gm.sum(1) > m)).sum())
+    assert int(failed.item()) == unrecoverable
+
+
 def test_large_batch_roundtrip(oracle):
     """BASELINE config 2/3 shape at full size: 100 000 groups x RS(10,3) x 1 KiB.
     Encode checked byte for byte against the oracle; reconstruct with 3 random erasures

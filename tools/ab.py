@@ -67,6 +67,7 @@ def main():
         ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
         ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
         ("recon impl2 (exact e rows)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),
+        ("recon impl3 (exact e, 8-B lanes)", lambda: qa.tune("recon_impl", 3), rec, dec_bytes),
     ]
     if a.pairs:
         variants = []
@@ -99,7 +100,7 @@ def main():
                    ("after encode + ~50us sleep", enc_sleep),
                    ("after XOR probe (same traffic, light VALU)", lambda: qa.probe_stream(data, scratch, B)),
                    ("after 200us sleep", lambda: torch.cuda._sleep(400000)), ("after reconstruct", rec)]
-        for impl in (1, 2):
+        for impl in (2, 3):
             qa.tune("recon_impl", impl)
             for label, before in befores:
                 tr = []
