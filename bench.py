@@ -38,8 +38,10 @@ GIB = float(1 << 30)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--spinup-ms", type=float, default=25.0,
+                   help="setup: run the step for this long before the W warmup steps (clock ramp, tools/sustain.py)")
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--m", type=int, default=3)
     p.add_argument("--block", type=int, default=1024)
@@ -181,11 +183,23 @@ def main():
         if ev is not None:
             ev[2].record(stream)
 
+    # setup, untimed: a fresh GPU runs the first ~20 steps (~10 ms) 5-8 % slower while its
+    # clocks leave the idle state (profiles/r01t_sustain.txt); spin it up before the W
+    # warmup steps so the timed region sees the steady state whatever W the caller picks
+    t_spin = time.perf_counter()
+    while (time.perf_counter() - t_spin) * 1e3 < args.spinup_ms:
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     # timed region: K steps between barrier + synchronize on both sides
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    for e in evs:  # torch creates the HIP event at its first record: do that outside the timed region
+        for x in e:
+            x.record(stream)
+    torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
