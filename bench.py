@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--variant", type=int, default=0, help="0 perm tables (default), 1 LDS log/exp")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-side", action="store_true", help="skip the side configurations (rank 0, after the timed run)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py), if present")
     return p.parse_args()
@@ -139,6 +140,64 @@ def cpu_baseline(args, budget_s):
     return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": f"{reps} x (encode {sample} groups + reconstruct {dec_groups} groups with {args.erasures} "
                       f"random erasures/group), RS({k},{m}) B={B}, {el:.1f} s, 1 thread"}
+
+# BASELINE configs measured beside the headline line (rank 0's GPU, after the timed region):
+# the Vandermonde flavour the network stack links (module/fec.c) at configs[1]+[2], config 4's
+# RS(16,4) on 1400-B MTU packets, and config 5's RS(4,2)
+SIDE = (("vandermonde", 10, 3, 1024, 100_000, 3), ("cauchy", 16, 4, 1400, 250_000, 4),
+        ("cauchy", 4, 2, 1024, 100_000, 2))
+
+
+def side_config(flavour, k, m, B, G, E, world, rank, steps=20, warmup=5):
+    """One encode + reconstruct step on G groups (G = the config's total / world ranks for
+    config 4, which BASELINE shards over the GPUs), device-resident, pitch = B rounded up to
+    16 B (bytes counted at B); per-kernel HIP events; reconstruct must restore the data."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n, pitch = k + m, (B + 15) // 16 * 16
+    code = qa.Code.cauchy(k, m) if flavour == "cauchy" else qa.Code.vandermonde(k, m)
+    data = torch.empty((G, k, pitch), dtype=torch.uint8, device=dev)
+    qa.synth_fill(data, rank_seed(SEED_ENCODE ^ (k << 8 | m), rank))
+    parity = torch.empty((G, m, pitch), dtype=torch.uint8, device=dev)
+    gm = erasure_marks(rank_seed(SEED_DECODE ^ (k << 8 | m), rank), G, n, E)
+    marks = torch.from_numpy(marks_to_rs_layout(gm, k)).to(dev)
+    dec_groups = int((gm[:, :k].sum(1) > 0).sum())
+    erased = int(gm[:, :k].sum())
+    work = data.clone()
+    work[torch.from_numpy(gm[:, :k].astype(bool)).to(dev)] = 0x5A
+    code.encode(data, parity, B)
+    code.prepare_reconstruct()
+    s = torch.cuda.current_stream()
+    for _ in range(warmup):
+        code.encode(data, parity, B)
+        code.reconstruct(work, parity, marks, B)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in evs:
+        for x in e:
+            x.record(s)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in evs:
+        e[0].record(s)
+        code.encode(data, parity, B)
+        e[1].record(s)
+        code.reconstruct(work, parity, marks, B)
+        e[2].record(s)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    ok = bool(torch.equal(work[..., :B], data[..., :B]))
+    enc_alg, dec_alg = (k + m) * B * G, (k * dec_groups + erased) * B
+    out = {"config": f"RS({k},{m}) {flavour}, {G:,} groups x {B} B, {E} random erasures/group",
+           "value": round((G + dec_groups) * k * B * steps / el / GIB, 2), "unit": "GiB/s",
+           "encode_gibs": round(G * k * B / (enc_ms * 1e-3) / GIB, 2),
+           "decode_gibs": round(dec_groups * k * B / (dec_ms * 1e-3) / GIB, 2),
+           "encode_frac": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "reconstruct_frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "encode_avg_ms": round(enc_ms, 4), "reconstruct_avg_ms": round(dec_ms, 4), "verified": ok}
+    del data, parity, work, marks
+    torch.cuda.empty_cache()
+    return out
 
 
 def load_traffic(path, workload_key):
@@ -253,6 +312,15 @@ def main():
         probe_ms = pe0.elapsed_time(pe1) / 10
         del scratch
 
+    side = None
+    if rank == 0 and not args.no_side:
+        side = []
+        for fl, sk, sm, sB, sG, sE in SIDE:
+            if sB == 1400:  # config 4 shards its 250 000 groups over the GPUs
+                sG = (sG + world - 1) // world
+            side.append(side_config(fl, sk, sm, sB, sG, sE, world, rank))
+        ok = ok and all(x["verified"] for x in side)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
@@ -289,6 +357,7 @@ def main():
             "probe_stream_gbs": round(enc_alg / (probe_ms * 1e-3) / 1e9, 1) if probe_ms else None,
             "verified": ok,
             "cpu_baseline": cpu,
+            "side_configs": side,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

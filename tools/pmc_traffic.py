@@ -58,7 +58,7 @@ def main():
     p.add_argument("--groups", type=int, default=100_000)
     a = p.parse_args()
     bench_args = ["--steps", "5", "--warmup", "1", "--k", str(a.k), "--m", str(a.m), "--block", str(a.block),
-                  "--groups", str(a.groups)]
+                  "--groups", str(a.groups), "--no-side"]
     fetch = run_pass("FETCH_SIZE", a.out, bench_args)
     write = run_pass("WRITE_SIZE", a.out, bench_args)
     k, m, B, G = a.k, a.m, a.block, a.groups
