@@ -455,6 +455,41 @@ int host_records(qfec_code* c, const uint8_t* marks, long long groups, std::vect
     return QFEC_OK;
 }
 
+// qfec_reconstruct for k + m above the LUT's reach (2^n entries): the group's n marks are
+// read back (n bytes per group, after the caller's stream has produced them), the decode
+// records are built per distinct pattern on the host (cached per code), and the explicit-
+// record kernel runs on the caller's stream.  Synchronous: returns after the kernel.
+int reconstruct_host_records(DevCtx& ctx, qfec_code* c, uint8_t* d_data, const uint8_t* d_par,
+                             const uint8_t* d_marks, long long groups, int block_size, long long pitch,
+                             unsigned* d_failed, hipStream_t s) {
+    const int n = c->k + c->m;
+    std::vector<uint8_t> hm((size_t)groups * n);
+    HIP_TRY(hipMemcpyAsync(hm.data(), d_marks, hm.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<int32_t> grec;
+    std::vector<uint32_t> recs;
+    long long nfail = 0;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        int rc = host_records(c, hm.data(), groups, grec, recs, &nfail);
+        if (rc) return rc;
+    }
+    if (recs.empty() && (!nfail || !d_failed)) return QFEC_OK;  // nothing to recover or count
+    recs.resize(std::max<size_t>(recs.size(), 8), 0);
+    std::lock_guard<std::mutex> lk(ctx.mu);  // d_small is the context's: held until the kernel is done
+    const size_t gw = round_up((size_t)groups, 4);
+    int rc = ensure_small(ctx, gw + recs.size());
+    if (rc) return rc;
+    memcpy(ctx.h_small, grec.data(), (size_t)groups * 4);
+    memcpy(ctx.h_small + gw, recs.data(), recs.size() * 4);
+    HIP_TRY(hipMemcpyAsync(ctx.d_small, ctx.h_small, (gw + recs.size()) * 4, hipMemcpyHostToDevice, s));
+    rc = run_reconstruct(ctx, c, nullptr, (const int32_t*)ctx.d_small, ctx.d_small + gw, d_data, d_par, nullptr,
+                         groups, block_size, pitch, d_failed, s);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    return QFEC_OK;
+}
+
 }  // namespace
 
 // ====================================================================== batched device API
@@ -585,6 +620,9 @@ int qfec_reconstruct(qfec_code* code, unsigned char* d_data, const unsigned char
     DevCtx* ctx = nullptr;
     int rc = current_ctx(&ctx);
     if (rc) return rc;
+    if (code->k + code->m > QFEC_LUT_MAX_N) return reconstruct_host_records(*ctx, code, d_data, d_parity, d_marks,
+                                                                           groups, block_size, pitch, d_failed,
+                                                                           (hipStream_t)stream);
     DevTables* d = nullptr;
     {
         std::lock_guard<std::mutex> lk(code->mu);
