@@ -65,7 +65,10 @@ int qfec_encode(qfec_code *code, const unsigned char *d_data, unsigned char *d_p
  * (module/rs.c:620-629; the same set network/NetFecCodec.cpp:504-528 hands to
  * fec_decode).  Groups with no erased data are untouched; groups with more erased data
  * than surviving parity are untouched and counted into *d_failed (device counter,
- * may be NULL; accumulated, not reset).  Requires k + m <= 24. */
+ * may be NULL; accumulated, not reset).  k + m <= 24: asynchronous on `stream`, erasure
+ * pattern -> decode matrix through a device LUT.  k + m > 24: the marks are read back
+ * (k + m bytes per group), decode records are built per distinct pattern on the host,
+ * and the call returns after the kernel has run on `stream`. */
 int qfec_reconstruct(qfec_code *code, unsigned char *d_data, const unsigned char *d_parity,
                      const unsigned char *d_marks, long long groups, int block_size,
                      long long pitch, unsigned int *d_failed, void *stream);

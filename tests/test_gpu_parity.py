@@ -203,11 +203,13 @@ def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
         d1 = data.copy()
         rs_path.reconstruct(d1, par.copy(), marks, B)  # explicit (host-record) path
         assert np.array_equal(d1, d0)
-    if k + m <= 24:
-        dd = to_dev(padded(data, pitch))
-        code.reconstruct(dd, to_dev(padded(par, pitch)), to_dev(marks), B)
-        torch.cuda.synchronize()
-        assert np.array_equal(dd.cpu().numpy()[..., :B], d0)
+    # batched device API: LUT path for k + m <= 24, host-record path above
+    dd = to_dev(padded(data, pitch))
+    failed = torch.zeros(1, dtype=torch.int32, device=DEV)
+    code.reconstruct(dd, to_dev(padded(par, pitch)), to_dev(marks), B, failed)
+    torch.cuda.synchronize()
+    assert np.array_equal(dd.cpu().numpy()[..., :B], d0)
+    assert (int(failed.item()) > 0) == (rc_ref == -1)
     assert rc_ref in (0, -1)
 
 
