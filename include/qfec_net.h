@@ -15,9 +15,13 @@
  *     sends each source datagram at once and the check datagrams at the k-th);
  *   - received packets are delivered per group, in source order (the reference's default
  *     is_sorted mode), at the flush that processes the group;
- *   - one (k, n) code per handle (the reference looks the codec up per header; open one
- *     handle per code); datagrams of another (k, n) are counted as foreign and dropped;
+ *   - the handle sends with one (k, n); it receives groups of any (k, n) with n <= 15, each
+ *     decoded with the code its headers name (the reference looks the codec up per header,
+ *     NetFecCodec.cpp:301, but only decodes the (k, n) pairs registered with it);
  *   - datagrams arriving for a group already processed are dropped (counted).
+ * Non-FEC datagrams (tag other than 0xEC / 0xED, or shorter than 11 bytes: FEC off at the
+ * sender) are handed over minus their tag byte with source index 0, as zfec_unpack_input
+ * does (:200-209), at the next flush_unpack before the groups.
  * Output callbacks have the reference's signatures (NetFecCodec.h:72-73).  Thread-safe per
  * handle (an internal mutex); callbacks run on the flushing thread. */
 #ifndef QFEC_NET_H
@@ -42,6 +46,12 @@ void qfec_net_free(qfec_net *net);
 
 /* A session = one NetFecCodecLayer's FEC state; peer is handed back to the callbacks. */
 int qfec_net_session(qfec_net *net, void *peer);
+
+/* enable_zfec (NetFecCodec.cpp:375-378, FecTransmission.cpp:72-77); sessions start enabled.
+ * With FEC off, qfec_net_pack_input queues [0x13][payload] (pack_fec_off_tag,
+ * FecCodecBuf.cpp:237-269), sent at the next flush before the session's groups, and the
+ * session's FEC numbering does not advance (NetFecCodec.cpp:75-94). */
+int qfec_net_enable(qfec_net *net, int session, int on);
 
 /* zfec_pack_input: queue one payload of session s.  Returns 0, or < 0 (size > max_pkt_size,
  * bad session).  The session's group is packed at the next flush once it holds k packets. */

@@ -20,7 +20,7 @@ EXPORTS = {
                "qfec_frame_udp", "qfec_unframe_udp", "qfec_synth_fill", "qfec_probe_stream",
                "qfec_tune", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
                "qfec_last_error", "qfec_version"],
-    "qfec_net.h": ["qfec_net_new", "qfec_net_free", "qfec_net_session", "qfec_net_pack_input", "qfec_net_flush_pack",
+    "qfec_net.h": ["qfec_net_new", "qfec_net_free", "qfec_net_session", "qfec_net_enable", "qfec_net_pack_input", "qfec_net_flush_pack",
                    "qfec_net_unpack_input", "qfec_net_flush_unpack", "qfec_net_stats"],
 }
 
@@ -66,6 +66,7 @@ def lib():
         "qfec_net_new": (vp, [i, i, i, i]),
         "qfec_net_free": (None, [vp]),
         "qfec_net_session": (i, [vp, vp]),
+        "qfec_net_enable": (i, [vp, i, i]),
         "qfec_net_pack_input": (i, [vp, i, vp, C.c_uint]),
         "qfec_net_flush_pack": (i, [vp, vp, vp]),
         "qfec_net_unpack_input": (i, [vp, i, vp, C.c_uint]),

@@ -24,6 +24,8 @@ __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_
 def _stream_handle(stream):
     if stream is None:
         import torch
+        if not torch.cuda.is_available():  # host-only calls (e.g. qfec_net's FEC-off traffic)
+            return None
         return C.c_void_p(torch.cuda.current_stream().cuda_stream)
     if isinstance(stream, int):
         return C.c_void_p(stream)
@@ -356,6 +358,10 @@ class NetFec:
         check(min(s, 0), "qfec_net_session")
         self._nsess += 1
         return s
+
+    def enable(self, session, on=True):
+        """enable_zfec: with FEC off a session's packets go out as [0x13][payload]."""
+        check(lib().qfec_net_enable(self._h, session, int(bool(on))), "qfec_net_enable")
 
     def pack_input(self, session, data):
         b = bytes(data)

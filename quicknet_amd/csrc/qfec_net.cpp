@@ -13,6 +13,7 @@
 #include <map>
 #include <mutex>
 #include <set>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -66,6 +67,7 @@ struct HostBuf {
 
 struct Session {
     void* peer = nullptr;
+    bool enabled = true;                          // enable_zfec (FecTransmission.cpp:72-77)
     uint32_t i_sent_pkt = 0, i_sent_src_pkt = 0;  // init_zfec_layer: both 0 (:623-625)
     std::vector<uint8_t> part;                    // the open group's payloads
     std::vector<int> part_sizes;
@@ -78,6 +80,7 @@ struct TxGroup {
 
 struct RxGroup {
     int session = 0;
+    int k = 0, n = 0;             // the group's code, from its headers (find_codec per header)
     uint32_t sent0 = 0, src0 = 0;
     int have = 0;
     bool ck = true;               // 0xED datagrams
@@ -100,8 +103,12 @@ struct qfec_net {
     std::vector<long long> tx_offs;
     std::vector<int> tx_sizes;
     std::vector<TxGroup> tx_groups;
+    // FEC-off traffic: [0x13][payload] datagrams to send (pack_fec_off_tag, FecCodecBuf.cpp:
+    // 237-269), and received non-FEC datagrams minus their tag (unpack_fec_head, :366-372)
+    std::vector<std::pair<int, std::vector<uint8_t>>> tx_plain, rx_plain;
     // receive queue
     std::map<std::pair<int, uint32_t>, RxGroup> rx;
+    std::map<int, qfec_code*> rx_codes;  // (k << 4 | n) -> code, for groups of another (k, n)
     std::set<std::pair<int, uint32_t>> rx_done;
     std::deque<std::pair<int, uint32_t>> rx_done_fifo;
     long long stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -126,10 +133,20 @@ void remember_done(qfec_net* net, const std::pair<int, uint32_t>& key) {
     }
 }
 
-// unpack the groups in `keys` (all with the same checksum mode) in one launch
-int unpack_batch(qfec_net* net, const std::vector<std::pair<int, uint32_t>>& keys, int ck,
+// the code for (k, n): the handle's own, or one made on first sight of another (k, n) --
+// the reference looks the codec up per header (find_codec, NetFecCodec.cpp:301)
+qfec_code* rx_code(qfec_net* net, int k, int n) {
+    if (k == net->k && n == net->n) return net->code;
+    qfec_code*& c = net->rx_codes[k << 4 | n];
+    if (!c) c = qfec_code_new(QFEC_VANDERMONDE, k, n - k);  // fec_new(k, n): FecCodec.cpp:84
+    return c;
+}
+
+// unpack the groups in `keys` (all with the same checksum mode and (k, n)) in one launch
+int unpack_batch(qfec_net* net, const std::vector<std::pair<int, uint32_t>>& keys, int ck, int k, int n,
                  qfec_unpack_output_fn out, hipStream_t s) {
-    const int k = net->k, n = net->n;
+    qfec_code* code = rx_code(net, k, n);
+    if (!code) return QFEC_ENOMEM;
     const size_t G = keys.size();
     if (!G) return 0;
     const size_t wp = net->wire_pitch, sp = net->shard_pitch;
@@ -152,7 +169,7 @@ int unpack_batch(qfec_net* net, const std::vector<std::pair<int, uint32_t>>& key
     if (hipMemcpyAsync(net->d_wire.p, hw, wbytes, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(net->d_len.p, hl, lbytes, hipMemcpyHostToDevice, s) != hipSuccess)
         return QFEC_EHIP;
-    int rc = qfec_unpack_datagrams(net->code, net->d_wire.as<unsigned char>(), (long long)wp, net->d_len.as<int>(),
+    int rc = qfec_unpack_datagrams(code, net->d_wire.as<unsigned char>(), (long long)wp, net->d_len.as<int>(),
                                    (long long)G, ck, net->max_pkt + 20 /* getPackedPktSize, FecCodecBuf.cpp:16-25 */,
                                    net->d_shards.as<unsigned char>(), (long long)sp, d_marks, d_rx, d_status, d_psize,
                                    s);
@@ -215,6 +232,7 @@ qfec_net* qfec_net_new(int k, int n, int max_pkt_size, int checksum) {
 void qfec_net_free(qfec_net* net) {
     if (!net) return;
     qfec_code_free(net->code);
+    for (auto& kv : net->rx_codes) qfec_code_free(kv.second);
     delete net;
 }
 
@@ -226,12 +244,26 @@ int qfec_net_session(qfec_net* net, void* peer) {
     return (int)net->sessions.size() - 1;
 }
 
+int qfec_net_enable(qfec_net* net, int session, int on) {
+    if (!net) return QFEC_EINVAL;
+    std::lock_guard<std::mutex> lk(net->mu);
+    if (session < 0 || session >= (int)net->sessions.size()) return QFEC_EINVAL;
+    net->sessions[session].enabled = on != 0;
+    return QFEC_OK;
+}
+
 int qfec_net_pack_input(qfec_net* net, int session, const void* data, unsigned int size) {
     if (!net || (!data && size)) return QFEC_EINVAL;
     std::lock_guard<std::mutex> lk(net->mu);
     if (session < 0 || session >= (int)net->sessions.size() || size > (unsigned)net->max_pkt) return QFEC_EINVAL;
     Session& S = net->sessions[session];
     const uint8_t* p = static_cast<const uint8_t*>(data);
+    if (!S.enabled) {  // zfec_pack_input with FEC off (NetFecCodec.cpp:75-94): numbering unchanged
+        std::vector<uint8_t> d(1 + (size_t)size, 0x13);  // tagFecOFFTag
+        if (size) memcpy(d.data() + 1, p, size);
+        net->tx_plain.emplace_back(session, std::move(d));
+        return QFEC_OK;
+    }
     S.part.insert(S.part.end(), p, p + size);
     S.part_sizes.push_back((int)size);
     if ((int)S.part_sizes.size() < net->k) return QFEC_OK;
@@ -255,8 +287,17 @@ int qfec_net_pack_input(qfec_net* net, int session, const void* data, unsigned i
 int qfec_net_flush_pack(qfec_net* net, qfec_pack_output_fn out, void* stream) {
     if (!net) return QFEC_EINVAL;
     std::lock_guard<std::mutex> lk(net->mu);
+    // FEC-off datagrams first, in queue order (no device work)
+    int plain = 0;
+    for (auto& pd : net->tx_plain) {
+        if (out) out(net->sessions[pd.first].peer, reinterpret_cast<const char*>(pd.second.data()),
+                     (unsigned)pd.second.size());
+        ++plain;
+    }
+    net->tx_plain.clear();
+    net->stats[1] += plain;
     const size_t G = net->tx_groups.size();
-    if (!G) return 0;
+    if (!G) return plain;
     if (qfec_device_count() <= 0) return QFEC_ENODEV;
     const int k = net->k, n = net->n;
     hipStream_t s;
@@ -311,7 +352,7 @@ int qfec_net_flush_pack(qfec_net* net, qfec_pack_output_fn out, void* stream) {
     net->tx_payload.clear();
     net->tx_offs.clear();
     net->tx_sizes.clear();
-    return emitted;
+    return plain + emitted;
 }
 
 int qfec_net_unpack_input(qfec_net* net, int session, const char* datagram, unsigned int size) {
@@ -321,21 +362,31 @@ int qfec_net_unpack_input(qfec_net* net, int session, const char* datagram, unsi
     const uint8_t* d = reinterpret_cast<const uint8_t*>(datagram);
     // header fields only (unpack_fec_head, FecCodecBuf.cpp:334-411); every validity and
     // checksum test is the device's
-    if (size < 11 || (d[0] != 0xEC && d[0] != 0xED) || size > net->wire_pitch) {
+    if (size == 0) {
+        net->stats[6]++;
+        return 0;
+    }
+    if (size < 11 || (d[0] != 0xEC && d[0] != 0xED)) {
+        // not an FEC datagram (FEC off at the sender, tag 0x13, or too short): handed over
+        // as it is minus the tag byte, source index 0 (zfec_unpack_input, :200-209)
+        net->rx_plain.emplace_back(session, std::vector<uint8_t>(d + 1, d + size));
+        return 1;
+    }
+    if (size > net->wire_pitch) {  // longer than this handle's datagrams can be
         net->stats[6]++;
         return 0;
     }
     const uint32_t sent = rd32(d + 1), src = rd32(d + 5);
     const uint32_t ikn = (uint32_t)d[9] | (uint32_t)d[10] << 8;
     const int hn = (int)(ikn & 0xF), hk = (int)((ikn >> 4) & 0xF), ik = (int)((ikn >> 8) & 0xF);
-    if (hn != net->n || hk != net->k || ik >= net->n) {
+    if (hk < 1 || hk >= hn || ik >= hn) {  // no codec can be made for it
         net->stats[6]++;
         return 0;
     }
     // group identity: its first sent index (iPktCurSegBeg = i_recv_pkt - cur_ni, :222) and its
     // first source index (iPktCurSegSrcBeg, :226-234)
     const uint32_t sent0 = sent - (uint32_t)ik;
-    const uint32_t src0 = ik < net->k ? src - (uint32_t)ik : src - (uint32_t)net->k + 1u;
+    const uint32_t src0 = ik < hk ? src - (uint32_t)ik : src - (uint32_t)hk + 1u;
     const std::pair<int, uint32_t> key(session, sent0);
     if (net->rx_done.count(key)) {
         net->stats[7]++;
@@ -344,11 +395,16 @@ int qfec_net_unpack_input(qfec_net* net, int session, const char* datagram, unsi
     RxGroup& R = net->rx[key];
     if (R.len.empty()) {
         R.session = session;
+        R.k = hk;
+        R.n = hn;
         R.sent0 = sent0;
         R.src0 = src0;
         R.ck = d[0] == 0xED;
-        R.rows.assign((size_t)net->n * net->wire_pitch, 0);
-        R.len.assign((size_t)net->n, 0);
+        R.rows.assign((size_t)hn * net->wire_pitch, 0);
+        R.len.assign((size_t)hn, 0);
+    } else if (R.k != hk || R.n != hn) {  // the group's other datagrams say another code
+        net->stats[6]++;
+        return 0;
     }
     if (R.len[ik]) return 0;  // duplicate
     memcpy(R.rows.data() + (size_t)ik * net->wire_pitch, d, size);
@@ -362,16 +418,27 @@ int qfec_net_flush_unpack(qfec_net* net, qfec_unpack_output_fn out, int all, voi
     std::lock_guard<std::mutex> lk(net->mu);
     hipStream_t s;
     pick_stream(stream, &s);
-    if (!net->rx.empty() && qfec_device_count() <= 0) return QFEC_ENODEV;
-    std::vector<std::pair<int, uint32_t>> keys[2];
-    for (auto& kv : net->rx)
-        if (all || kv.second.have >= net->k) keys[kv.second.ck ? 1 : 0].push_back(kv.first);
+    // non-FEC datagrams first, in arrival order (no device work)
     int delivered = 0;
-    for (int ck = 0; ck < 2; ++ck) {
-        const int rc = unpack_batch(net, keys[ck], ck, out, s);
+    for (auto& pd : net->rx_plain) {
+        if (out) out(net->sessions[pd.first].peer, reinterpret_cast<const char*>(pd.second.data()),
+                     (unsigned)pd.second.size(), 0u);
+        ++delivered;
+    }
+    net->rx_plain.clear();
+    net->stats[3] += delivered;
+    // groups: one launch per (checksum mode, k, n)
+    std::map<std::tuple<int, int, int>, std::vector<std::pair<int, uint32_t>>> batches;
+    for (auto& kv : net->rx)
+        if (all || kv.second.have >= kv.second.k)
+            batches[std::make_tuple(kv.second.ck ? 1 : 0, kv.second.k, kv.second.n)].push_back(kv.first);
+    if (!batches.empty() && qfec_device_count() <= 0) return QFEC_ENODEV;
+    for (auto& b : batches) {
+        const int rc = unpack_batch(net, b.second, std::get<0>(b.first), std::get<1>(b.first), std::get<2>(b.first),
+                                    out, s);
         if (rc < 0) return rc;
         delivered += rc;
-        for (auto& key : keys[ck]) {
+        for (auto& key : b.second) {
             net->rx.erase(key);
             remember_done(net, key);
         }

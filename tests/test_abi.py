@@ -136,12 +136,38 @@ def test_net_layer_host_side():
     assert L.qfec_net_pack_input(h, 7, b"x", 1) < 0               # no such session
     for i in range(4):
         assert L.qfec_net_pack_input(h, s1, bytes([i]) * 10, 10) == 0
-    # foreign datagrams are dropped on the host: too short, not FEC, another (k, n)
-    assert L.qfec_net_unpack_input(h, 0, b"\xed" * 5, 5) == 0
+    # dropped on the host: empty, a header no codec fits (k >= n), ik >= n
+    assert L.qfec_net_unpack_input(h, 0, b"", 0) == 0
+    bad = bytes([0xED]) + bytes(8) + bytes([5 | 7 << 4, 0]) + bytes(20)
+    assert L.qfec_net_unpack_input(h, 0, bad, len(bad)) == 0
+    bad = bytes([0xED]) + bytes(8) + bytes([5 | 3 << 4, 9]) + bytes(20)
+    assert L.qfec_net_unpack_input(h, 0, bad, len(bad)) == 0
+    # queued: another (k, n) (decoded with its own code), and non-FEC / short datagrams
     other = bytes([0xED]) + bytes(8) + bytes([5 | 3 << 4, 0]) + bytes(20)
-    assert L.qfec_net_unpack_input(h, 0, other, len(other)) == 0
+    assert L.qfec_net_unpack_input(h, 0, other, len(other)) == 1
+    assert L.qfec_net_unpack_input(h, 0, b"\xed" * 5, 5) == 1
     st = (C.c_longlong * 8)()
-    assert L.qfec_net_stats(h, st) == 0 and st[6] == 2
+    assert L.qfec_net_stats(h, st) == 0 and st[6] == 3
+    assert L.qfec_net_enable(h, 9, 0) < 0
     if L.qfec_device_count() <= 0:
         assert L.qfec_net_flush_pack(h, None, None) == -2   # QFEC_ENODEV
     L.qfec_net_free(h)
+
+
+def test_net_layer_fec_off_host_side():
+    """FEC off at a session (enable_zfec): [0x13][payload] datagrams, no numbering advance;
+    non-FEC datagrams received are handed over minus their tag, source index 0.  Neither
+    needs the device, so this runs anywhere (byte-pinned to the reference in
+    tests/test_reference_callers.py)."""
+    net = qa.NetFec(4, 6, max_pkt_size=1400)
+    s = net.session()
+    net.enable(s, False)
+    net.pack_input(s, b"abc")
+    net.pack_input(s, b"")
+    assert net.flush_pack() == [(s, b"\x13abc"), (s, b"\x13")]
+    rx = qa.NetFec(4, 6)
+    r = rx.session()
+    assert rx.unpack_input(r, b"\x13abc") == 1
+    assert rx.unpack_input(r, b"\xed" * 5) == 1   # an FEC tag but under 11 bytes: plain too
+    assert rx.flush_unpack() == [(r, b"abc", 0), (r, b"\xed" * 4, 0)]
+    assert rx.stats()["delivered"] == 2

@@ -116,3 +116,33 @@ def test_receive_delivers_what_the_reference_would():
     # a datagram for a group already delivered is late
     assert rx.unpack_input(R[0], per[S[0]][0]) == 0
     assert rx.stats()["late"] == 1
+
+
+def test_receive_groups_of_several_codes():
+    """One receiving handle decodes groups of any (k, n) its headers name (the reference looks
+    the codec up per header, NetFecCodec.cpp:301), next to FEC-off datagrams of the same
+    session, which it hands over first with source index 0 (:200-209)."""
+    rng = np.random.default_rng(3)
+    codes = [(4, 6), (3, 5), (10, 13), (7, 8)]
+    rx = qa.NetFec(10, 13, max_pkt_size=1400)
+    sessions = [rx.session() for _ in codes]  # numbering is per session: one sender stream each
+    expect = []
+    for (k, n), r in zip(codes, sessions):
+        tx = qa.NetFec(k, n, max_pkt_size=1400)
+        s = tx.session()
+        sent = [rng.integers(0, 256, size=int(rng.integers(0, 1401)), dtype=np.uint8).tobytes()
+                for _ in range(3 * k)]
+        for p in sent:
+            tx.pack_input(s, p)
+        dg = [d for _, d in tx.flush_pack()]
+        for g in range(3):
+            lost = set(rng.choice(n, n - k, replace=False).tolist())  # exactly k of n arrive
+            for j in range(n):
+                if j not in lost:
+                    assert rx.unpack_input(r, dg[g * n + j]) == 1
+        expect.append([(p, i) for i, p in enumerate(sent)])
+    assert rx.unpack_input(sessions[0], b"\x13plain") == 1
+    got = rx.flush_unpack()
+    assert got[0] == (sessions[0], b"plain", 0)
+    for r, exp in zip(sessions, expect):
+        assert [(p, src) for (ss, p, src) in got[1:] if ss == r] == exp

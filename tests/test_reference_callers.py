@@ -159,3 +159,40 @@ def test_reference_callers_on_libqfec_match_reference():
         for i in lost:
             if i < k:
                 assert r_q[i] == pls[i].tobytes()
+
+
+def test_fec_off_datagrams_match_reference():
+    """FEC off: the reference's pack_fec_off_tag (FecCodecBuf.cpp:237-269) against qfec_net's
+    [0x13][payload] datagrams, and unpack_fec_head on non-FEC datagrams (:366-372) against
+    qfec_net's delivery (tag byte dropped, source index 0).  Host-side only."""
+    import quicknet_amd as qa
+    L, _, _ = load("ref")
+    L.pack_fec_off_tag.argtypes = [C.POINTER(FecCodecBufS), C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    L.pack_fec_off_tag.restype = C.c_void_p
+    S, R = FecCodecBufS(), FecCodecBufS()
+    L.init_fec_buf(C.byref(S), 2048, 16)
+    L.init_fec_buf(C.byref(R), 2048, 16)
+    net = qa.NetFec(4, 6, max_pkt_size=2048)
+    s = net.session()
+    net.enable(s, False)
+    ref = []
+    for p in [b"", b"x", bytes(range(200)), bytes(1400)]:
+        buf = np.frombuffer(p + b"\0", np.uint8)
+        out = C.c_int()
+        q = L.pack_fec_off_tag(C.byref(S), buf.ctypes.data, len(p), C.byref(out))
+        ref.append(C.string_at(q, out.value))
+        net.pack_input(s, p)
+    assert [d for _, d in net.flush_pack()] == ref
+    rx = qa.NetFec(4, 6, max_pkt_size=2048)
+    r = rx.session()
+    want = []
+    for d in ref + [b"\xed" * 7]:
+        buf = np.frombuffer(d, np.uint8)
+        h, out = FecCodecHead(), C.c_int()
+        q = L.unpack_fec_head(C.byref(R), C.byref(h), buf.ctypes.data, len(d), C.byref(out))
+        assert out.value == len(d) - 1
+        want.append(C.string_at(q, out.value))
+        assert rx.unpack_input(r, d) == 1
+    assert [(p, src) for _, p, src in rx.flush_unpack()] == [(w, 0) for w in want]
+    L.release_fec_buf(C.byref(S))
+    L.release_fec_buf(C.byref(R))
