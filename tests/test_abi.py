@@ -17,11 +17,12 @@ from quicknet_amd._lib import EXPORTS, lib
 def header_functions(path):
     txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"^typedef .*?;", "", txt, flags=re.S | re.M)   # callback types
     names = re.findall(r"^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\(", txt, flags=re.M)
     return sorted(set(n for n in names if n not in ("defined",)))
 
 
-@pytest.mark.parametrize("header", ["qfec.h", "qfec_fec.h", "qfec_rs.h"])
+@pytest.mark.parametrize("header", ["qfec.h", "qfec_fec.h", "qfec_rs.h", "qfec_net.h"])
 def test_exports_match_headers(header):
     L = lib()
     declared = header_functions(os.path.join(ROOT, "include", header))
