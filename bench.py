@@ -76,22 +76,26 @@ def barrier(world):
         dist.barrier()
 
 
-def all_max(x, world):
+def _all_reduce(x, world, op):
+    """One float over all ranks.  The tensor lives where the backend wants it: on the GPU for
+    RCCL, on the host for gloo (tests/test_multiproc.py drives these helpers over gloo)."""
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
     return float(t.item())
+
+
+def all_max(x, world):
+    import torch.distributed as dist
+    return _all_reduce(x, world, dist.ReduceOp.MAX)
 
 
 def all_sum(x, world):
-    if world == 1:
-        return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _all_reduce(x, world, dist.ReduceOp.SUM)
 
 
 def cpu_baseline(args, budget_s):

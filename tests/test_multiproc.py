@@ -89,3 +89,35 @@ def test_gloo_two_ranks_match_single():
     assert hashlib.sha256(blob).digest() == hashlib.sha256(par.tobytes()).digest()
     assert units == G and tmax > 0
     assert aggregate_rate([32, 32], [1.0, 2.0]) == 32.0
+
+
+def _bench_helpers_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench  # the same helpers bench.py's timed region uses (gloo: host tensors)
+    bench.barrier(world)
+    el = bench.all_max(0.5 + rank, world)                 # the slowest rank's time
+    ok = bench.all_sum(0.0 if rank != 1 else 1.0, world)  # one rank failed verification
+    total = bench.all_sum(float(100 * (rank + 1)), world)  # all ranks' bytes
+    if rank == 0:
+        out.put((el, ok, total))
+    dist.destroy_process_group()
+
+
+def test_bench_reductions_over_gloo():
+    """bench.py's barrier / max-over-ranks time / summed bytes, run as two gloo ranks: the
+    job value is all ranks' bytes over the slowest rank's time, and one rank's failed check
+    makes the whole line fail."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_helpers_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    el, ok, total = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert (el, ok, total) == (1.5, 1.0, 300.0)
