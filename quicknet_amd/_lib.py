@@ -7,7 +7,8 @@ the library is missing, importing the codec raises.
 import ctypes as C
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libqfec.so")
+# QFEC_LIB: another build of the same library, for before/after A/B runs (tools/ab_lib.sh)
+LIB_PATH = os.environ.get("QFEC_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libqfec.so")
 
 # every symbol the headers in include/ declare (checked by tests/test_abi.py)
 EXPORTS = {

@@ -637,6 +637,7 @@ struct UnpackPlan {
     int sv_row[K], sv_size[K];
     int ns;               // survivors loaded (K when recoverable, else the valid data rows)
     int lost_row[M], e;   // decoded rows
+    bool dec;             // rows to decode (known from the masks, before the record loads)
     const uint32_t* tab;
     uint32_t zero_rows;   // data rows to zero (lost, group not recoverable)
     uint32_t ex_off[M];   // rows only checksummed (first round)
@@ -667,7 +668,7 @@ __device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const ui
     for (int j = 0; j < M; ++j)
 #pragma unroll
         for (int d = 0; d < NV; ++d) acc[j][d] = 0;
-    if (pl.e > 0) {
+    if (pl.dec) {  // not pl.e: the table loads need not wait for the record header
 #pragma unroll
         for (int c = 0; c < K; ++c) {
             Sel sc[NV];
@@ -786,9 +787,9 @@ __global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t*
     uint32_t stated = 0;
     bool okh = false;
     if (lane < N) {
+        // the header load does not wait for the length: row starts are always in the buffer
         len = wire_len[g * N + lane];
-        uint4 h = make_uint4(0, 0, 0, 0);
-        if (len >= 11 && len <= (int)wp) h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
+        const uint4 h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
         const uint32_t tag = get_byte(h, 0);
         hdr = tag == 0xED ? 13 : 11;
         const uint32_t ikn = get_byte(h, 9) | (get_byte(h, 10) << 8);
@@ -818,6 +819,7 @@ __global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t*
         recoverable = __builtin_popcount(avail) >= K;
         pl.ns = 0;
         pl.e = 0;
+        pl.dec = false;
         pl.zero_rows = 0;
         pl.tab = records;
         uint32_t take = avail;
@@ -843,6 +845,7 @@ __global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t*
             const int rec = lut[(~avail) & rowmask];
             pl.tab = records + rec + rec_hdr;
             pl.e = (int)records[rec];
+            pl.dec = true;
 #pragma unroll
             for (int j = 0; j < M; ++j) {  // the record header has room for M lost ids
                 const int lr = (int)records[rec + 4 + K + j];
