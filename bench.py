@@ -366,6 +366,7 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
+        barrier(world)  # the other ranks wait for rank 0's side configurations, then all tear down
         dist.destroy_process_group()
     return 0 if ok else 1
 
