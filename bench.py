@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--variant", type=int, default=0, help="0 perm tables (default), 1 LDS log/exp")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16,
+                   help="threads for the all-cores CPU baseline (the GPU box's CPU share is 16; 0 skips it)")
     p.add_argument("--no-side", action="store_true", help="skip the side configurations (rank 0, after the timed run)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py), if present")
@@ -150,6 +152,61 @@ def cpu_baseline(args, budget_s):
     return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": f"{reps} x (encode {sample} groups + reconstruct {dec_groups} groups with {args.erasures} "
                       f"random erasures/group), RS({k},{m}) B={B}, {el:.1f} s, 1 thread"}
+
+def cpu_baseline_threads(args, budget_s, threads):
+    """The same reference rs.c sample on `threads` host threads: groups split into contiguous
+    slices (quicknet_amd.sharding's rule), one pointer array per slice, each thread looping
+    encode + reconstruct on its slice until the budget is spent.  ctypes drops the GIL for
+    the foreign call, so the threads run the C code in parallel; rs.c is reentrant after
+    reed_solomon_init (its tables are read-only, the decode matrix lives on the stack)."""
+    import threading
+    from oracle.oracle import RefCodec
+    from quicknet_amd.sharding import shard_range
+    from quicknet_amd.synth import synth_bytes
+    if not RefCodec.available() or args.flavour != "cauchy":
+        return None
+    k, m, B = args.k, args.m, args.block
+    sample = 10_000
+    data = synth_bytes(SEED_ENCODE, sample * k * B).reshape(sample, k, B)
+    par = np.zeros((sample, m, B), np.uint8)
+    gm = erasure_marks(SEED_DECODE, sample, k + m, args.erasures)
+    ref = RefCodec()
+    h = ref.rs.reed_solomon_new(k, m)
+    slices = []
+    for t in range(threads):
+        a, b = shard_range(sample, t, threads)
+        if b > a:
+            sl_marks = marks_to_rs_layout(gm[a:b], k)
+            slices.append((ref.shard_ptrs(data[a:b], par[a:b]), sl_marks, (b - a) * (k + m),
+                           (b - a + int((gm[a:b, :k].sum(1) > 0).sum())) * k * B))
+    done = [0] * len(slices)
+    spent = [0.0] * len(slices)
+    start = threading.Barrier(len(slices) + 1)
+
+    def run(i):
+        ptrs, mk, n, _ = slices[i]
+        start.wait()
+        t0 = time.perf_counter()
+        while True:
+            ref.rs_encode(h, ptrs, n, B)
+            ref.rs_reconstruct(h, ptrs, mk, n, B)
+            done[i] += 1
+            spent[i] = time.perf_counter() - t0
+            if spent[i] >= budget_s:
+                break
+
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(len(slices))]
+    for t in ths:
+        t.start()
+    start.wait()
+    for t in ths:
+        t.join()
+    el = max(spent)
+    gib = sum(done[i] * slices[i][3] for i in range(len(slices))) / GIB
+    return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": len(slices), "kind": "reference",
+            "sample": f"{sum(done)} slice passes over {sample} groups split {len(slices)} ways (encode + reconstruct with "
+                      f"{args.erasures} random erasures/group), RS({k},{m}) B={B}, {el:.1f} s, {len(slices)} threads"}
+
 
 # BASELINE configs measured beside the headline line (rank 0's GPU, after the timed region):
 # the Vandermonde flavour the network stack links (module/fec.c) at configs[1]+[2], config 4's
@@ -331,12 +388,17 @@ def main():
             side.append(side_config(fl, sk, sm, sB, sG, sE, world, rank))
         ok = ok and all(x["verified"] for x in side)
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             cpu = cpu_baseline(args, args.cpu_seconds)
         except Exception as exc:  # report, never fake
             cpu = {"value": None, "error": repr(exc)}
+        if args.cpu_threads > 0:
+            try:
+                cpu_mt = cpu_baseline_threads(args, args.cpu_seconds / 2, args.cpu_threads)
+            except Exception as exc:
+                cpu_mt = {"value": None, "error": repr(exc)}
 
     if rank == 0:
         out = {
@@ -367,6 +429,7 @@ def main():
             "probe_stream_gbs": round(enc_alg / (probe_ms * 1e-3) / 1e9, 1) if probe_ms else None,
             "verified": ok,
             "cpu_baseline": cpu,
+            "cpu_baseline_threads": cpu_mt,
             "side_configs": side,
         }
         print(json.dumps(out), flush=True)
