@@ -147,7 +147,7 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
                       int block_size, long long pitch, void *stream);
 
 /* Experiment knobs for interleaved A/B timing (tools/ab.py, tools/wire_ab.py): "encode_impl"
- * 0|1, "recon_impl" -1 (auto) | 0 | 1, "wire_fused" 1 (fused datagram send where a (k, m)
+ * 0|1, "recon_impl" -1 (auto) | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B lanes, "wire_fused" 1 (fused datagram send where a (k, m)
  * instance exists) | 0 (staged build -> encode -> emit), "wire_store_nt" 0-3.  Defaults are the measured best; results are identical. */
 int qfec_tune(const char *key, int value);
 

@@ -66,6 +66,7 @@ struct ReconArgs {
                               // 2 exact-e rows (16-B lanes), 3 exact-e rows (8-B lanes)
     uint32_t wpg;             // waves per group = ceil(cols / 64) (vec16 LUT kernels)
     uint32_t cols8, wpg8;     // the same at 8-B columns: ceil(B / 8), ceil(cols8 / 64)
+    uint32_t cols12, wpg12;   // the same at 12-B columns (recon_impl 4)
 };
 
 // FEC datagram batches (qfec_wire.hip): shards[G][n][pitch], wire[G][n][wire_pitch]

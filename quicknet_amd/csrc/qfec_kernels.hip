@@ -350,8 +350,13 @@ __device__ __forceinline__ void ldv(uint32_t (&v)[D], const uint8_t* p) {
     if constexpr (D == 4) {
         const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
         v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else if constexpr (D == 3) {  // merged into one global_load_dwordx3 ... nt
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+        v[0] = __builtin_nontemporal_load(q);
+        v[1] = __builtin_nontemporal_load(q + 1);
+        v[2] = __builtin_nontemporal_load(q + 2);
     } else {
-        static_assert(D == 2, "4 or 2 dwords per lane");
+        static_assert(D == 2, "4, 3 or 2 dwords per lane");
         const u32x2 t = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
         v[0] = t.x; v[1] = t.y;
     }
@@ -361,6 +366,11 @@ __device__ __forceinline__ void stv(uint8_t* p, const uint32_t (&v)[D]) {
     if constexpr (D == 4) {
         const u32x4 t = {v[0], v[1], v[2], v[3]};
         __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(p));
+    } else if constexpr (D == 3) {
+        uint32_t* q = reinterpret_cast<uint32_t*>(p);
+        __builtin_nontemporal_store(v[0], q);
+        __builtin_nontemporal_store(v[1], q + 1);
+        __builtin_nontemporal_store(v[2], q + 2);
     } else {
         const u32x2 t = {v[0], v[1]};
         __builtin_nontemporal_store(t, reinterpret_cast<u32x2*>(p));
@@ -453,7 +463,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const uint32_t wpg = IMPL == 3 ? a.wpg8 : a.wpg;
+    const uint32_t wpg = IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
     if (g >= a.groups) return;
@@ -482,9 +492,10 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
         src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : par_g + (uint64_t)(s - K) * pitch;
     }
     const uint32_t col = part * 64u + lane;
-    if (col < (IMPL == 3 ? a.cols8 : a.cols)) {
+    if (col < (IMPL == 3 ? a.cols8 : IMPL == 4 ? a.cols12 : a.cols)) {
         if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
         else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 8u);
+        else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 12u);
         else if (IMPL == 1) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
         else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
     }
@@ -648,11 +659,14 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 
 #define QFEC_REC_CASE(KK, MM)                                                      \
     if (a.k == KK && a.m == MM) {                                                  \
-        /* auto: exact-e rows up to k*m = 64 (8-B lanes when that fills the      */ \
-        /* waves better, e.g. B = 1400), else the row loop; tools/ab.py times all */ \
-        const int im = a.impl < 0 ? (KK * MM <= 64 ? (lanes8 ? 3 : 2) : 0) : a.impl; \
-        const unsigned pgrid = im == 3 ? pgrid8 : pgrid16;                         \
-        if (im == 3) QFEC_REC_LAUNCH(KK, MM, 3);                                   \
+        /* auto: exact-e rows up to k*m = 64 (8-B or 12-B lanes when they fill   */ \
+        /* the waves better, e.g. B = 1400), else the row loop; tools/ab.py times */ \
+        int im = a.impl < 0 ? (KK * MM <= 64 ? (KK * MM <= 30 && lanes12 ? 4 : lanes8 ? 3 : 2) : 0) \
+                            : a.impl;                                              \
+        if (im == 4 && !lanes12_ok) im = 2;                                        \
+        const unsigned pgrid = im == 3 ? pgrid8 : im == 4 ? pgrid12 : pgrid16;     \
+        if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                                   \
+        else if (im == 3) QFEC_REC_LAUNCH(KK, MM, 3);                              \
         else if (im == 2) QFEC_REC_LAUNCH(KK, MM, 2);                              \
         else if (im == 1) QFEC_REC_LAUNCH(KK, MM, 1);                              \
         else QFEC_REC_LAUNCH(KK, MM, 0);                                           \
@@ -670,10 +684,19 @@ hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
         hipLaunchKernelGGL((k_reconstruct_any<true>), dim3(grid), dim3(256), 0, stream, a);
         return hipGetLastError();
     }
-    const uint64_t waves = a.groups * (uint64_t)std::max(a.wpg, a.wpg8);
+    const uint64_t waves = a.groups * (uint64_t)std::max(std::max(a.wpg, a.wpg8), a.wpg12);
     if (waves > 0xFFFFFFFFull) return hipErrorInvalidValue;  // caller chunks batches
     const unsigned pgrid16 = grid_for(a.groups * (uint64_t)a.wpg, 4);
     const unsigned pgrid8 = grid_for(a.groups * (uint64_t)a.wpg8, 4);
+    const unsigned pgrid12 = grid_for(a.groups * (uint64_t)a.wpg12, 4);
+    // 12-B lanes write no further than the 16-B columns do (B = 1400: 117 x 12 = 1404 <= 1408)
+    const bool lanes12_ok = a.cols12 * 12u <= a.cols * 16u;
+    // 12-B lanes where they fill as well as 8-B lanes with 2/3 of the waves; for small k*m
+    // only (profiles/r01ak_recon_lanes.txt: RS(10,3) B=1400 12-B 5 918 vs 8-B 5 734 GB/s,
+    // RS(16,4) B=1400 4 964 vs 5 108 -- at 90 VGPRs the 12-B body drops to 5 waves/SIMD)
+    const double fill16 = (double)a.cols / (64.0 * a.wpg), fill8 = (double)a.cols8 / (64.0 * a.wpg8),
+                 fill12 = (double)a.cols12 / (64.0 * a.wpg12);
+    const bool lanes12 = lanes12_ok && fill12 > fill16 + 0.1 && fill12 >= fill8 - 0.01;
     // 8-B lanes when they fill the group's waves clearly better than 16-B lanes
     const bool lanes8 = (double)a.cols8 / (64.0 * a.wpg8) > (double)a.cols / (64.0 * a.wpg) + 0.1;
     QFEC_REC_CASE(10, 3)

@@ -394,6 +394,8 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.wpg = (a.cols + 63) / 64;
     a.cols8 = (uint32_t)((block + 7) / 8);
     a.wpg8 = (a.cols8 + 63) / 64;
+    a.cols12 = (uint32_t)((block + 11) / 12);
+    a.wpg12 = (a.cols12 + 63) / 64;
     hipError_t e = launch_reconstruct(a, s);
     if (e != hipSuccess) return hip_fail(e, "reconstruct kernel launch");
     return QFEC_OK;
@@ -528,7 +530,7 @@ int qfec_get_kernel_variant(void) { return g_variant.load(); }
 // experiment knobs, for A/B timing in one process (tools/ab.py); not needed in production
 int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
-    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 3) { tuning().recon_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 4) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
     if (!strcmp(key, "wire_chunk") && value >= 0) { tuning().wire_chunk = value; return QFEC_OK; }

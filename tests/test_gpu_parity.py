@@ -213,8 +213,9 @@ def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
     assert rc_ref in (0, -1)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2, 3])
-@pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (4, 2, 100), (12, 4, 40), (3, 2, 1400)])
+@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (4, 2, 100), (12, 4, 40), (3, 2, 1400),
+                                   (10, 3, 1400), (4, 2, 1012)])
 def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
     """Every LUT reconstruct body (row loop, all rows, exact-e rows on 16-B and on 8-B
     lanes) against the oracle's rs.c restatement, on random erasure patterns (0..m+1

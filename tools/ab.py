@@ -28,6 +28,7 @@ def main():
     p.add_argument("--block", type=int, default=1024)
     p.add_argument("--groups", type=int, default=100_000)
     p.add_argument("--erasures", type=int, default=3)
+    p.add_argument("--recon-only", action="store_true")
     p.add_argument("--pairs", action="store_true", help="time reconstruct right after encode, as bench.py does")
     a = p.parse_args()
     k, m, B, G = a.k, a.m, a.block, a.groups
@@ -68,7 +69,10 @@ def main():
         ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
         ("recon impl2 (exact e rows)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),
         ("recon impl3 (exact e, 8-B lanes)", lambda: qa.tune("recon_impl", 3), rec, dec_bytes),
+        ("recon impl4 (exact e, 12-B lanes)", lambda: qa.tune("recon_impl", 4), rec, dec_bytes),
     ]
+    if a.recon_only:
+        variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]
     if a.pairs:
         variants = []
     times = {v[0]: [] for v in variants}
