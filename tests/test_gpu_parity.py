@@ -248,6 +248,28 @@ def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
     assert int(failed.item()) == unrecoverable
 
 
+@pytest.mark.parametrize("impl", [0, 1])
+@pytest.mark.parametrize("flavour", ["cauchy", "vandermonde"])
+@pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (10, 3, 100), (16, 4, 8)])
+def test_encode_impls_vs_oracle(oracle, impl, flavour, k, m, B):
+    """Both encode bodies (all rows at once, row loop) against the oracle's
+    restatement of rs.c's code_some_shards on 300 random groups."""
+    G = 300
+    code = qa.Code.cauchy(k, m) if flavour == "cauchy" else qa.Code.vandermonde(k, m)
+    data = synth_bytes(k * 13 + B, G * k * B).reshape(G, k, B)
+    expect = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(code.rows, data, expect, B)
+    pitch = round16(B)
+    p = to_dev(np.full((G, m, pitch), 0x5A, np.uint8))
+    qa.tune("encode_impl", impl)
+    try:
+        code.encode(to_dev(padded(data, pitch, 0xC3)), p, B)
+        torch.cuda.synchronize()
+    finally:
+        qa.tune("encode_impl", 0)
+    assert np.array_equal(p.cpu().numpy()[..., :B], expect)
+
+
 def test_large_batch_roundtrip(oracle):
     """BASELINE config 2/3 shape at full size: 100 000 groups x RS(10,3) x 1 KiB.
     Encode checked byte for byte against the oracle; reconstruct with 3 random erasures

@@ -29,6 +29,7 @@ def main():
     p.add_argument("--groups", type=int, default=100_000)
     p.add_argument("--erasures", type=int, default=3)
     p.add_argument("--recon-only", action="store_true")
+    p.add_argument("--encode-only", action="store_true")
     p.add_argument("--pairs", action="store_true", help="time reconstruct right after encode, as bench.py does")
     a = p.parse_args()
     k, m, B, G = a.k, a.m, a.block, a.groups
@@ -73,6 +74,8 @@ def main():
     ]
     if a.recon_only:
         variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]
+    if a.encode_only:
+        variants = [v for v in variants if v[0].startswith(("encode impl0", "encode impl1", "probe"))]
     if a.pairs:
         variants = []
     times = {v[0]: [] for v in variants}
