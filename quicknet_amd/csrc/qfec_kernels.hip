@@ -660,8 +660,9 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 #define QFEC_REC_CASE(KK, MM)                                                      \
     if (a.k == KK && a.m == MM) {                                                  \
         /* auto: exact-e rows up to k*m = 64 (8-B or 12-B lanes when they fill   */ \
-        /* the waves better, e.g. B = 1400), else the row loop; tools/ab.py times */ \
-        int im = a.impl < 0 ? (KK * MM <= 64 ? (KK * MM <= 30 && lanes12 ? 4 : lanes8 ? 3 : 2) : 0) \
+        /* the waves better, e.g. B = 1400, 8-B for k >= 10), else the row loop    */ \
+        const bool wide8 = KK >= 10 && fill8 >= fill16 - 0.01;                     \
+        int im = a.impl < 0 ? (KK * MM <= 64 ? (KK * MM <= 30 && lanes12 ? 4 : (lanes8 || wide8) ? 3 : 2) : 0) \
                             : a.impl;                                              \
         if (im == 4 && !lanes12_ok) im = 2;                                        \
         const unsigned pgrid = im == 3 ? pgrid8 : im == 4 ? pgrid12 : pgrid16;     \
@@ -698,7 +699,11 @@ hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
                  fill12 = (double)a.cols12 / (64.0 * a.wpg12);
     const bool lanes12 = lanes12_ok && fill12 > fill16 + 0.1 && fill12 >= fill8 - 0.01;
     // 8-B lanes when they fill the group's waves clearly better than 16-B lanes
-    const bool lanes8 = (double)a.cols8 / (64.0 * a.wpg8) > (double)a.cols / (64.0 * a.wpg) + 0.1;
+    const bool lanes8 = fill8 > fill16 + 0.1;
+    // and for k >= 10 even when 16-B lanes fill their waves: the 8-B body's lower register
+    // count (RS(10,3) 69 vs 103 VGPRs: 7 vs 4 waves/SIMD) wins when reconstruct runs right
+    // after an encode, as in the bench step (profiles/r01aq_pairs.txt: RS(10,3) B=1024
+    // +2.5 %, RS(16,4) B=1024 +6.2 %; RS(4,2) B=1024 loses 6.7 % and stays on 16-B lanes)
     QFEC_REC_CASE(10, 3)
     QFEC_REC_CASE(16, 4)
     QFEC_REC_CASE(4, 2)
