@@ -213,12 +213,12 @@ def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
     assert rc_ref in (0, -1)
 
 
-@pytest.mark.parametrize("impl", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4])
 @pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (4, 2, 100), (12, 4, 40), (3, 2, 1400),
-                                   (10, 3, 1400), (4, 2, 1012)])
+                                   (10, 3, 1400), (4, 2, 1012), (16, 4, 1024), (12, 4, 1400), (8, 4, 1024)])
 def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
-    """Every LUT reconstruct body (row loop, all rows, exact-e rows on 16-B and on 8-B
-    lanes) against the oracle's rs.c restatement, on random erasure patterns (0..m+1
+    """Every LUT reconstruct body (-1 = the auto choice; row loop, all rows, exact-e rows on
+    16-B, 8-B and 12-B lanes) against the oracle's rs.c restatement, on random erasure patterns (0..m+1
     erasures, so unrecoverable groups too) with random, inconsistent parity: the survivor
     rule and the stale-row quirk have to match byte for byte."""
     G = 700
