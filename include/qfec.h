@@ -60,6 +60,14 @@ int qfec_code_shape(const qfec_code *code, int *k, int *m);
 int qfec_encode(qfec_code *code, const unsigned char *d_data, unsigned char *d_parity,
                 long long groups, int block_size, long long pitch, void *stream);
 
+/* qfec_encode on HOST buffers (the network path starts and ends in host memory): the batch
+ * runs in ~32 MiB chunks over two internal streams, H2D -> encode -> D2H of one chunk
+ * overlapping the staging of the next.  Pageable buffers are staged through pinned memory;
+ * hipHostMalloc'd / registered buffers are DMA'd directly.  Returns after the last parity
+ * chunk is in h_parity.  Layouts as qfec_encode. */
+int qfec_encode_host(qfec_code *code, const unsigned char *h_data, unsigned char *h_parity,
+                     long long groups, int block_size, long long pitch);
+
 /* Rewrite every erased data shard from k survivors: the surviving data shards in
  * ascending order, then the first e surviving parity shards in ascending order
  * (module/rs.c:620-629; the same set network/NetFecCodec.cpp:504-528 hands to

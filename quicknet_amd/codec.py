@@ -152,6 +152,19 @@ class Code:
         check(lib().qfec_code_rows(self._h, out.ctypes.data), "qfec_code_rows")
         return out
 
+    def encode_host(self, data, parity, block_size=None):
+        """qfec_encode_host: data uint8 [G, k, pitch] and parity [G, m, pitch] in HOST memory
+        (numpy arrays, or CPU tensors, pinned or not); returns when parity is written."""
+        G, k, pitch = data.shape
+        if k != self.k or parity.shape[0] != G or parity.shape[1] != self.m or parity.shape[2] != pitch:
+            raise QfecError(f"shape mismatch: data {tuple(data.shape)} parity {tuple(parity.shape)} for ({self.k},{self.m})")
+        block_size = pitch if block_size is None else block_size
+        ptr = (lambda a: a.ctypes.data) if isinstance(data, np.ndarray) else (lambda t: t.data_ptr())
+        for a in (data, parity):
+            if not (a.flags["C_CONTIGUOUS"] if isinstance(a, np.ndarray) else a.is_contiguous()):
+                raise QfecError("encode_host: contiguous host buffers required")
+        check(lib().qfec_encode_host(self._h, ptr(data), ptr(parity), G, block_size, pitch), "qfec_encode_host")
+
     def encode(self, data, parity, block_size=None, stream=None):
         """parity[g] = P x data[g]; data uint8 [G, k, pitch], parity uint8 [G, m, pitch] on device."""
         G, k, pitch = data.shape

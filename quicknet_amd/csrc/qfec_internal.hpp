@@ -127,6 +127,7 @@ struct Tuning {
     int wire_rx_tail = 1;   // fused receive: 1 = tail dwords ride on the last 16-B pass (0: own pass)
     int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
     int wire_chunk = 0;     // fused send: groups per body + head launch pair (0: as many as fit)
+    int host_chunk = 0;     // qfec_encode_host: groups per pipelined chunk (0: ~32 MiB of data)
 };
 Tuning& tuning();
 

@@ -85,6 +85,17 @@ struct DevCtx {
     uint32_t* h_small = nullptr; // pinned mirror
     unsigned* d_counter = nullptr;
     int init_rc = QFEC_ENODEV;
+    // qfec_encode_host: two chunk slots, each with its own stream, event, device buffers
+    // and pinned staging (created on first use)
+    struct HostSlot {
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        uint8_t* d_buf = nullptr;  // data chunk | parity chunk
+        uint8_t* h_in = nullptr;   // pinned
+        uint8_t* h_out = nullptr;  // pinned
+        size_t in_cap = 0, out_cap = 0;
+    } host[2];
+    std::mutex host_mu;
 };
 
 DevCtx g_ctx[kMaxDevices];
@@ -175,6 +186,38 @@ bool is_device_ptr(const void* p) {
         return false;
     }
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+// host memory the DMA engines can read directly (hipHostMalloc'd or hipHostRegister'ed)
+bool is_pinned_host(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+int ensure_host_slot(DevCtx::HostSlot& h, size_t in_bytes, size_t out_bytes) {
+    if (!h.stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
+    }
+    if (in_bytes > h.in_cap || out_bytes > h.out_cap) {
+        if (h.d_buf) HIP_TRY(hipFree(h.d_buf));
+        if (h.h_in) HIP_TRY(hipHostFree(h.h_in));
+        if (h.h_out) HIP_TRY(hipHostFree(h.h_out));
+        h.d_buf = h.h_in = h.h_out = nullptr;
+        h.in_cap = h.out_cap = 0;
+        HIP_TRY(hipMalloc(&h.d_buf, in_bytes + out_bytes));
+        HIP_TRY(hipHostMalloc(&h.h_in, in_bytes, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&h.h_out, out_bytes, hipHostMallocDefault));
+        h.in_cap = in_bytes;
+        h.out_cap = out_bytes;
+    }
+    return QFEC_OK;
 }
 
 }  // namespace
@@ -531,6 +574,7 @@ int qfec_get_kernel_variant(void) { return g_variant.load(); }
 int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
     if (!strcmp(key, "recon_impl") && value >= -1 && value <= 4) { tuning().recon_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "host_chunk") && value >= 0) { tuning().host_chunk = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
     if (!strcmp(key, "wire_chunk") && value >= 0) { tuning().wire_chunk = value; return QFEC_OK; }
@@ -594,6 +638,67 @@ int qfec_encode(qfec_code* code, const unsigned char* d_data, unsigned char* d_p
     }
     if (rc) return rc;
     return run_encode(*ctx, code, tab, code->m, d_data, d_parity, groups, block_size, pitch, (hipStream_t)stream);
+}
+
+int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char* h_parity, long long groups,
+                     int block_size, long long pitch) {
+    if (!code || groups < 0 || block_size < 1 || pitch < block_size || (groups > 0 && (!h_data || !h_parity))) {
+        set_error("qfec_encode_host: invalid argument");
+        return QFEC_EINVAL;
+    }
+    if (groups == 0 || code->m == 0) return QFEC_OK;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    uint32_t* tab = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_enc(code, ctx->device, &tab);
+    }
+    if (rc) return rc;
+    const int k = code->k, m = code->m;
+    const size_t in_g = (size_t)k * (size_t)pitch, out_g = (size_t)m * (size_t)pitch;
+    // chunk: ~32 MiB of data shards (tuning "host_chunk" = groups per chunk overrides)
+    long long gc = tuning().host_chunk > 0 ? tuning().host_chunk
+                                           : std::max<long long>(1, (long long)((size_t)32 << 20) / (long long)in_g);
+    gc = std::min(gc, groups);
+    const bool pin_in = is_pinned_host(h_data), pin_out = is_pinned_host(h_parity);
+    std::lock_guard<std::mutex> lk(ctx->host_mu);
+    for (auto& h : ctx->host)
+        if ((rc = ensure_host_slot(h, (size_t)gc * in_g, (size_t)gc * out_g))) return rc;
+    long long pending[2] = {-1, -1};  // chunk whose parity sits in the slot's staging
+    auto drain = [&](int sl) -> int {
+        if (pending[sl] < 0) return QFEC_OK;
+        HIP_TRY(hipEventSynchronize(ctx->host[sl].done));
+        if (!pin_out) {
+            const long long g0 = pending[sl] * gc, gn = std::min(gc, groups - g0);
+            memcpy(h_parity + (size_t)g0 * out_g, ctx->host[sl].h_out, (size_t)gn * out_g);
+        }
+        pending[sl] = -1;
+        return QFEC_OK;
+    };
+    const long long nchunks = (groups + gc - 1) / gc;
+    for (long long i = 0; i < nchunks; ++i) {
+        const int sl = (int)(i & 1);
+        DevCtx::HostSlot& h = ctx->host[sl];
+        if ((rc = drain(sl))) return rc;  // the slot's previous chunk: copies done, parity out
+        const long long g0 = i * gc, gn = std::min(gc, groups - g0);
+        const unsigned char* src = h_data + (size_t)g0 * in_g;
+        if (!pin_in) {  // pageable: through pinned staging, overlapping the other slot's work
+            memcpy(h.h_in, src, (size_t)gn * in_g);
+            src = h.h_in;
+        }
+        uint8_t* d_in = h.d_buf;
+        uint8_t* d_out = h.d_buf + (size_t)gc * in_g;
+        HIP_TRY(hipMemcpyAsync(d_in, src, (size_t)gn * in_g, hipMemcpyHostToDevice, h.stream));
+        if ((rc = run_encode(*ctx, code, tab, m, d_in, d_out, gn, block_size, pitch, h.stream))) return rc;
+        unsigned char* dst = pin_out ? h_parity + (size_t)g0 * out_g : h.h_out;
+        HIP_TRY(hipMemcpyAsync(dst, d_out, (size_t)gn * out_g, hipMemcpyDeviceToHost, h.stream));
+        HIP_TRY(hipEventRecord(h.done, h.stream));
+        pending[sl] = i;
+    }
+    if ((rc = drain((int)(nchunks & 1)))) return rc;  // older slot first
+    return drain((int)((nchunks + 1) & 1));
 }
 
 int qfec_prepare_reconstruct(qfec_code* code) {

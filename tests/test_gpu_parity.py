@@ -270,6 +270,33 @@ def test_encode_impls_vs_oracle(oracle, impl, flavour, k, m, B):
     assert np.array_equal(p.cpu().numpy()[..., :B], expect)
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("k,m,B,chunk", [(10, 3, 1024, 7), (16, 4, 1400, 0), (4, 2, 37, 5)])
+def test_encode_host_vs_oracle(oracle, k, m, B, chunk, pinned):
+    """qfec_encode_host (host in, host out, chunked over two streams) against the oracle;
+    chunk = groups per pipelined chunk (0: the ~32 MiB default, one chunk here), pageable
+    numpy buffers or pinned torch tensors."""
+    G = 101
+    code = qa.Code.cauchy(k, m)
+    pitch = B if B % 16 else round16(B)
+    data = synth_bytes(k * 31 + B, G * k * B).reshape(G, k, B)
+    expect = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(code.rows, data, expect, B)
+    hd = padded(data, pitch, 0xC3)
+    if pinned:
+        hd = torch.from_numpy(hd).pin_memory()
+        hp = torch.full((G, m, pitch), 0x5A, dtype=torch.uint8).pin_memory()
+    else:
+        hp = np.full((G, m, pitch), 0x5A, np.uint8)
+    qa.tune("host_chunk", chunk)
+    try:
+        code.encode_host(hd, hp, B)
+    finally:
+        qa.tune("host_chunk", 0)
+    got = hp.numpy() if pinned else hp
+    assert np.array_equal(got[..., :B], expect)
+
+
 def test_large_batch_roundtrip(oracle):
     """BASELINE config 2/3 shape at full size: 100 000 groups x RS(10,3) x 1 KiB.
     Encode checked byte for byte against the oracle; reconstruct with 3 random erasures
