@@ -68,6 +68,13 @@ int qfec_encode(qfec_code *code, const unsigned char *d_data, unsigned char *d_p
 int qfec_encode_host(qfec_code *code, const unsigned char *h_data, unsigned char *h_parity,
                      long long groups, int block_size, long long pitch);
 
+/* qfec_reconstruct on HOST buffers, chunked like qfec_encode_host: h_data is rewritten in
+ * place, h_marks is in the rs.c layout over all `groups` (G*k data marks, then G*m parity
+ * marks); *failed (may be NULL) = groups left under-determined.  k + m <= 24. */
+int qfec_reconstruct_host(qfec_code *code, unsigned char *h_data, const unsigned char *h_parity,
+                          const unsigned char *h_marks, long long groups, int block_size, long long pitch,
+                          long long *failed);
+
 /* Rewrite every erased data shard from k survivors: the surviving data shards in
  * ascending order, then the first e surviving parity shards in ascending order
  * (module/rs.c:620-629; the same set network/NetFecCodec.cpp:504-528 hands to

@@ -16,7 +16,7 @@ EXPORTS = {
     "qfec_rs.h": ["reed_solomon_init", "reed_solomon_new", "reed_solomon_release", "reed_solomon_encode",
                   "reed_solomon_reconstruct", "reed_solomon_error"],
     "qfec.h": ["qfec_code_new", "qfec_code_from_rows", "qfec_code_free", "qfec_code_rows", "qfec_code_shape",
-               "qfec_encode", "qfec_encode_host", "qfec_reconstruct", "qfec_prepare_reconstruct", "qfec_decode_rows",
+               "qfec_encode", "qfec_encode_host", "qfec_reconstruct", "qfec_reconstruct_host", "qfec_prepare_reconstruct", "qfec_decode_rows",
                "qfec_fec_code", "qfec_rs_code", "qfec_fec_matrix", "qfec_pack_datagrams", "qfec_unpack_datagrams",
                "qfec_frame_udp", "qfec_unframe_udp", "qfec_synth_fill", "qfec_probe_stream",
                "qfec_tune", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
@@ -56,6 +56,7 @@ def lib():
         "qfec_code_shape": (i, [vp, C.POINTER(i), C.POINTER(i)]),
         "qfec_encode": (i, [vp, vp, vp, ll, i, ll, vp]),
         "qfec_encode_host": (i, [vp, vp, vp, ll, i, ll]),
+        "qfec_reconstruct_host": (i, [vp, vp, vp, vp, ll, i, ll, vp]),
         "qfec_reconstruct": (i, [vp, vp, vp, vp, ll, i, ll, vp, vp]),
         "qfec_prepare_reconstruct": (i, [vp]),
         "qfec_decode_rows": (i, [vp, vp, vp, vp, vp]),

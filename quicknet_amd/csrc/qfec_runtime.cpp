@@ -701,6 +701,85 @@ int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char
     return drain((int)((nchunks + 1) & 1));
 }
 
+int qfec_reconstruct_host(qfec_code* code, unsigned char* h_data, const unsigned char* h_parity,
+                          const unsigned char* h_marks, long long groups, int block_size, long long pitch,
+                          long long* failed) {
+    if (!code || groups < 0 || block_size < 1 || pitch < block_size ||
+        (groups > 0 && (!h_data || !h_marks || (code->m > 0 && !h_parity)))) {
+        set_error("qfec_reconstruct_host: invalid argument");
+        return QFEC_EINVAL;
+    }
+    if (failed) *failed = 0;
+    if (groups == 0) return QFEC_OK;
+    const int k = code->k, m = code->m;
+    if (k + m > QFEC_LUT_MAX_N) {
+        set_error("qfec_reconstruct_host: k + m = %d > %d (use reed_solomon_reconstruct)", k + m, QFEC_LUT_MAX_N);
+        return QFEC_EUNSUP;
+    }
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    DevTables* d = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_lut(code, ctx->device, &d);
+    }
+    if (rc) return rc;
+    // chunk slot layout, device and pinned alike: data [gc][k][pitch] | parity [gc][m][pitch]
+    // | marks [gc*k data marks][gc*m parity marks] | failed counter (8 B)
+    const size_t dg = (size_t)k * (size_t)pitch, pg = (size_t)m * (size_t)pitch;
+    long long gc = tuning().host_chunk > 0 ? tuning().host_chunk
+                                           : std::max<long long>(1, (long long)((size_t)32 << 20) / (long long)dg);
+    gc = std::min(gc, groups);
+    const size_t mk_off = (size_t)gc * (dg + pg), cnt_off = round_up(mk_off + (size_t)gc * (k + m), 16);
+    const size_t slot_bytes = cnt_off + 16;
+    std::lock_guard<std::mutex> lk(ctx->host_mu);
+    for (auto& h : ctx->host)
+        if ((rc = ensure_host_slot(h, slot_bytes, slot_bytes))) return rc;
+    long long pending[2] = {-1, -1};
+    long long nfail = 0;
+    auto drain = [&](int sl) -> int {
+        if (pending[sl] < 0) return QFEC_OK;
+        DevCtx::HostSlot& h = ctx->host[sl];
+        HIP_TRY(hipEventSynchronize(h.done));
+        const long long g0 = pending[sl] * gc, gn = std::min(gc, groups - g0);
+        memcpy(h_data + (size_t)g0 * dg, h.h_out, (size_t)gn * dg);
+        nfail += *reinterpret_cast<const unsigned*>(h.h_out + cnt_off);
+        pending[sl] = -1;
+        return QFEC_OK;
+    };
+    const long long nchunks = (groups + gc - 1) / gc;
+    for (long long i = 0; i < nchunks; ++i) {
+        const int sl = (int)(i & 1);
+        DevCtx::HostSlot& h = ctx->host[sl];
+        if ((rc = drain(sl))) return rc;
+        const long long g0 = i * gc, gn = std::min(gc, groups - g0);
+        // stage the chunk: data, parity, then its marks in rs.c layout for gn groups
+        memcpy(h.h_in, h_data + (size_t)g0 * dg, (size_t)gn * dg);
+        if (m) memcpy(h.h_in + (size_t)gn * dg, h_parity + (size_t)g0 * pg, (size_t)gn * pg);
+        uint8_t* hm = h.h_in + (size_t)gn * (dg + pg);
+        memcpy(hm, h_marks + (size_t)g0 * k, (size_t)gn * k);
+        memcpy(hm + (size_t)gn * k, h_marks + (size_t)groups * k + (size_t)g0 * m, (size_t)gn * m);
+        memset(h.h_in + cnt_off, 0, 16);
+        const size_t used = (size_t)gn * (dg + pg + k + m);
+        uint8_t* dd = h.d_buf;
+        HIP_TRY(hipMemcpyAsync(dd, h.h_in, used, hipMemcpyHostToDevice, h.stream));
+        HIP_TRY(hipMemcpyAsync(dd + cnt_off, h.h_in + cnt_off, 16, hipMemcpyHostToDevice, h.stream));
+        if ((rc = run_reconstruct(*ctx, code, d->d_lut, nullptr, d->d_rec, dd, dd + (size_t)gn * dg,
+                                  dd + (size_t)gn * (dg + pg), gn, block_size, pitch,
+                                  reinterpret_cast<unsigned*>(dd + cnt_off), h.stream)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(h.h_out, dd, (size_t)gn * dg, hipMemcpyDeviceToHost, h.stream));
+        HIP_TRY(hipMemcpyAsync(h.h_out + cnt_off, dd + cnt_off, 16, hipMemcpyDeviceToHost, h.stream));
+        HIP_TRY(hipEventRecord(h.done, h.stream));
+        pending[sl] = i;
+    }
+    if ((rc = drain((int)(nchunks & 1)))) return rc;
+    if ((rc = drain((int)((nchunks + 1) & 1)))) return rc;
+    if (failed) *failed = nfail;
+    return QFEC_OK;
+}
+
 int qfec_prepare_reconstruct(qfec_code* code) {
     if (!code) return QFEC_EINVAL;
     DevCtx* ctx = nullptr;

@@ -297,6 +297,33 @@ def test_encode_host_vs_oracle(oracle, k, m, B, chunk, pinned):
     assert np.array_equal(got[..., :B], expect)
 
 
+@pytest.mark.parametrize("k,m,B,chunk", [(10, 3, 1024, 7), (16, 4, 1400, 0), (4, 2, 37, 5)])
+def test_reconstruct_host_vs_oracle(oracle, k, m, B, chunk):
+    """qfec_reconstruct_host (host buffers, chunked over two streams) against the oracle's
+    rs.c restatement on random patterns with inconsistent parity, incl. unrecoverable groups."""
+    G = 211
+    code = qa.Code.cauchy(k, m)
+    pitch = B if B % 16 else round16(B)
+    rng = np.random.default_rng(k * 7 + B)
+    data = synth_bytes(k * 17 + B, G * k * B).reshape(G, k, B)
+    par = synth_bytes(k * 19 + B, G * m * B).reshape(G, m, B)
+    gm = np.zeros((G, k + m), np.uint8)
+    for g in range(G):
+        gm[g, rng.choice(k + m, size=int(rng.integers(0, m + 2)), replace=False)] = 1
+    marks = marks_to_rs_layout(gm, k)
+    expect = data.copy()
+    expect.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+    work = padded(expect, pitch, 0xC3)
+    oracle.rs_reconstruct(code.rows, expect, par.copy(), marks, B)
+    qa.tune("host_chunk", chunk)
+    try:
+        nf = code.reconstruct_host(work, padded(par, pitch), np.ascontiguousarray(marks), B)
+    finally:
+        qa.tune("host_chunk", 0)
+    assert np.array_equal(work[..., :B], expect)
+    assert nf == int(((gm[:, :k].sum(1) > 0) & (gm.sum(1) > m)).sum())
+
+
 def test_large_batch_roundtrip(oracle):
     """BASELINE config 2/3 shape at full size: 100 000 groups x RS(10,3) x 1 KiB.
     Encode checked byte for byte against the oracle; reconstruct with 3 random erasures
