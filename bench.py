@@ -439,6 +439,17 @@ def main():
                 cpu_mt = cpu_baseline_threads(args, args.cpu_seconds / 2, args.cpu_threads)
             except Exception as exc:
                 cpu_mt = {"value": None, "error": repr(exc)}
+        # the reference's datagram pipeline (FecCodecBuf.cpp + system/fec.c, oracle/_ref),
+        # RS(10,13) 1 KiB payloads, send + receive, 1 thread: the CPU side of DESIGN 3.5
+        ref_wire = os.path.join(ROOT, "oracle", "_ref", "ref_wire_bench")
+        if cpu is not None and os.path.exists(ref_wire):
+            import subprocess
+            try:
+                r = subprocess.run([ref_wire, "10", "13", "1024", "2000", str(args.cpu_seconds / 5)],
+                                   capture_output=True, text=True, timeout=120)
+                cpu["wire"] = json.loads(r.stdout) if r.returncode == 0 else {"error": r.stderr[-200:]}
+            except Exception as exc:
+                cpu["wire"] = {"error": repr(exc)}
 
     if rank == 0:
         out = {

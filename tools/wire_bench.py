@@ -71,14 +71,7 @@ def main():
     gib = G * k * S / float(1 << 30)
     pitch = shards.shape[2]
     wire_bytes = int(wlen.sum().item())
-    cpu = None
-    ref = os.path.join(ROOT, "oracle", "_ref", "ref_wire_bench")
-    if os.path.exists(ref) and a.cpu_seconds > 0:
-        import subprocess
-        r = subprocess.run([ref, str(k), str(n), str(S), "2000", str(a.cpu_seconds)], capture_output=True, text=True,
-                           timeout=120)
-        cpu = json.loads(r.stdout) if r.returncode == 0 else {"error": r.stderr[-200:]}
-        cpu["kind"] = "reference (network/FecCodecBuf.cpp + system/fec.c, 1 thread)"
+    cpu = None  # the reference CPU pipeline is timed by bench.py's cpu_baseline leg ("wire")
     print(json.dumps({
         "send_path": "staged" if a.staged else "fused",
         "workload": f"{G} groups x RS({k},{n}) x {S}-B payloads, checksum on, {n - k} random losses/group",
