@@ -8,15 +8,26 @@ One step = the BASELINE.json configs[1] + configs[2] workload on one batch held 
 Cauchy matrix (bit-exact with module/rs.c).  Weak scaling: every rank owns its own
 100 000 groups (distinct seeds); value = all ranks' data bytes / the slowest rank's time.
 
+Beside the headline, every rank also runs (inside barriers, max-over-ranks timing):
+  config4     RS(16,4) encode + 4-erasure reconstruct of 250 000 x 1400 B groups, split
+              contiguously over the ranks (strong scaling: the job is fixed), and
+  host_mixed  config 5: mixed (4,2)/(10,3)/(16,4) batches streamed host -> device -> host
+              through the qfec_pipe engine (pinned buffers, 3 HIP streams per GPU).
+
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+      --gpus N > 1 without WORLD_SIZE: this process starts N rank processes itself (before
+      any GPU call) and exits with the worst of their return codes.
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, the same protocol)
 
 Prints ONE JSON line (rank 0).  Data GiB/s counts payload bytes: k*B per encoded group and
 k*B per decoded group (groups with no erased data shard cost nothing, rs.c:620).
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,18 +37,21 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-import quicknet_amd as qa  # noqa: E402
-from quicknet_amd.sharding import rank_seed  # noqa: E402
-from quicknet_amd.synth import SEED_DECODE, SEED_ENCODE, erasure_marks, marks_to_rs_layout  # noqa: E402
+import quicknet_amd as qa  # noqa: E402  (libqfec.so is loaded lazily, at the first codec call)
+from quicknet_amd.sharding import rank_seed, shard_range  # noqa: E402
+from quicknet_amd.synth import SEED_DECODE, SEED_ENCODE, SEED_RS16, erasure_marks, marks_to_rs_layout  # noqa: E402
 
 METRIC = "RS(k,m) FEC encode+decode GiB/s (device-resident) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 GIB = float(1 << 30)
+# the kernel sources whose PMC traffic profiles/traffic.json holds (stale if they change)
+KERNEL_SOURCES = ("quicknet_amd/csrc/qfec_kernels.hip", "quicknet_amd/csrc/qfec_internal.hpp",
+                  "quicknet_amd/csrc/qfec_device.hpp")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); >1 without WORLD_SIZE spawns them")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--spinup-ms", type=float, default=25.0,
@@ -53,22 +67,76 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="threads for the all-cores CPU baseline (the GPU box's CPU share is 16; 0 skips it)")
-    p.add_argument("--no-side", action="store_true", help="skip the side configurations (rank 0, after the timed run)")
+    p.add_argument("--no-side", action="store_true", help="skip the rank-0 side configurations")
+    p.add_argument("--no-config4", action="store_true", help="skip the sharded RS(16,4) config 4 leg")
+    p.add_argument("--config4-groups", type=int, default=250_000, help="config 4 job size (tests shrink it)")
+    p.add_argument("--no-host", action="store_true", help="skip the host-to-host legs (config 5)")
+    p.add_argument("--protocol-check", action="store_true",
+                   help="no GPU work: run the rank launch + barrier/max/sum protocol only (CPU tests)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py), if present")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def dist_setup():
+# ---------------------------------------------------------------------------- rank launch
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """--gpus N > 1 with no WORLD_SIZE in the environment: start N fresh rank processes (this
+    process never touches the GPU: torch.cuda.device_count() does not initialise it on this
+    image) and return the worst of their exit codes.  A rank that fails ends the others."""
+    n = args.gpus
+    backend = os.environ.get("QFEC_BENCH_BACKEND", "nccl")
+    if not args.protocol_check and backend == "nccl":
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rcs = [None] * n
+    failed_at = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0) and failed_at is None:
+                    failed_at = time.time()
+        if failed_at is not None and time.time() - failed_at > 30:
+            for i, p in enumerate(procs):  # the survivors would wait on a barrier forever
+                if rcs[i] is None:
+                    p.kill()
+                    rcs[i] = p.wait()
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc != 0]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+
+
+def dist_setup(args):
     """One rank per GPU over RCCL.  QFEC_BENCH_BACKEND=gloo (rehearsal only) runs the same
     rank protocol over gloo, with ranks sharing the visible GPUs round-robin."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     backend = os.environ.get("QFEC_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
+    if args.protocol_check:
+        backend = "gloo"
+    elif backend != "nccl":
         local %= max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
+    if not args.protocol_check:
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
@@ -106,15 +174,45 @@ def all_sum(x, world):
     return _all_reduce(x, world, dist.ReduceOp.SUM)
 
 
+def all_gather_float(x, world, rank):
+    """Every rank's value of x, in rank order (a one-hot sum: one all-reduce of `world` floats)."""
+    if world == 1:
+        return [x]
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.zeros(world, dtype=torch.float64, device=dev)
+    t[rank] = x
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.cpu().tolist()]
+
+
+def protocol_check(args, rank, world):
+    """The launch + timing protocol with no GPU work (CPU tests): each rank 'works' for a
+    rank-dependent time; the line carries the same n_gpus / max-time / summed-units fields."""
+    barrier(world)
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    t1 = time.perf_counter()
+    barrier(world)
+    el = all_max(t1 - t0, world)
+    units = all_sum(float(1000 * (rank + 1)), world)
+    ranks = all_gather_float(float(os.getpid()), world, rank)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "protocol_check": True, "n_gpus": world, "gpus_arg": args.gpus,
+                          "elapsed_max_s": el, "units": units, "distinct_rank_pids": len(set(ranks))}), flush=True)
+    return 0
+
+
+# ---------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(args, budget_s):
     """The reference's own rs.c (oracle/_ref, kind 'reference') -- or the CPU restatement
     (oracle/liboracle.so, kind 'port') when _ref is absent -- on a bounded sample of the same
     workload: encode + 3-erasure reconstruct of `sample` groups, 1 thread, repeated until the
     budget is spent."""
     from oracle.oracle import Oracle, RefCodec
+    from quicknet_amd.synth import synth_bytes
     k, m, B = args.k, args.m, args.block
     sample = 10_000
-    from quicknet_amd.synth import synth_bytes
     data = synth_bytes(SEED_ENCODE, sample * k * B).reshape(sample, k, B)
     par = np.zeros((sample, m, B), np.uint8)
     gm = erasure_marks(SEED_DECODE, sample, k + m, args.erasures)
@@ -149,9 +247,21 @@ def cpu_baseline(args, budget_s):
         if el >= budget_s:
             break
     gib = reps * (sample + dec_groups) * k * B / GIB
-    return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+    return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": 1, "kind": kind, "cpu_model": cpu_model(),
             "sample": f"{reps} x (encode {sample} groups + reconstruct {dec_groups} groups with {args.erasures} "
                       f"random erasures/group), RS({k},{m}) B={B}, {el:.1f} s, 1 thread"}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
 
 def cpu_baseline_threads(args, budget_s, threads):
     """The same reference rs.c sample on `threads` host threads: groups split into contiguous
@@ -161,7 +271,6 @@ def cpu_baseline_threads(args, budget_s, threads):
     reed_solomon_init (its tables are read-only, the decode matrix lives on the stack)."""
     import threading
     from oracle.oracle import RefCodec
-    from quicknet_amd.sharding import shard_range
     from quicknet_amd.synth import synth_bytes
     if not RefCodec.available() or args.flavour != "cauchy":
         return None
@@ -208,43 +317,84 @@ def cpu_baseline_threads(args, budget_s, threads):
                       f"{args.erasures} random erasures/group), RS({k},{m}) B={B}, {el:.1f} s, {len(slices)} threads"}
 
 
-# BASELINE configs measured beside the headline line (rank 0's GPU, after the timed region):
-# the Vandermonde flavour the network stack links (module/fec.c) at configs[1]+[2], config 4's
-# RS(16,4) on 1400-B MTU packets, and config 5's RS(4,2)
-SIDE = (("vandermonde", 10, 3, 1024, 100_000, 3), ("cauchy", 16, 4, 1400, 250_000, 4),
-        ("cauchy", 4, 2, 1024, 100_000, 2))
+def cpu_config0(budget_s):
+    """BASELINE configs[0] literally: RS(10,3) encode of 10 000 x 1 KiB packets (1 000 groups)
+    through the reference's own per-packet fec.c, as network/FecCodec.cpp drives it
+    (fec_new(10, 13), then fec_encode(.., 10 + j, 1024) for j < 3 per group,
+    FecCodecBuf.cpp:151), 1 thread, repeated until the budget is spent."""
+    import ctypes as C
+    from oracle.oracle import RefCodec
+    from quicknet_amd.synth import SEED_CPU_ENCODE, synth_bytes
+    if not RefCodec.available():
+        return None
+    ref = RefCodec()
+    k, n, B, G = 10, 13, 1024, 1000
+    data = synth_bytes(SEED_CPU_ENCODE, G * k * B).reshape(G, k, B)
+    out = np.zeros((G, n - k, B), np.uint8)
+    code = ref.fec.fec_new(k, n)
+    srcs = [(C.c_void_p * k)(*[data[g, i].ctypes.data for i in range(k)]) for g in range(G)]
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        for g in range(G):
+            for j in range(n - k):
+                ref.fec.fec_encode(code, srcs[g], C.c_void_p(out[g, j].ctypes.data), k + j, B)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    ref.fec.fec_free(code)
+    return {"value": round(reps * G * k * B / el / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "reference",
+            "sample": f"{reps} x {G * k} packets, RS(10,3) fec_encode per parity packet (system/fec.c), {el:.1f} s"}
 
 
-def side_config(flavour, k, m, B, G, E, world, rank, steps=20, warmup=5, spinup_ms=25.0):
-    """One encode + reconstruct step on G groups (G = the config's total / world ranks for
-    config 4, which BASELINE shards over the GPUs), device-resident, pitch = B rounded up to
-    16 B (bytes counted at B); per-kernel HIP events; reconstruct must restore the data."""
-    dev = torch.device("cuda", torch.cuda.current_device())
+# ---------------------------------------------------------------------------- GPU legs
+# rank 0's side configurations (after the timed region): the Vandermonde flavour the network
+# stack links (module/fec.c) at configs[1]+[2], and config 5's RS(4,2) shape device-resident
+SIDE = (("vandermonde", 10, 3, 1024, 100_000, 3), ("cauchy", 4, 2, 1024, 100_000, 2))
+
+
+def _make_batch(flavour, k, m, B, G, E, seed_data, marks_gm, dev):
     n, pitch = k + m, (B + 15) // 16 * 16
     code = qa.Code.cauchy(k, m) if flavour == "cauchy" else qa.Code.vandermonde(k, m)
     data = torch.empty((G, k, pitch), dtype=torch.uint8, device=dev)
-    qa.synth_fill(data, rank_seed(SEED_ENCODE ^ (k << 8 | m), rank))
+    qa.synth_fill(data, seed_data)
     parity = torch.empty((G, m, pitch), dtype=torch.uint8, device=dev)
-    gm = erasure_marks(rank_seed(SEED_DECODE ^ (k << 8 | m), rank), G, n, E)
+    gm = marks_gm
     marks = torch.from_numpy(marks_to_rs_layout(gm, k)).to(dev)
-    dec_groups = int((gm[:, :k].sum(1) > 0).sum())
-    erased = int(gm[:, :k].sum())
     work = data.clone()
     work[torch.from_numpy(gm[:, :k].astype(bool)).to(dev)] = 0x5A
     code.encode(data, parity, B)
     code.prepare_reconstruct()
-    s = torch.cuda.current_stream()
-    # the main line's spin-up: the host-side setup above leaves the GPU idle long enough
-    # for its clocks to drop, and the first ~20 steps after that run slow
+    return code, data, parity, marks, work
+
+
+def _spin(step, spinup_ms):
     t_spin = time.perf_counter()
     while (time.perf_counter() - t_spin) * 1e3 < spinup_ms:
         for _ in range(5):
-            code.encode(data, parity, B)
-            code.reconstruct(work, parity, marks, B)
+            step()
         torch.cuda.synchronize()
-    for _ in range(warmup):
+
+
+def side_config(flavour, k, m, B, G, E, rank, steps=20, warmup=5, spinup_ms=25.0):
+    """One encode + reconstruct step on G groups, device-resident, pitch = B rounded up to
+    16 B (bytes counted at B); per-kernel HIP events; reconstruct must restore the data."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    gm = erasure_marks(rank_seed(SEED_DECODE ^ (k << 8 | m), rank), G, k + m, E)
+    code, data, parity, marks, work = _make_batch(flavour, k, m, B, G, E, rank_seed(SEED_ENCODE ^ (k << 8 | m), rank),
+                                                  gm, dev)
+    dec_groups = int((gm[:, :k].sum(1) > 0).sum())
+    erased = int(gm[:, :k].sum())
+    s = torch.cuda.current_stream()
+
+    def step():
         code.encode(data, parity, B)
         code.reconstruct(work, parity, marks, B)
+
+    _spin(step, spinup_ms)
+    for _ in range(warmup):
+        step()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     for e in evs:
         for x in e:
@@ -275,18 +425,111 @@ def side_config(flavour, k, m, B, G, E, world, rank, steps=20, warmup=5, spinup_
     return out
 
 
+CONFIG4 = dict(k=16, m=4, B=1400, E=4)
+
+
+def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=25.0):
+    """BASELINE configs[3]: RS(16,4) encode + decode of 4 000 000 x 1400 B packets = 250 000
+    groups, split contiguously over the ranks (quicknet_amd.sharding.shard_range; groups are
+    independent, rs.c:582-586, so there is no collective).  Erasures: 4 of 20 per group drawn
+    over the whole job (seed 0x5EED0004), so every rank decodes its slice of the same pattern
+    list at any N.  Timed on every rank between barriers; value = all ranks' data bytes /
+    the slowest rank's time."""
+    k, m, B, E = CONFIG4["k"], CONFIG4["m"], CONFIG4["B"], CONFIG4["E"]
+    Gt = groups
+    a, b = shard_range(Gt, rank, world)
+    G = b - a
+    dev = torch.device("cuda", torch.cuda.current_device())
+    gm = erasure_marks(SEED_RS16, Gt, k + m, E)[a:b]
+    code, data, parity, marks, work = _make_batch("cauchy", k, m, B, G, E, rank_seed(SEED_RS16, rank), gm, dev)
+    dec_groups = int((gm[:, :k].sum(1) > 0).sum())
+    erased = int(gm[:, :k].sum())
+    s = torch.cuda.current_stream()
+
+    def step():
+        code.encode(data, parity, B)
+        code.reconstruct(work, parity, marks, B)
+
+    _spin(step, spinup_ms)
+    for _ in range(warmup):
+        step()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in evs:
+        for x in e:
+            x.record(s)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in evs:
+        e[0].record(s)
+        code.encode(data, parity, B)
+        e[1].record(s)
+        code.reconstruct(work, parity, marks, B)
+        e[2].record(s)
+    torch.cuda.synchronize()
+    barrier(world)
+    el_rank = time.perf_counter() - t0
+    el = all_max(el_rank, world)
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    ok = bool(torch.equal(work[..., :B], data[..., :B]))
+    ok = all_sum(0.0 if ok else 1.0, world) == 0.0
+    bytes_rank = (G + dec_groups) * k * B * steps
+    total = all_sum(float(bytes_rank), world)
+    per_rank_ms = all_gather_float(el_rank / steps * 1e3, world, rank)
+    enc_alg, dec_alg = (k + m) * B * G, (k * dec_groups + erased) * B
+    out = {"config": f"RS({k},{m}) cauchy, {Gt:,} groups x {B} B ({Gt * k:,} packets) split over {world} rank(s), "
+                     f"{E} random erasures/group (BASELINE configs[3])",
+           "value": round(total / el / GIB, 2), "unit": "GiB/s", "scaling": "strong",
+           "ms_per_step": round(el / steps * 1e3, 4), "per_rank_ms": [round(x, 4) for x in per_rank_ms],
+           "groups_per_rank": [shard_range(Gt, r, world)[1] - shard_range(Gt, r, world)[0] for r in range(world)],
+           "rank0_encode_frac": round(enc_alg / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "rank0_reconstruct_frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "rank0_encode_avg_ms": round(enc_ms, 4), "rank0_reconstruct_avg_ms": round(dec_ms, 4),
+           "verified": ok}
+    del data, parity, work, marks
+    torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic(path, workload_key):
+    """PMC bytes per launch for this workload from profiles/traffic.json, or None when absent
+    or measured on other kernel sources (the file records their sha256)."""
     try:
         with open(path) as f:
             t = json.load(f)
-        return t.get(workload_key)
     except (OSError, ValueError):
-        return None
+        return None, "absent"
+    ent = t.get(workload_key)
+    if not isinstance(ent, dict):
+        return None, "no entry for this workload"
+    want = kernel_sources_hash()
+    if ent.get("kernel_sources_sha256") != want:
+        return None, f"stale: measured on kernel sources {ent.get('kernel_sources_sha256')}, now {want}"
+    return ent, f"{os.path.relpath(path, ROOT)} ({ent.get('run', 'PMC run')}, kernel sources {want})"
 
 
-def main():
-    args = parse()
-    rank, world, local = dist_setup()
+def kernel_sources_hash():
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
+    rank, world, local = dist_setup(args)
+    if args.protocol_check:
+        rc = protocol_check(args, rank, world)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return rc
     qa.set_kernel_variant(args.variant)
     dev = torch.device("cuda", local)
     k, m, B, G, E = args.k, args.m, args.block, args.groups, args.erasures
@@ -320,11 +563,7 @@ def main():
     # setup, untimed: a fresh GPU runs the first ~20 steps (~10 ms) 5-8 % slower while its
     # clocks leave the idle state (profiles/r01t_sustain.txt); spin it up before the W
     # warmup steps so the timed region sees the steady state whatever W the caller picks
-    t_spin = time.perf_counter()
-    while (time.perf_counter() - t_spin) * 1e3 < args.spinup_ms:
-        for _ in range(5):
-            step()
-        torch.cuda.synchronize()
+    _spin(step, args.spinup_ms)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -343,6 +582,7 @@ def main():
     barrier(world)
     t1 = time.perf_counter()
     el = all_max(t1 - t0, world)
+    per_rank_ms = all_gather_float((t1 - t0) / args.steps * 1e3, world, rank)
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
 
@@ -358,13 +598,13 @@ def main():
     dec_alg = (k * dec_groups + erased_data) * B   # read k survivors, write e erased
     enc_gbs = enc_alg / (enc_ms * 1e-3) / 1e9
     dec_gbs = dec_alg / (dec_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.traffic, f"rs{k}_{m}_b{B}_g{G}")
+    traffic, traffic_src = load_traffic(args.traffic, f"rs{k}_{m}_b{B}_g{G}")
 
     def roof(kernel, ach, alg, ms, tkey):
         tr = traffic.get(tkey) if isinstance(traffic, dict) else None
         return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr, "kernel": kernel,
-                "algorithmic_bytes": alg, "avg_ms": round(ms, 4),
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr, "traffic_source": traffic_src,
+                "kernel": kernel, "algorithmic_bytes": alg, "avg_ms": round(ms, 4),
                 "read_frac": round((alg - (m * B * G if kernel == "encode" else erased_data * B)) / (ms * 1e-3) / 1e9
                                    / HBM_PEAK_GBS, 4)}
 
@@ -373,7 +613,7 @@ def main():
     dominant, other = (r_enc, r_dec) if enc_ms >= dec_ms else (r_dec, r_enc)
 
     # calibration probe: the encode's traffic with XOR only (not a codec)
-    probe_ms = copy_gbs = host_line = None
+    probe_ms = copy_gbs = None
     if rank == 0:
         pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         scratch = torch.empty_like(parity)
@@ -401,31 +641,29 @@ def main():
         torch.cuda.synchronize()
         copy_gbs = 2 * data.numel() / (pe0.elapsed_time(pe1) / 10 * 1e-3) / 1e9
         del cdst
-        # host-inclusive encode (the path starts and ends in host memory): qfec_encode_host
-        # over the same batch from pinned host buffers, best of 3, parity verified
-        try:
-            h_data = data.cpu().pin_memory()
-            h_par = torch.empty(parity.shape, dtype=torch.uint8).pin_memory()
-            ts = []
-            for _ in range(4):
-                t_h = time.perf_counter()
-                code.encode_host(h_data, h_par, B)
-                ts.append(time.perf_counter() - t_h)
-            host_gibs = G * k * B / min(ts[1:]) / GIB
-            host_ok = bool(torch.equal(h_par, parity.cpu()))
-            host_line = {"value": round(host_gibs, 2), "unit": "GiB/s", "verified": host_ok,
-                         "what": "qfec_encode_host, pinned host buffers, H2D + encode + D2H chunked over 2 streams"}
-            del h_data, h_par
-        except Exception as exc:  # report, never fake
-            host_line = {"value": None, "error": repr(exc)}
+    del work, marks
+    torch.cuda.empty_cache()
+
+    # BASELINE configs[3] on every rank (strong scaling over the ranks)
+    config4 = None
+    if not args.no_config4:
+        config4 = config4_sharded(rank, world, args.config4_groups)
+        ok = ok and config4["verified"]
+
+    # BASELINE configs[4] (host -> device -> host) on every rank, and the single-shape
+    # host-inclusive encode on rank 0; both verified byte for byte
+    host_mixed = host_line = None
+    if not args.no_host:
+        from quicknet_amd.hoststream import host_encode_leg, host_mixed_leg
+        host_mixed = host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather_float)
+        ok = ok and bool(host_mixed.get("verified"))
+        if rank == 0:
+            host_line = host_encode_leg(code, data, parity, B)
+            ok = ok and bool(host_line.get("verified"))
 
     side = None
     if rank == 0 and not args.no_side:
-        side = []
-        for fl, sk, sm, sB, sG, sE in SIDE:
-            if sB == 1400:  # config 4 shards its 250 000 groups over the GPUs
-                sG = (sG + world - 1) // world
-            side.append(side_config(fl, sk, sm, sB, sG, sE, world, rank))
+        side = [side_config(fl, sk, sm, sB, sG, sE, rank) for fl, sk, sm, sB, sG, sE in SIDE]
         ok = ok and all(x["verified"] for x in side)
 
     cpu = cpu_mt = None
@@ -439,11 +677,14 @@ def main():
                 cpu_mt = cpu_baseline_threads(args, args.cpu_seconds / 2, args.cpu_threads)
             except Exception as exc:
                 cpu_mt = {"value": None, "error": repr(exc)}
+        try:
+            cpu["config0"] = cpu_config0(args.cpu_seconds / 5)
+        except Exception as exc:
+            cpu["config0"] = {"error": repr(exc)}
         # the reference's datagram pipeline (FecCodecBuf.cpp + system/fec.c, oracle/_ref),
         # RS(10,13) 1 KiB payloads, send + receive, 1 thread: the CPU side of DESIGN 3.5
         ref_wire = os.path.join(ROOT, "oracle", "_ref", "ref_wire_bench")
         if cpu is not None and os.path.exists(ref_wire):
-            import subprocess
             try:
                 r = subprocess.run([ref_wire, "10", "13", "1024", "2000", str(args.cpu_seconds / 5)],
                                    capture_output=True, text=True, timeout=120)
@@ -460,6 +701,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 4),
+            "per_rank_ms": [round(x, 4) for x in per_rank_ms],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -479,6 +721,8 @@ def main():
             "roofline_other": other,
             "probe_stream_gbs": round(enc_alg / (probe_ms * 1e-3) / 1e9, 1) if probe_ms else None,
             "copy_d2d_gbs": round(copy_gbs, 1) if copy_gbs else None,
+            "config4": config4,
+            "host_to_host_mixed": host_mixed,
             "host_to_host_encode": host_line,
             "verified": ok,
             "cpu_baseline": cpu,

@@ -75,6 +75,29 @@ int qfec_reconstruct_host(qfec_code *code, unsigned char *h_data, const unsigned
                           const unsigned char *h_marks, long long groups, int block_size, long long pitch,
                           long long *failed);
 
+/* ---- host streaming pipe (BASELINE config 5: mixed (k,m) batches host -> device -> host) ----
+ * A pipe owns `nstreams` slots per device (HIP stream + event + `slot_bytes` of device
+ * staging), over the listed devices (devices = NULL / ndev = 0: every visible device;
+ * a device may be listed more than once).  qfec_pipe_encode / qfec_pipe_reconstruct split a
+ * batch into pieces that fit a slot and spread over all slots; each piece takes the next
+ * slot round-robin (devices interleaved), waits for that slot's previous piece, and queues
+ * H2D -> kernel -> D2H on its stream, so the copies of one piece overlap the kernels and
+ * copies of the others.  They return once the pieces are queued.  Host buffers must be
+ * PINNED (hipHostMalloc'd or hipHostRegister'ed; DMA'd directly) and must not be touched
+ * until qfec_pipe_wait returns.  Layouts as qfec_encode / qfec_reconstruct_host (marks in
+ * the rs.c layout over the batch's `groups`).  Any number of codes may share a pipe.
+ * qfec_pipe_wait: every queued piece has finished; *failed (may be NULL) = under-determined
+ * groups since the previous wait.  On an error return the pipe has been drained. */
+typedef struct qfec_pipe qfec_pipe;
+qfec_pipe *qfec_pipe_new(const int *devices, int ndev, int nstreams, long long slot_bytes);
+void qfec_pipe_free(qfec_pipe *pipe);
+int qfec_pipe_encode(qfec_pipe *pipe, qfec_code *code, const unsigned char *h_data, unsigned char *h_parity,
+                     long long groups, int block_size, long long pitch);
+int qfec_pipe_reconstruct(qfec_pipe *pipe, qfec_code *code, unsigned char *h_data, const unsigned char *h_parity,
+                          const unsigned char *h_marks, long long groups, int block_size, long long pitch);
+int qfec_pipe_wait(qfec_pipe *pipe, long long *failed);
+int qfec_pipe_slots(const qfec_pipe *pipe);
+
 /* Rewrite every erased data shard from k survivors: the surviving data shards in
  * ascending order, then the first e surviving parity shards in ascending order
  * (module/rs.c:620-629; the same set network/NetFecCodec.cpp:504-528 hands to

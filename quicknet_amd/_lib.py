@@ -17,6 +17,7 @@ EXPORTS = {
                   "reed_solomon_reconstruct", "reed_solomon_error"],
     "qfec.h": ["qfec_code_new", "qfec_code_from_rows", "qfec_code_free", "qfec_code_rows", "qfec_code_shape",
                "qfec_encode", "qfec_encode_host", "qfec_reconstruct", "qfec_reconstruct_host", "qfec_prepare_reconstruct", "qfec_decode_rows",
+               "qfec_pipe_new", "qfec_pipe_free", "qfec_pipe_encode", "qfec_pipe_reconstruct", "qfec_pipe_wait", "qfec_pipe_slots",
                "qfec_fec_code", "qfec_rs_code", "qfec_fec_matrix", "qfec_pack_datagrams", "qfec_unpack_datagrams",
                "qfec_frame_udp", "qfec_unframe_udp", "qfec_synth_fill", "qfec_probe_stream",
                "qfec_tune", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
@@ -59,6 +60,12 @@ def lib():
         "qfec_reconstruct_host": (i, [vp, vp, vp, vp, ll, i, ll, vp]),
         "qfec_reconstruct": (i, [vp, vp, vp, vp, ll, i, ll, vp, vp]),
         "qfec_prepare_reconstruct": (i, [vp]),
+        "qfec_pipe_new": (vp, [vp, i, i, ll]),
+        "qfec_pipe_free": (None, [vp]),
+        "qfec_pipe_encode": (i, [vp, vp, vp, vp, ll, i, ll]),
+        "qfec_pipe_reconstruct": (i, [vp, vp, vp, vp, vp, ll, i, ll]),
+        "qfec_pipe_wait": (i, [vp, C.POINTER(ll)]),
+        "qfec_pipe_slots": (i, [vp]),
         "qfec_decode_rows": (i, [vp, vp, vp, vp, vp]),
         "qfec_fec_code": (vp, [vp]),
         "qfec_rs_code": (vp, [vp]),

@@ -18,7 +18,7 @@ from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
 
 __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
            "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count", "frame_udp", "unframe_udp",
-           "NetFec"]
+           "NetFec", "Pipe"]
 
 
 def _stream_handle(stream):
@@ -32,13 +32,28 @@ def _stream_handle(stream):
     return C.c_void_p(stream.cuda_stream)
 
 
-def _dev_ptr(t):
+_U8, _I32, _I64 = "u8", "i32", "i64"
+
+
+def _dev_ptr(t, kind=_U8, what="tensor"):
+    """Device pointer of a contiguous tensor on the CURRENT device (the C side launches on the
+    calling thread's current device and stream), with the element type the ABI reads:
+    u8 = torch.uint8 bytes, i32 = 4-byte integers (int32 / uint32), i64 = int64."""
     if t is None:
         return None
-    if not t.is_cuda:
-        raise QfecError("expected a device tensor")
+    if not getattr(t, "is_cuda", False):
+        raise QfecError(f"{what}: expected a device tensor")
     if not t.is_contiguous():
-        raise QfecError("expected a contiguous tensor")
+        raise QfecError(f"{what}: expected a contiguous tensor")
+    import torch
+    ok = {_U8: t.dtype == torch.uint8,
+          _I32: t.dtype in (torch.int32, getattr(torch, "uint32", torch.int32)),
+          _I64: t.dtype == torch.int64}[kind]
+    if not ok:
+        raise QfecError(f"{what}: dtype {t.dtype} where the ABI reads {kind}")
+    if t.device.index != torch.cuda.current_device():
+        raise QfecError(f"{what}: on {t.device} but the current device is cuda:{torch.cuda.current_device()} "
+                        "(use `with torch.cuda.device(...)`)")
     return C.c_void_p(t.data_ptr())
 
 
@@ -57,7 +72,7 @@ def tune(key, value):
 
 def synth_fill(t, seed, stream=None):
     """Fill a device uint8 tensor with quicknet_amd.synth.synth_bytes(seed, t.numel())."""
-    check(lib().qfec_synth_fill(_dev_ptr(t), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(stream)),
+    check(lib().qfec_synth_fill(_dev_ptr(t, what="synth_fill"), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(stream)),
           "qfec_synth_fill")
 
 
@@ -65,7 +80,7 @@ def probe_stream(data, parity, block_size, stream=None):
     """Calibration only: the encode's traffic with XOR in place of GF arithmetic."""
     G, k, pitch = data.shape
     m = parity.shape[1]
-    check(lib().qfec_probe_stream(_dev_ptr(data), _dev_ptr(parity), G, k, m, block_size, pitch,
+    check(lib().qfec_probe_stream(_dev_ptr(data, what="data"), _dev_ptr(parity, what="parity"), G, k, m, block_size, pitch,
                                   _stream_handle(stream)), "qfec_probe_stream")
 
 
@@ -82,9 +97,11 @@ def frame_udp(rows, lengths, masks, gmask=0, cmd=0x11, protocol=0xFF, conv_hid=N
         out_pitch = (pitch + P + 15) // 16 * 16
     out = torch.empty((R, out_pitch), dtype=torch.uint8, device=rows.device)
     out_len = torch.empty(R, dtype=torch.int32, device=rows.device)
-    check(lib().qfec_frame_udp(_dev_ptr(rows), pitch, _dev_ptr(lengths), R, _dev_ptr(masks),
-                               _dev_ptr(conv_hid) if conv_hid is not None else None, int(gmask), int(cmd), int(protocol),
-                               _dev_ptr(out), out_pitch, _dev_ptr(out_len), _stream_handle(stream)), "qfec_frame_udp")
+    check(lib().qfec_frame_udp(_dev_ptr(rows, what="rows"), pitch, _dev_ptr(lengths, _I32, "lengths"), R,
+                               _dev_ptr(masks, what="masks"),
+                               _dev_ptr(conv_hid, _I32, "conv_hid") if conv_hid is not None else None, int(gmask), int(cmd),
+                               int(protocol), _dev_ptr(out), out_pitch, _dev_ptr(out_len, _I32), _stream_handle(stream)),
+          "qfec_frame_udp")
     return out, out_len
 
 
@@ -101,9 +118,10 @@ def unframe_udp(frames, lengths, gmask=0, session=False, out_pitch=None, stream=
     status = torch.empty(R, dtype=torch.int32, device=dev)
     info = torch.empty((R, 4), dtype=torch.uint8, device=dev)
     ch = torch.zeros((R, 2), dtype=torch.int32, device=dev) if session else None
-    check(lib().qfec_unframe_udp(_dev_ptr(frames), pitch, _dev_ptr(lengths), R, int(gmask), int(bool(session)),
-                                 _dev_ptr(out), out_pitch, _dev_ptr(out_len), _dev_ptr(status), _dev_ptr(info),
-                                 _dev_ptr(ch) if ch is not None else None, _stream_handle(stream)), "qfec_unframe_udp")
+    check(lib().qfec_unframe_udp(_dev_ptr(frames, what="frames"), pitch, _dev_ptr(lengths, _I32, "lengths"), R, int(gmask),
+                                 int(bool(session)), _dev_ptr(out), out_pitch, _dev_ptr(out_len, _I32),
+                                 _dev_ptr(status, _I32), _dev_ptr(info),
+                                 _dev_ptr(ch, _I32) if ch is not None else None, _stream_handle(stream)), "qfec_unframe_udp")
     return out, out_len, status, info, ch
 
 
@@ -187,7 +205,7 @@ class Code:
         if k != self.k or parity.shape[0] != G or parity.shape[1] != self.m or parity.shape[2] != pitch:
             raise QfecError(f"shape mismatch: data {tuple(data.shape)} parity {tuple(parity.shape)} for ({self.k},{self.m})")
         block_size = pitch if block_size is None else block_size
-        check(lib().qfec_encode(self._h, _dev_ptr(data), _dev_ptr(parity), G, block_size, pitch,
+        check(lib().qfec_encode(self._h, _dev_ptr(data, what="data"), _dev_ptr(parity, what="parity"), G, block_size, pitch,
                                 _stream_handle(stream)), "qfec_encode")
 
     def prepare_reconstruct(self):
@@ -200,8 +218,9 @@ class Code:
         if k != self.k or parity.shape[0] != G or parity.shape[1] != self.m or marks.numel() != G * (self.k + self.m):
             raise QfecError("shape mismatch")
         block_size = pitch if block_size is None else block_size
-        check(lib().qfec_reconstruct(self._h, _dev_ptr(data), _dev_ptr(parity), _dev_ptr(marks), G, block_size,
-                                     pitch, _dev_ptr(failed), _stream_handle(stream)), "qfec_reconstruct")
+        check(lib().qfec_reconstruct(self._h, _dev_ptr(data, what="data"), _dev_ptr(parity, what="parity"),
+                                     _dev_ptr(marks, what="marks"), G, block_size, pitch,
+                                     _dev_ptr(failed, _I32, "failed"), _stream_handle(stream)), "qfec_reconstruct")
 
     # -- FEC datagram batches (network/FecCodecBuf.cpp wire format); n = k + m <= 15
     def pack_datagrams(self, payload, offsets, sizes, seq, checksum=True, shard_pitch=None, wire_pitch=None,
@@ -221,9 +240,10 @@ class Code:
         shards = torch.empty((G, n, shard_pitch), dtype=torch.uint8, device=dev)
         wire = torch.empty((G, n, wire_pitch), dtype=torch.uint8, device=dev)
         wire_len = torch.empty((G, n), dtype=torch.int32, device=dev)
-        check(lib().qfec_pack_datagrams(self._h, _dev_ptr(payload), _dev_ptr(offsets), _dev_ptr(sizes), _dev_ptr(seq),
+        check(lib().qfec_pack_datagrams(self._h, _dev_ptr(payload, what="payload"), _dev_ptr(offsets, _I64, "offsets"),
+                                        _dev_ptr(sizes, _I32, "sizes"), _dev_ptr(seq, _I32, "seq"),
                                         G, int(bool(checksum)), _dev_ptr(shards), shard_pitch, _dev_ptr(wire),
-                                        wire_pitch, _dev_ptr(wire_len), _stream_handle(stream)), "qfec_pack_datagrams")
+                                        wire_pitch, _dev_ptr(wire_len, _I32), _stream_handle(stream)), "qfec_pack_datagrams")
         return shards, wire, wire_len
 
     def unpack_datagrams(self, wire, wire_len, checksum=True, dec_pkt_size=2068, shard_pitch=None, stream=None):
@@ -239,9 +259,10 @@ class Code:
         rx = torch.empty((G, n), dtype=torch.int32, device=dev)
         status = torch.empty((G, self.k), dtype=torch.int32, device=dev)
         psize = torch.empty((G, self.k), dtype=torch.int32, device=dev)
-        check(lib().qfec_unpack_datagrams(self._h, _dev_ptr(wire), wire_pitch, _dev_ptr(wire_len), G, int(bool(checksum)),
-                                          dec_pkt_size, _dev_ptr(shards), shard_pitch, _dev_ptr(marks), _dev_ptr(rx),
-                                          _dev_ptr(status), _dev_ptr(psize), _stream_handle(stream)),
+        check(lib().qfec_unpack_datagrams(self._h, _dev_ptr(wire, what="wire"), wire_pitch,
+                                          _dev_ptr(wire_len, _I32, "wire_len"), G, int(bool(checksum)),
+                                          dec_pkt_size, _dev_ptr(shards), shard_pitch, _dev_ptr(marks), _dev_ptr(rx, _I32),
+                                          _dev_ptr(status, _I32), _dev_ptr(psize, _I32), _stream_handle(stream)),
               "qfec_unpack_datagrams")
         return shards, status, psize, rx
 
@@ -434,3 +455,72 @@ class NetFec:
         keys = ["groups_packed", "datagrams_out", "groups_unpacked", "delivered", "recovered", "undecodable",
                 "foreign", "late"]
         return dict(zip(keys, list(a)))
+
+
+def _host_ptr(a, what):
+    """Address of a contiguous uint8 host buffer (numpy array or CPU tensor)."""
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"] or a.dtype != np.uint8:
+            raise QfecError(f"{what}: contiguous uint8 host array required")
+        return C.c_void_p(a.ctypes.data)
+    import torch
+    if a.is_cuda or not a.is_contiguous() or a.dtype != torch.uint8:
+        raise QfecError(f"{what}: contiguous uint8 host tensor required")
+    return C.c_void_p(a.data_ptr())
+
+
+class Pipe:
+    """include/qfec.h qfec_pipe: batches streamed host -> device -> host over `streams` HIP
+    streams per device on `devices` (None: every visible device), each stream slot holding
+    `slot_bytes` of device staging.  encode / reconstruct queue a batch and return; wait()
+    blocks until every queued batch is done and returns the under-determined group count.
+    Buffers must be PINNED host memory (torch .pin_memory() tensors or hipHostMalloc'd) and
+    are kept referenced here until wait()."""
+
+    def __init__(self, devices=None, streams=3, slot_bytes=96 << 20):
+        devs = list(devices) if devices else []
+        arr = (C.c_int * len(devs))(*devs) if devs else None
+        h = lib().qfec_pipe_new(arr, len(devs), streams, slot_bytes)
+        if not h:
+            raise QfecError(f"qfec_pipe_new: {lib().qfec_last_error().decode()}")
+        self._h = C.c_void_p(h)
+        self.slots = lib().qfec_pipe_slots(self._h)
+        self._held = []
+
+    def close(self):
+        if self._h:
+            lib().qfec_pipe_free(self._h)
+            self._h = None
+            self._held = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode(self, code, data, parity, block_size=None):
+        G, k, pitch = data.shape
+        if k != code.k or tuple(parity.shape) != (G, code.m, pitch):
+            raise QfecError("pipe encode: shape mismatch")
+        block_size = pitch if block_size is None else block_size
+        check(lib().qfec_pipe_encode(self._h, code._h, _host_ptr(data, "data"), _host_ptr(parity, "parity"), G,
+                                     block_size, pitch), "qfec_pipe_encode")
+        self._held += [code, data, parity]
+
+    def reconstruct(self, code, data, parity, marks, block_size=None):
+        G, k, pitch = data.shape
+        nmarks = marks.size if isinstance(marks, np.ndarray) else marks.numel()
+        if k != code.k or tuple(parity.shape) != (G, code.m, pitch) or nmarks != G * (code.k + code.m):
+            raise QfecError("pipe reconstruct: shape mismatch")
+        block_size = pitch if block_size is None else block_size
+        check(lib().qfec_pipe_reconstruct(self._h, code._h, _host_ptr(data, "data"), _host_ptr(parity, "parity"),
+                                          _host_ptr(marks, "marks"), G, block_size, pitch), "qfec_pipe_reconstruct")
+        self._held += [code, data, parity, marks]
+
+    def wait(self):
+        nf = C.c_longlong(0)
+        rc = lib().qfec_pipe_wait(self._h, C.byref(nf))
+        self._held = []
+        check(rc, "qfec_pipe_wait")
+        return int(nf.value)

@@ -220,6 +220,14 @@ int ensure_host_slot(DevCtx::HostSlot& h, size_t in_bytes, size_t out_bytes) {
     return QFEC_OK;
 }
 
+// after an error in the host-buffer pipelines: wait for whatever the slots still have in
+// flight, so no DMA writes into caller memory after the call has returned
+void quiesce_host_slots(DevCtx& c) {
+    for (auto& h : c.host)
+        if (h.stream) (void)hipStreamSynchronize(h.stream);
+    (void)hipGetLastError();
+}
+
 }  // namespace
 
 // ====================================================================== code objects
@@ -678,10 +686,11 @@ int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char
         return QFEC_OK;
     };
     const long long nchunks = (groups + gc - 1) / gc;
-    for (long long i = 0; i < nchunks; ++i) {
+    auto chunk = [&](long long i) -> int {
         const int sl = (int)(i & 1);
         DevCtx::HostSlot& h = ctx->host[sl];
-        if ((rc = drain(sl))) return rc;  // the slot's previous chunk: copies done, parity out
+        int r = drain(sl);  // the slot's previous chunk: copies done, parity out
+        if (r) return r;
         const long long g0 = i * gc, gn = std::min(gc, groups - g0);
         const unsigned char* src = h_data + (size_t)g0 * in_g;
         if (!pin_in) {  // pageable: through pinned staging, overlapping the other slot's work
@@ -691,14 +700,18 @@ int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char
         uint8_t* d_in = h.d_buf;
         uint8_t* d_out = h.d_buf + (size_t)gc * in_g;
         HIP_TRY(hipMemcpyAsync(d_in, src, (size_t)gn * in_g, hipMemcpyHostToDevice, h.stream));
-        if ((rc = run_encode(*ctx, code, tab, m, d_in, d_out, gn, block_size, pitch, h.stream))) return rc;
+        if ((r = run_encode(*ctx, code, tab, m, d_in, d_out, gn, block_size, pitch, h.stream))) return r;
         unsigned char* dst = pin_out ? h_parity + (size_t)g0 * out_g : h.h_out;
         HIP_TRY(hipMemcpyAsync(dst, d_out, (size_t)gn * out_g, hipMemcpyDeviceToHost, h.stream));
         HIP_TRY(hipEventRecord(h.done, h.stream));
         pending[sl] = i;
-    }
-    if ((rc = drain((int)(nchunks & 1)))) return rc;  // older slot first
-    return drain((int)((nchunks + 1) & 1));
+        return QFEC_OK;
+    };
+    for (long long i = 0; i < nchunks && !rc; ++i) rc = chunk(i);
+    if (!rc) rc = drain((int)(nchunks & 1));  // older slot first
+    if (!rc) rc = drain((int)((nchunks + 1) & 1));
+    if (rc) quiesce_host_slots(*ctx);  // no copy may still be writing into the caller's buffers
+    return rc;
 }
 
 int qfec_reconstruct_host(qfec_code* code, unsigned char* h_data, const unsigned char* h_parity,
@@ -749,10 +762,11 @@ int qfec_reconstruct_host(qfec_code* code, unsigned char* h_data, const unsigned
         return QFEC_OK;
     };
     const long long nchunks = (groups + gc - 1) / gc;
-    for (long long i = 0; i < nchunks; ++i) {
+    auto chunk = [&](long long i) -> int {
         const int sl = (int)(i & 1);
         DevCtx::HostSlot& h = ctx->host[sl];
-        if ((rc = drain(sl))) return rc;
+        int r = drain(sl);
+        if (r) return r;
         const long long g0 = i * gc, gn = std::min(gc, groups - g0);
         // stage the chunk: data, parity, then its marks in rs.c layout for gn groups
         memcpy(h.h_in, h_data + (size_t)g0 * dg, (size_t)gn * dg);
@@ -765,17 +779,23 @@ int qfec_reconstruct_host(qfec_code* code, unsigned char* h_data, const unsigned
         uint8_t* dd = h.d_buf;
         HIP_TRY(hipMemcpyAsync(dd, h.h_in, used, hipMemcpyHostToDevice, h.stream));
         HIP_TRY(hipMemcpyAsync(dd + cnt_off, h.h_in + cnt_off, 16, hipMemcpyHostToDevice, h.stream));
-        if ((rc = run_reconstruct(*ctx, code, d->d_lut, nullptr, d->d_rec, dd, dd + (size_t)gn * dg,
-                                  dd + (size_t)gn * (dg + pg), gn, block_size, pitch,
-                                  reinterpret_cast<unsigned*>(dd + cnt_off), h.stream)))
-            return rc;
+        if ((r = run_reconstruct(*ctx, code, d->d_lut, nullptr, d->d_rec, dd, dd + (size_t)gn * dg,
+                                 dd + (size_t)gn * (dg + pg), gn, block_size, pitch,
+                                 reinterpret_cast<unsigned*>(dd + cnt_off), h.stream)))
+            return r;
         HIP_TRY(hipMemcpyAsync(h.h_out, dd, (size_t)gn * dg, hipMemcpyDeviceToHost, h.stream));
         HIP_TRY(hipMemcpyAsync(h.h_out + cnt_off, dd + cnt_off, 16, hipMemcpyDeviceToHost, h.stream));
         HIP_TRY(hipEventRecord(h.done, h.stream));
         pending[sl] = i;
+        return QFEC_OK;
+    };
+    for (long long i = 0; i < nchunks && !rc; ++i) rc = chunk(i);
+    if (!rc) rc = drain((int)(nchunks & 1));
+    if (!rc) rc = drain((int)((nchunks + 1) & 1));
+    if (rc) {
+        quiesce_host_slots(*ctx);
+        return rc;
     }
-    if ((rc = drain((int)(nchunks & 1)))) return rc;
-    if ((rc = drain((int)((nchunks + 1) & 1)))) return rc;
     if (failed) *failed = nfail;
     return QFEC_OK;
 }
@@ -865,6 +885,284 @@ int qfec_probe_stream(const unsigned char* d_data, unsigned char* d_parity, long
     hipError_t e = launch_probe_xor(a, (hipStream_t)stream);
     return e == hipSuccess ? QFEC_OK : hip_fail(e, "probe launch");
 }
+
+}  // extern "C"
+
+// ====================================================================== host streaming pipe
+// BASELINE config 5: batches that start and end in (pinned) host memory, streamed over
+// several HIP streams per device and several devices.  Each slot = (device, stream, event,
+// device staging, failed counter).  A piece of a batch takes the next slot round-robin
+// (devices interleaved), waits for that slot's previous piece, and queues H2D -> kernel ->
+// D2H on the slot's stream, so one piece's copies overlap the other slots' kernels and
+// copies.  The caller's buffers must be pinned (DMA'd directly, no host memcpy) and stay
+// untouched until qfec_pipe_wait.
+struct qfec_pipe {
+    struct Slot {
+        int device = 0;
+        DevCtx* ctx = nullptr;
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        uint8_t* d_buf = nullptr;
+        unsigned* d_failed = nullptr;  // accumulated under-determined groups (reconstruct)
+        unsigned* h_failed = nullptr;  // pinned read-back
+        bool busy = false;
+    };
+    std::mutex mu;
+    std::vector<Slot> slots;
+    size_t next = 0;
+    size_t cap = 0;  // staging bytes per slot
+};
+
+namespace {
+
+// wait for every queued piece (errors are reported after all slots are drained, so no DMA
+// is left in flight into caller memory when an error returns)
+int pipe_drain(qfec_pipe* p) {
+    int rc = QFEC_OK;
+    for (auto& s : p->slots) {
+        if (!s.busy) continue;
+        hipError_t e = hipEventSynchronize(s.done);
+        if (e != hipSuccess) {
+            (void)hipSetDevice(s.device);
+            (void)hipStreamSynchronize(s.stream);
+            if (!rc) rc = hip_fail(e, "qfec_pipe: piece failed");
+        }
+        s.busy = false;
+    }
+    return rc;
+}
+
+struct DeviceRestore {
+    int prev = -1;
+    DeviceRestore() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~DeviceRestore() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+// the next slot, with its previous piece finished
+int pipe_take(qfec_pipe* p, qfec_pipe::Slot** out) {
+    qfec_pipe::Slot& s = p->slots[p->next++ % p->slots.size()];
+    HIP_TRY(hipSetDevice(s.device));
+    if (s.busy) {
+        HIP_TRY(hipEventSynchronize(s.done));
+        s.busy = false;
+    }
+    *out = &s;
+    return QFEC_OK;
+}
+
+// groups per piece: fits a slot, and a batch spreads over all slots
+long long pipe_piece(const qfec_pipe* p, long long groups, size_t per_group) {
+    long long fit = (long long)(p->cap / per_group);
+    long long even = (groups + (long long)p->slots.size() - 1) / (long long)p->slots.size();
+    return std::max<long long>(1, std::min(fit, std::max<long long>(even, 64)));
+}
+
+}  // namespace
+
+extern "C" {
+
+qfec_pipe* qfec_pipe_new(const int* devices, int ndev, int nstreams, long long slot_bytes) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        set_error("qfec_pipe_new: no HIP device available");
+        return nullptr;
+    }
+    if (nstreams < 1 || nstreams > 16 || slot_bytes < (1 << 16) || ndev < 0 || ndev > 64 || (ndev > 0 && !devices)) {
+        set_error("qfec_pipe_new: invalid argument");
+        return nullptr;
+    }
+    std::vector<int> devs;
+    if (ndev == 0)
+        for (int d = 0; d < count; ++d) devs.push_back(d);
+    else
+        devs.assign(devices, devices + ndev);
+    for (int d : devs)
+        if (d < 0 || d >= count || d >= kMaxDevices) {
+            set_error("qfec_pipe_new: device %d out of range (%d visible)", d, count);
+            return nullptr;
+        }
+    DeviceRestore restore;
+    qfec_pipe* p = new (std::nothrow) qfec_pipe();
+    if (!p) return nullptr;
+    p->cap = round_up((size_t)slot_bytes, 4096);
+    p->slots.resize((size_t)nstreams * devs.size());
+    int rc = QFEC_OK;
+    for (size_t i = 0; i < p->slots.size() && !rc; ++i) {
+        qfec_pipe::Slot& s = p->slots[i];
+        s.device = devs[i % devs.size()];  // devices interleaved: consecutive pieces land on different GPUs
+        if (hipSetDevice(s.device) != hipSuccess) { rc = QFEC_EHIP; break; }
+        if ((rc = current_ctx(&s.ctx))) break;
+        if (hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+            hipMalloc(&s.d_buf, p->cap) != hipSuccess || hipMalloc(&s.d_failed, 16) != hipSuccess ||
+            hipMemset(s.d_failed, 0, 16) != hipSuccess ||
+            hipHostMalloc(&s.h_failed, 16, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("qfec_pipe_new: allocation on device %d failed", s.device);
+            rc = QFEC_ENOMEM;
+        }
+    }
+    if (rc) {
+        qfec_pipe_free(p);
+        return nullptr;
+    }
+    return p;
+}
+
+void qfec_pipe_free(qfec_pipe* p) {
+    if (!p) return;
+    DeviceRestore restore;
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        (void)pipe_drain(p);
+        for (auto& s : p->slots) {
+            if (hipSetDevice(s.device) != hipSuccess) continue;
+            if (s.d_buf) (void)hipFree(s.d_buf);
+            if (s.d_failed) (void)hipFree(s.d_failed);
+            if (s.h_failed) (void)hipHostFree(s.h_failed);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+        }
+    }
+    delete p;
+}
+
+int qfec_pipe_encode(qfec_pipe* p, qfec_code* code, const unsigned char* h_data, unsigned char* h_parity,
+                     long long groups, int block_size, long long pitch) {
+    if (!p || !code || groups < 0 || block_size < 1 || pitch < block_size || (groups > 0 && (!h_data || !h_parity))) {
+        set_error("qfec_pipe_encode: invalid argument");
+        return QFEC_EINVAL;
+    }
+    if (groups == 0 || code->m == 0) return QFEC_OK;
+    const int k = code->k, m = code->m;
+    const size_t in_g = (size_t)k * (size_t)pitch, out_g = (size_t)m * (size_t)pitch;
+    if (in_g + out_g > p->cap) {
+        set_error("qfec_pipe_encode: one group (%zu B) exceeds the slot staging (%zu B)", in_g + out_g, p->cap);
+        return QFEC_EINVAL;
+    }
+    if (!is_pinned_host(h_data) || !is_pinned_host(h_parity)) {
+        set_error("qfec_pipe_encode: host buffers must be pinned (hipHostMalloc / hipHostRegister)");
+        return QFEC_EINVAL;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    DeviceRestore restore;
+    const long long gp = pipe_piece(p, groups, in_g + out_g);
+    int rc = QFEC_OK;
+    for (long long g0 = 0; g0 < groups && !rc; g0 += gp) {
+        const long long gn = std::min(gp, groups - g0);
+        qfec_pipe::Slot* s = nullptr;
+        if ((rc = pipe_take(p, &s))) break;
+        uint32_t* tab = nullptr;
+        {
+            std::lock_guard<std::mutex> ck(code->mu);
+            rc = ensure_enc(code, s->device, &tab);
+        }
+        if (rc) break;
+        uint8_t* d_in = s->d_buf;
+        uint8_t* d_out = s->d_buf + (size_t)gn * in_g;
+        if (hipMemcpyAsync(d_in, h_data + (size_t)g0 * in_g, (size_t)gn * in_g, hipMemcpyHostToDevice, s->stream) !=
+            hipSuccess) { rc = hip_fail(hipGetLastError(), "qfec_pipe_encode: H2D"); break; }
+        s->busy = true;
+        if ((rc = run_encode(*s->ctx, code, tab, m, d_in, d_out, gn, block_size, pitch, s->stream))) break;
+        if (hipMemcpyAsync(h_parity + (size_t)g0 * out_g, d_out, (size_t)gn * out_g, hipMemcpyDeviceToHost,
+                           s->stream) != hipSuccess) { rc = hip_fail(hipGetLastError(), "qfec_pipe_encode: D2H"); break; }
+        if (hipEventRecord(s->done, s->stream) != hipSuccess) { rc = hip_fail(hipGetLastError(), "event"); break; }
+    }
+    if (rc) {
+        const std::string err = t_last_error;
+        (void)pipe_drain(p);
+        t_last_error = err;
+    }
+    return rc;
+}
+
+int qfec_pipe_reconstruct(qfec_pipe* p, qfec_code* code, unsigned char* h_data, const unsigned char* h_parity,
+                          const unsigned char* h_marks, long long groups, int block_size, long long pitch) {
+    if (!p || !code || groups < 0 || block_size < 1 || pitch < block_size ||
+        (groups > 0 && (!h_data || !h_marks || (code->m > 0 && !h_parity)))) {
+        set_error("qfec_pipe_reconstruct: invalid argument");
+        return QFEC_EINVAL;
+    }
+    if (groups == 0) return QFEC_OK;
+    const int k = code->k, m = code->m;
+    if (k + m > QFEC_LUT_MAX_N) {
+        set_error("qfec_pipe_reconstruct: k + m = %d > %d", k + m, QFEC_LUT_MAX_N);
+        return QFEC_EUNSUP;
+    }
+    const size_t dg = (size_t)k * (size_t)pitch, pg = (size_t)m * (size_t)pitch;
+    const size_t per_group = dg + pg + (size_t)(k + m);
+    if (per_group + 64 > p->cap) {
+        set_error("qfec_pipe_reconstruct: one group exceeds the slot staging (%zu B)", p->cap);
+        return QFEC_EINVAL;
+    }
+    if (!is_pinned_host(h_data) || (m && !is_pinned_host(h_parity)) || !is_pinned_host(h_marks)) {
+        set_error("qfec_pipe_reconstruct: host buffers must be pinned (hipHostMalloc / hipHostRegister)");
+        return QFEC_EINVAL;
+    }
+    std::lock_guard<std::mutex> lk(p->mu);
+    DeviceRestore restore;
+    const long long gp = pipe_piece(p, groups, per_group + 1);
+    int rc = QFEC_OK;
+    for (long long g0 = 0; g0 < groups && !rc; g0 += gp) {
+        const long long gn = std::min(gp, groups - g0);
+        qfec_pipe::Slot* s = nullptr;
+        if ((rc = pipe_take(p, &s))) break;
+        DevTables* d = nullptr;
+        {
+            std::lock_guard<std::mutex> ck(code->mu);
+            rc = ensure_lut(code, s->device, &d);
+        }
+        if (rc) break;
+        // slot layout: data [gn][k][pitch] | parity [gn][m][pitch] | marks in rs.c layout
+        // for the piece: gn*k data marks, then gn*m parity marks (module/rs.c:609-612)
+        uint8_t* dd = s->d_buf;
+        uint8_t* dp = dd + (size_t)gn * dg;
+        uint8_t* dm = dp + (size_t)gn * pg;
+        s->busy = true;
+        if (hipMemcpyAsync(dd, h_data + (size_t)g0 * dg, (size_t)gn * dg, hipMemcpyHostToDevice, s->stream) ||
+            (m && hipMemcpyAsync(dp, h_parity + (size_t)g0 * pg, (size_t)gn * pg, hipMemcpyHostToDevice, s->stream)) ||
+            hipMemcpyAsync(dm, h_marks + (size_t)g0 * k, (size_t)gn * k, hipMemcpyHostToDevice, s->stream) ||
+            (m && hipMemcpyAsync(dm + (size_t)gn * k, h_marks + (size_t)groups * k + (size_t)g0 * m, (size_t)gn * m,
+                                 hipMemcpyHostToDevice, s->stream))) {
+            rc = hip_fail(hipGetLastError(), "qfec_pipe_reconstruct: H2D");
+            break;
+        }
+        if ((rc = run_reconstruct(*s->ctx, code, d->d_lut, nullptr, d->d_rec, dd, dp, dm, gn, block_size, pitch,
+                                  s->d_failed, s->stream)))
+            break;
+        if (hipMemcpyAsync(h_data + (size_t)g0 * dg, dd, (size_t)gn * dg, hipMemcpyDeviceToHost, s->stream) !=
+            hipSuccess) { rc = hip_fail(hipGetLastError(), "qfec_pipe_reconstruct: D2H"); break; }
+        if (hipEventRecord(s->done, s->stream) != hipSuccess) { rc = hip_fail(hipGetLastError(), "event"); break; }
+    }
+    if (rc) {
+        const std::string err = t_last_error;
+        (void)pipe_drain(p);
+        t_last_error = err;
+    }
+    return rc;
+}
+
+int qfec_pipe_wait(qfec_pipe* p, long long* failed) {
+    if (!p) return QFEC_EINVAL;
+    std::lock_guard<std::mutex> lk(p->mu);
+    DeviceRestore restore;
+    int rc = pipe_drain(p);
+    long long nf = 0;
+    for (auto& s : p->slots) {  // read back and reset the slots' failed counters
+        if (hipSetDevice(s.device) != hipSuccess ||
+            hipMemcpyAsync(s.h_failed, s.d_failed, 4, hipMemcpyDeviceToHost, s.stream) != hipSuccess ||
+            hipMemsetAsync(s.d_failed, 0, 4, s.stream) != hipSuccess || hipStreamSynchronize(s.stream) != hipSuccess) {
+            if (!rc) rc = hip_fail(hipGetLastError(), "qfec_pipe_wait");
+            continue;
+        }
+        nf += *s.h_failed;
+    }
+    if (failed) *failed = nf;
+    return rc;
+}
+
+int qfec_pipe_slots(const qfec_pipe* p) { return p ? (int)p->slots.size() : QFEC_EINVAL; }
 
 }  // extern "C"
 
@@ -1213,7 +1511,8 @@ int reed_solomon_encode(reed_solomon* rs, unsigned char** shards, int nr_shards,
         return rc;
     }
     const size_t pitch = round_up((size_t)block_size, 16);
-    const long long per = std::max<long long>(1, (long long)(kChunkBytes / ((size_t)n * pitch)));
+    const long long per = tuning().host_chunk > 0 ? tuning().host_chunk
+                                                  : std::max<long long>(1, (long long)(kChunkBytes / ((size_t)n * pitch)));
     for (long long g0 = 0; g0 < G && !rc; g0 += per) {
         const long long gn = std::min(per, G - g0);
         const size_t dbytes = (size_t)gn * k * pitch, pbytes = (size_t)gn * m * pitch;
@@ -1252,51 +1551,67 @@ int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned 
         }
         mk = hmarks.data();
     }
-    // groups under-determined -> -1 (rs.c:631-634); host-side count, same rule as the kernel
-    std::vector<int32_t> grec;
-    std::vector<uint32_t> recs;
-    long long nfail = 0;
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        host_records(c, mk, G, grec, recs, &nfail);
-    }
-    if (recs.empty()) return nfail ? -1 : 0;  // nothing to recover
-    DevCtx* ctx = nullptr;
-    int rc = current_ctx(&ctx);
-    if (rc) { fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error()); return rc; }
+    // chunks of ~kChunkBytes of staged shards, each with its own decode records (built from
+    // that chunk's marks), so staging stays bounded whatever the batch size; groups left
+    // under-determined -> -1 (rs.c:631-634), counted on the host by the kernel's rule
     unsigned char** data = shards;
     unsigned char** par = shards + G * k;
-    const bool dev = is_device_ptr(shards[0]);
     const size_t pitch = round_up((size_t)block_size, 16);
-    std::vector<uint8_t> only((size_t)G * k);
-    for (size_t i = 0; i < only.size(); ++i) only[i] = mk[i] ? 1 : 0;
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    // one batch: data | parity | group records | record words (chunking keeps the
-    // record offsets of the whole call valid, so stage the groups in one pass)
-    const size_t dbytes = (size_t)G * k * pitch, pbytes = (size_t)G * m * pitch;
-    const size_t gbytes = round_up((size_t)G * 4, 16), rbytes = round_up(recs.size() * 4, 16);
-    if ((rc = ensure_stage(*ctx, dbytes + pbytes + gbytes + rbytes, dbytes + pbytes + gbytes + rbytes)) == 0) {
+    const long long per = tuning().host_chunk > 0 ? tuning().host_chunk  // knob: tests force several chunks
+                                                  : std::max<long long>(1, (long long)(kChunkBytes / ((size_t)n * pitch)));
+    DevCtx* ctx = nullptr;
+    bool dev = false;
+    long long nfail_all = 0;
+    int rc = QFEC_OK;
+    std::vector<uint8_t> cmarks, only;
+    std::vector<int32_t> grec;
+    std::vector<uint32_t> recs;
+    for (long long g0 = 0; g0 < G && !rc; g0 += per) {
+        const long long gn = std::min(per, G - g0);
+        cmarks.resize((size_t)gn * n);  // this chunk's marks in the rs.c layout
+        memcpy(cmarks.data(), mk + (size_t)g0 * k, (size_t)gn * k);
+        memcpy(cmarks.data() + (size_t)gn * k, mk + (size_t)G * k + (size_t)g0 * m, (size_t)gn * m);
+        long long nfail = 0;
+        {
+            std::lock_guard<std::mutex> lk(c->mu);
+            host_records(c, cmarks.data(), gn, grec, recs, &nfail);
+        }
+        nfail_all += nfail;
+        if (recs.empty()) continue;  // nothing to recover in this chunk
+        if (!ctx) {
+            if ((rc = current_ctx(&ctx))) break;
+            dev = is_device_ptr(shards[0]);
+        }
+        only.resize((size_t)gn * k);
+        for (size_t i = 0; i < only.size(); ++i) only[i] = cmarks[i] ? 1 : 0;
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        // staged chunk: data | parity | group records | record words
+        const size_t dbytes = (size_t)gn * k * pitch, pbytes = (size_t)gn * m * pitch;
+        const size_t gbytes = round_up((size_t)gn * 4, 16), rbytes = round_up(recs.size() * 4, 16);
+        const size_t tot = dbytes + pbytes + gbytes + rbytes;
+        if ((rc = ensure_stage(*ctx, tot, tot))) break;
         uint8_t* d_d = ctx->d_stage;
         uint8_t* d_p = d_d + dbytes;
         int32_t* d_g = (int32_t*)(d_p + pbytes);
         uint32_t* d_r = (uint32_t*)((uint8_t*)d_g + gbytes);
         uint8_t* hs = ctx->h_stage;
-        memcpy(hs + dbytes + pbytes, grec.data(), (size_t)G * 4);
+        memcpy(hs + dbytes + pbytes, grec.data(), (size_t)gn * 4);
         memcpy(hs + dbytes + pbytes + gbytes, recs.data(), recs.size() * 4);
-        rc = gather_rows(*ctx, data, (size_t)G * k, block_size, pitch, d_d, hs, dev);
-        if (!rc) rc = gather_rows(*ctx, par, (size_t)G * m, block_size, pitch, d_p, hs + dbytes, dev);
+        rc = gather_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, hs, dev);
+        if (!rc) rc = gather_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, hs + dbytes, dev);
         if (!rc && hipMemcpyAsync(d_g, hs + dbytes + pbytes, gbytes + rbytes, hipMemcpyHostToDevice, ctx->stream) !=
                        hipSuccess)
-            rc = QFEC_EHIP;
-        if (!rc) rc = run_reconstruct(*ctx, c, nullptr, d_g, d_r, d_d, d_p, nullptr, G, block_size, (long long)pitch,
+            rc = hip_fail(hipGetLastError(), "reed_solomon_reconstruct: H2D");
+        if (!rc) rc = run_reconstruct(*ctx, c, nullptr, d_g, d_r, d_d, d_p, nullptr, gn, block_size, (long long)pitch,
                                       nullptr, ctx->stream);
-        if (!rc) rc = scatter_rows(*ctx, data, (size_t)G * k, block_size, pitch, d_d, hs, dev, only.data());
+        if (!rc) rc = scatter_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, hs, dev, only.data());
+        if (rc) (void)hipStreamSynchronize(ctx->stream);  // nothing left in flight into the staging
     }
     if (rc) {
         fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error());
         return rc;
     }
-    return nfail ? -1 : 0;
+    return nfail_all ? -1 : 0;
 }
 
 }  // extern "C"

@@ -1,0 +1,157 @@
+"""Host-to-host legs of bench.py: the FEC path starts and ends in host memory (the UDP socket /
+PacketBuffer, network/FecCodecBuf.cpp), so BASELINE configs[4] is measured host -> device ->
+host through the product's streaming engine (include/qfec.h qfec_pipe).
+
+host_mixed_leg   configs[4]: (4,2), (10,3) and (16,4 @ 1400 B) batches of ~64 MiB of data
+                 each, interleaved, encode AND reconstruct (m random erasures of n per
+                 group), every batch in its own pinned host buffers, 3 HIP streams per GPU.
+                 Runs on every rank (one GPU each) between barriers; value = all ranks' data
+                 bytes / the slowest rank's time.  Verified byte for byte afterwards.
+host_encode_leg  the single-shape host-inclusive encode (qfec_encode_host) of the headline
+                 batch, rank 0.
+
+Everything here is measurement plumbing around the C ABI; the arithmetic is libqfec's.
+"""
+import time
+
+import torch
+
+from .codec import Code, Pipe, QfecError, synth_fill
+from .sharding import rank_seed
+from .synth import SEED_DECODE, SEED_ENCODE, erasure_marks, marks_to_rs_layout
+
+GIB = float(1 << 30)
+MIXED = ((4, 2, 1024), (10, 3, 1024), (16, 4, 1400))
+
+
+def _round16(x):
+    return (x + 15) // 16 * 16
+
+
+def make_mixed_batches(rank, dev, batch_bytes=64 << 20, per_shape=2, shapes=MIXED):
+    """Pinned host batches: tx (data -> parity to compute) and rx (damaged data + parity +
+    marks -> data to restore) per (shape, rep); parity and payload made on the device."""
+    batches = []
+    for rep in range(per_shape):
+        for k, m, B in shapes:
+            n, pitch = k + m, _round16(B)
+            G = max(1, batch_bytes // (k * pitch))
+            code = Code.cauchy(k, m)
+            tag = (k << 8 | m) ^ (rep << 16)
+            d = torch.empty((G, k, pitch), dtype=torch.uint8, device=dev)
+            synth_fill(d, rank_seed(SEED_ENCODE ^ tag, rank))
+            p = torch.empty((G, m, pitch), dtype=torch.uint8, device=dev)
+            code.encode(d, p, B)
+            code.prepare_reconstruct()
+            gm = erasure_marks(rank_seed(SEED_DECODE ^ tag, rank), G, n, m)
+            lost = torch.from_numpy(gm[:, :k].astype(bool))
+            b = {"code": code, "k": k, "m": m, "B": B, "G": G,
+                 "tx_data": torch.empty((G, k, pitch), dtype=torch.uint8, pin_memory=True),
+                 "tx_par": torch.empty((G, m, pitch), dtype=torch.uint8, pin_memory=True),
+                 "rx_data": torch.empty((G, k, pitch), dtype=torch.uint8, pin_memory=True),
+                 "rx_par": torch.empty((G, m, pitch), dtype=torch.uint8, pin_memory=True),
+                 "rx_marks": torch.from_numpy(marks_to_rs_layout(gm, k)).pin_memory(),
+                 "lost": lost, "dec_groups": int(lost.any(1).sum()), "par_ref": p.cpu()}
+            b["tx_data"].copy_(d)
+            b["rx_data"].copy_(d)
+            b["rx_par"].copy_(p)
+            del d, p
+            batches.append(b)
+    torch.cuda.synchronize()
+    return batches
+
+
+def damage(batches):
+    """Erase the marked data shards of every rx batch and clear every tx parity (untimed)."""
+    for b in batches:
+        b["rx_data"][b["lost"]] = 0x5A
+        b["tx_par"].zero_()
+
+
+def run_mixed(pipe, batches):
+    """Queue every batch (encode tx, reconstruct rx, interleaved) and wait: one pass."""
+    for b in batches:
+        pipe.encode(b["code"], b["tx_data"], b["tx_par"], b["B"])
+        pipe.reconstruct(b["code"], b["rx_data"], b["rx_par"], b["rx_marks"], b["B"])
+    return pipe.wait()
+
+
+def verify(batches):
+    ok = True
+    for b in batches:
+        B = b["B"]
+        ok &= bool(torch.equal(b["tx_par"][..., :B], b["par_ref"][..., :B]))
+        ok &= bool(torch.equal(b["rx_data"][..., :B], b["tx_data"][..., :B]))
+    return ok
+
+
+def mixed_units(batches):
+    """(data bytes, H2D bytes, D2H bytes) of one pass (data counted at B, copies at pitch)."""
+    data = h2d = d2h = 0
+    for b in batches:
+        k, m, B, G = b["k"], b["m"], b["B"], b["G"]
+        pitch = b["tx_data"].shape[2]
+        data += G * k * B + b["dec_groups"] * k * B
+        h2d += G * k * pitch + G * (k + m) * pitch + G * (k + m)
+        d2h += G * m * pitch + G * k * pitch
+    return data, h2d, d2h
+
+
+def host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather, passes=3, streams=3):
+    dev = torch.device("cuda", torch.cuda.current_device())
+    try:
+        batches = make_mixed_batches(rank, dev)
+        pipe = Pipe(devices=[dev.index], streams=streams)
+        damage(batches)
+        nf = run_mixed(pipe, batches)  # warm-up pass (restores rx, computes tx)
+        damage(batches)
+        err = None
+    except (QfecError, RuntimeError) as exc:  # report, never fake (the collectives below still run)
+        err, nf = repr(exc), -1
+    barrier(world)
+    t0 = time.perf_counter()
+    if err is None:
+        for _ in range(passes):
+            nf += run_mixed(pipe, batches)
+    t1 = time.perf_counter()
+    barrier(world)
+    el = all_max(t1 - t0, world)
+    ok = err is None and nf == 0 and verify(batches)
+    ok = all_sum(0.0 if ok else 1.0, world) == 0.0
+    data, h2d, d2h = mixed_units(batches) if err is None else (0, 0, 0)
+    total = all_sum(float(data * passes), world)
+    per_rank = all_gather((t1 - t0) * 1e3 / passes, world, rank)
+    out = {"value": round(total / el / GIB, 2) if el > 0 else None, "unit": "GiB/s", "verified": ok,
+           "what": "BASELINE configs[4]: (4,2), (10,3) 1 KiB and (16,4) 1400 B batches of ~64 MiB data, interleaved, "
+                   "encode + reconstruct (m random erasures of n per group), pinned host buffers per batch, "
+                   f"qfec_pipe with {streams} HIP streams per GPU, host -> device -> host",
+           "passes": passes, "ms_per_pass": round(el / passes * 1e3, 3),
+           "per_rank_ms_per_pass": [round(x, 3) for x in per_rank],
+           "pcie_gbs_per_rank": round((h2d + d2h) * passes / (t1 - t0) / 1e9, 2) if err is None else None,
+           "h2d_gbs_per_rank": round(h2d * passes / (t1 - t0) / 1e9, 2) if err is None else None,
+           "batches_per_rank": len(batches) if err is None else 0}
+    if err is not None:
+        out["error"] = err
+    if err is None:
+        pipe.close()
+    del batches
+    return out
+
+
+def host_encode_leg(code, data, parity, B):
+    """qfec_encode_host over the headline batch from pinned host buffers, best of 3 after one
+    warm-up call; parity verified against the device-resident encode."""
+    try:
+        h_data = data.cpu().pin_memory()
+        h_par = torch.empty(parity.shape, dtype=torch.uint8).pin_memory()
+        ts = []
+        for _ in range(4):
+            t = time.perf_counter()
+            code.encode_host(h_data, h_par, B)
+            ts.append(time.perf_counter() - t)
+        G, k = data.shape[0], data.shape[1]
+        ok = bool(torch.equal(h_par, parity.cpu()))
+        return {"value": round(G * k * B / min(ts[1:]) / GIB, 2), "unit": "GiB/s", "verified": ok,
+                "what": "qfec_encode_host, pinned host buffers, H2D + encode + D2H chunked over 2 streams"}
+    except Exception as exc:  # report, never fake
+        return {"value": None, "verified": False, "error": repr(exc)}

@@ -1,0 +1,199 @@
+"""GPU: the host-memory paths against the oracle.
+
+* qfec_pipe (BASELINE configs[4]): interleaved (4,2) / (10,3) / (16,4 @ 1400 B) batches,
+  encode AND reconstruct, from pinned host buffers over 3 streams per device, and over a
+  two-entry device list (the multi-device slot rotation; the box has one GPU, so the list
+  names it twice).  Byte-checked against the oracle (module/rs.c restatement, pinned).
+* reed_solomon_reconstruct on host pointer arrays spanning several staging chunks.
+* The Python face rejects tensors the C ABI would misread (dtype) or cannot reach (host).
+* A product multi-rank run: two gloo ranks share cuda:0, each runs libqfec on its
+  shard_range slice; the gathered result equals the single-rank oracle output.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import quicknet_amd as qa
+from quicknet_amd.sharding import shard_range
+from quicknet_amd.synth import marks_to_rs_layout, synth_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+DEV = torch.device("cuda:0")
+MIXED = [(4, 2, 1024, 301), (10, 3, 1024, 257), (16, 4, 1400, 129)]
+
+
+def round16(x):
+    return (x + 15) // 16 * 16
+
+
+def random_marks(rng, G, k, m, unrecoverable=True):
+    gm = np.zeros((G, k + m), np.uint8)
+    hi = m + 2 if unrecoverable else m + 1
+    for g in range(G):
+        gm[g, rng.choice(k + m, size=int(rng.integers(0, hi)), replace=False)] = 1
+    return gm
+
+
+def make_case(oracle, k, m, B, G, seed):
+    """Pinned host buffers for one encode batch and one reconstruct batch + oracle answers."""
+    pitch = round16(B)
+    rng = np.random.default_rng(seed)
+    code = qa.Code.cauchy(k, m)
+    data = synth_bytes(seed, G * k * B).reshape(G, k, B)
+    par_ref = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(code.rows, data, par_ref, B)
+    # reconstruct with INCONSISTENT parity: pins the survivor rule byte for byte (rs.c:620-629)
+    rx_par = synth_bytes(seed + 1, G * m * B).reshape(G, m, B)
+    gm = random_marks(rng, G, k, m)
+    marks = marks_to_rs_layout(gm, k)
+    damaged = data.copy()
+    damaged.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+    rx_ref = damaged.copy()
+    oracle.rs_reconstruct(code.rows, rx_ref, rx_par.copy(), marks, B)
+    nfail = int(((gm[:, :k].sum(1) > 0) & (gm.sum(1) > m)).sum())
+
+    def pin(a, pad=0xC3):
+        out = np.full(a.shape[:-1] + (pitch,), pad, np.uint8)
+        out[..., :B] = a
+        return torch.from_numpy(out).pin_memory()
+
+    return {"code": code, "B": B, "tx_data": pin(data), "tx_par": torch.full((G, m, pitch), 0x5A, dtype=torch.uint8)
+            .pin_memory(), "par_ref": par_ref, "rx_data": pin(damaged), "rx_par": pin(rx_par),
+            "rx_marks": torch.from_numpy(marks).pin_memory(), "rx_ref": rx_ref, "nfail": nfail}
+
+
+@pytest.mark.parametrize("devices,streams,slot", [([0], 3, 1 << 20), ([0, 0], 3, 1 << 20), ([0], 1, 64 << 20),
+                                                  (None, 4, 256 << 10)])
+def test_pipe_mixed_vs_oracle(oracle, devices, streams, slot):
+    pipe = qa.Pipe(devices=devices, streams=streams, slot_bytes=slot)
+    assert pipe.slots == streams * (len(devices) if devices else torch.cuda.device_count())
+    cases = [make_case(oracle, k, m, B, G, 1000 + 7 * k + B) for k, m, B, G in MIXED]
+    for c in cases:  # interleaved: encode one shape, reconstruct it, then the next shape
+        pipe.encode(c["code"], c["tx_data"], c["tx_par"], c["B"])
+        pipe.reconstruct(c["code"], c["rx_data"], c["rx_par"], c["rx_marks"], c["B"])
+    nf = pipe.wait()
+    for c in cases:
+        B = c["B"]
+        assert np.array_equal(c["tx_par"].numpy()[..., :B], c["par_ref"])
+        assert np.array_equal(c["rx_data"].numpy()[..., :B], c["rx_ref"])
+    assert nf == sum(c["nfail"] for c in cases)
+    # a second round on the same pipe: the failed counters were reset by wait()
+    c = cases[1]
+    pipe.reconstruct(c["code"], c["rx_data"], c["rx_par"], c["rx_marks"], c["B"])
+    assert pipe.wait() == c["nfail"]
+    pipe.close()
+
+
+def test_pipe_rejects_pageable_and_oversize(oracle):
+    pipe = qa.Pipe(devices=[0], streams=2, slot_bytes=1 << 16)
+    code = qa.Code.cauchy(10, 3)
+    with pytest.raises(qa.QfecError, match="pinned"):
+        pipe.encode(code, np.zeros((4, 10, 1024), np.uint8), np.zeros((4, 3, 1024), np.uint8))
+    big = torch.zeros((2, 10, 8192), dtype=torch.uint8).pin_memory()
+    with pytest.raises(qa.QfecError, match="exceeds"):
+        pipe.encode(code, big, torch.zeros((2, 3, 8192), dtype=torch.uint8).pin_memory())
+    assert pipe.wait() == 0
+    pipe.close()
+
+
+def test_codec_rejects_misread_tensors():
+    """tensors with another element type would be read as bytes; host tensors
+    cannot be launched on."""
+    code = qa.Code.cauchy(4, 2)
+    d = torch.zeros((8, 4, 64), dtype=torch.uint8, device=DEV)
+    p = torch.zeros((8, 2, 64), dtype=torch.uint8, device=DEV)
+    with pytest.raises(qa.QfecError, match="dtype"):
+        code.encode(d.to(torch.int32), p)
+    with pytest.raises(qa.QfecError, match="device tensor"):
+        code.encode(d.cpu(), p)
+    marks = torch.zeros(8 * 6, dtype=torch.uint8, device=DEV)
+    with pytest.raises(qa.QfecError, match="dtype"):
+        code.reconstruct(d, p, marks, failed=torch.zeros(1, dtype=torch.float32, device=DEV))
+    code.encode(d, p)  # the well-typed call still works
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("chunk", [7, 0])
+def test_rs_reconstruct_host_chunks(oracle, chunk):
+    """reed_solomon_reconstruct over host pointer arrays, staged in chunks of `chunk` groups
+    (0: the 256 MiB default) with per-chunk decode records; unrecoverable groups -> -1."""
+    k, m, B, G = 10, 3, 1000, 53
+    rs = qa.ReedSolomon(k, m)
+    rng = np.random.default_rng(5)
+    data = synth_bytes(77, G * k * B).reshape(G, k, B)
+    par = synth_bytes(78, G * m * B).reshape(G, m, B)
+    gm = random_marks(rng, G, k, m)
+    marks = marks_to_rs_layout(gm, k)
+    work = data.copy()
+    work.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+    expect = work.copy()
+    oracle.rs_reconstruct(rs.parity.copy(), expect, par.copy(), marks, B)
+    qa.tune("host_chunk", chunk)
+    try:
+        rc = rs.reconstruct(work, par.copy(), marks, B)
+    finally:
+        qa.tune("host_chunk", 0)
+    assert np.array_equal(work, expect)
+    assert rc == (-1 if ((gm[:, :k].sum(1) > 0) & (gm.sum(1) > m)).any() else 0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_worker(rank, world, port, G, k, m, B, q):
+    """One rank: libqfec encode + reconstruct of its contiguous slice on cuda:0 (ranks share
+    the one GPU of the box), results gathered over gloo for the check only."""
+    import torch.distributed as dist
+    from quicknet_amd.synth import erasure_marks
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    a, b = shard_range(G, rank, world)
+    code = qa.Code.cauchy(k, m)
+    data = synth_bytes(4242, G * k * B).reshape(G, k, B)[a:b]
+    gm = erasure_marks(4343, G, k + m, m)[a:b]
+    d = torch.from_numpy(np.ascontiguousarray(data)).to("cuda:0")
+    p = torch.empty((b - a, m, B), dtype=torch.uint8, device="cuda:0")
+    code.encode(d, p)
+    w = d.clone()
+    w[torch.from_numpy(gm[:, :k].astype(bool)).to("cuda:0")] = 0x5A
+    code.reconstruct(w, p, torch.from_numpy(marks_to_rs_layout(gm, k)).to("cuda:0"))
+    torch.cuda.synchronize()
+    out = [None] * world
+    dist.all_gather_object(out, (p.cpu().numpy().tobytes(), bool(torch.equal(w, d))))
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+def test_two_ranks_share_gpu_match_single(oracle):
+    import torch.multiprocessing as mp
+    G, k, m, B, world = 1001, 10, 3, 1024, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, G, k, m, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=90)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    data = synth_bytes(4242, G * k * B).reshape(G, k, B)
+    ref = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(qa.Code.cauchy(k, m).rows, data, ref, B)
+    assert b"".join(x[0] for x in out) == ref.tobytes()
+    assert all(x[1] for x in out)  # every rank's reconstruct restored its slice

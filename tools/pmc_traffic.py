@@ -56,6 +56,7 @@ def main():
     p.add_argument("--m", type=int, default=3)
     p.add_argument("--block", type=int, default=1024)
     p.add_argument("--groups", type=int, default=100_000)
+    p.add_argument("--tag", default="PMC run", help="which run produced the numbers (recorded in the JSON)")
     a = p.parse_args()
     bench_args = ["--steps", "5", "--warmup", "1", "--k", str(a.k), "--m", str(a.m), "--block", str(a.block),
                   "--groups", str(a.groups), "--no-side"]
@@ -79,7 +80,11 @@ def main():
     if os.path.exists(a.json):
         with open(a.json) as fh:
             doc = json.load(fh)
+    sys.path.insert(0, ROOT)
+    from bench import kernel_sources_hash
     doc[key] = {
+        "kernel_sources_sha256": kernel_sources_hash(),  # bench.py ignores the entry once the kernels change
+        "run": a.tag,
         "encode_bytes_per_launch": res.get("encode", {}).get("bytes_per_launch"),
         "reconstruct_bytes_per_launch": res.get("reconstruct", {}).get("bytes_per_launch"),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes = 2*FETCH_SIZE*1024 "
