@@ -247,6 +247,45 @@ def gen_reconstruct(rs):
     np.savez_compressed(os.path.join(OUT, "reconstruct.npz"), **out)
 
 
+def gen_reconstruct_large(rs):
+    """rs.c reconstruct at the bench block sizes (B = 1024 / 1400), where the GPU's 8-, 12- and
+    16-byte-lane bodies and the multi-wave-per-group split engage: sampled masks with 0..m+1
+    erasures (so unrecoverable groups too), consistent and inconsistent parity, erased
+    buffers pre-filled with 0x5A.  Stored as sha256 digests of the whole reconstructed data
+    region plus rc (the fixtures stay small); tests regenerate inputs from the seeds."""
+    out = {}
+    cases = [(10, 3, 1024, 600), (16, 4, 1400, 400), (10, 3, 1400, 300), (4, 2, 1024, 300), (16, 4, 1024, 300),
+             (12, 4, 1400, 200)]
+    for k, m, B, sample in cases:
+        n = k + m
+        gen = np.random.default_rng(0xB16B + 13 * k + B)
+        gmarks = np.zeros((sample, n), np.uint8)
+        for g in range(sample):
+            gmarks[g, gen.choice(n, size=int(gen.integers(0, m + 2)), replace=False)] = 1
+        seed = 0x1A2E + 31 * k + m + B
+        data0 = synth_bytes(seed, sample * k * B).reshape(sample * k, B)
+        par_c = np.zeros((sample * m, B), dtype=np.uint8)
+        h = rs.reed_solomon_new(k, m)
+        ptrs = (C.c_void_p * (sample * n))(*([ptr(data0, i * B) for i in range(sample * k)] +
+                                              [ptr(par_c, i * B) for i in range(sample * m)]))
+        rs.reed_solomon_encode(h, ptrs, sample * n, B)
+        rs.reed_solomon_release(h)
+        par_i = synth_bytes(seed ^ 0xFFFF, sample * m * B).reshape(sample * m, B)
+        marks = np.concatenate([gmarks[:, :k].reshape(-1), gmarks[:, k:].reshape(-1)]).astype(np.uint8)
+        key = f"{k}_{m}_{B}"
+        for kind, par in (("cons", par_c), ("incons", par_i)):
+            d = data0.copy()
+            d[marks[:sample * k] == 1] = 0x5A
+            p = par.copy()
+            rc = rs_reconstruct_batch(rs, k, m, d, p, marks, B)
+            assert np.array_equal(p, par)
+            out[f"{kind}_{key}"] = np.frombuffer(hashlib.sha256(d.tobytes()).digest(), dtype=np.uint8)
+            out[f"rc_{kind}_{key}"] = np.array([rc], dtype=np.int32)
+        out[f"seed_{key}"] = np.array([seed], dtype=np.uint64)
+        out[f"marks_{key}"] = gmarks
+    np.savez_compressed(os.path.join(OUT, "reconstruct_large.npz"), **out)
+
+
 def gen_fec_decode(fec):
     """fec.c fec_decode on k received packets: NetFecCodec order (first k valid in group
     order), random arrival order (exercises shuffle, fec.c:738-771), and error cases
@@ -407,13 +446,14 @@ def gen_wire():
 
 
 def main():
+    """python oracle/gen_golden.py [name ...]  (default: every fixture file)"""
     os.makedirs(OUT, exist_ok=True)
     rs, fec = load_ref()
-    gen_matrices(rs, fec)
-    gen_encode(rs, fec)
-    gen_reconstruct(rs)
-    gen_fec_decode(fec)
-    gen_wire()
+    gens = {"matrices": lambda: gen_matrices(rs, fec), "encode": lambda: gen_encode(rs, fec),
+            "reconstruct": lambda: gen_reconstruct(rs), "reconstruct_large": lambda: gen_reconstruct_large(rs),
+            "fec_decode": lambda: gen_fec_decode(fec), "wire": gen_wire}
+    for name in (sys.argv[1:] or list(gens)):
+        gens[name]()
     manifest = {
         "generator": "oracle/gen_golden.py",
         "reference": "skywind3000/QuickNet @ 2024-10-08, module/rs.c + system/fec.c compiled by oracle/Makefile",

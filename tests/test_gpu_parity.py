@@ -159,6 +159,44 @@ def test_reconstruct_vs_golden(golden, oracle, k, m, B, path):
             assert np.array_equal(out.reshape(G * k, B), z[f"incons_{key}"])
 
 
+RECON_LARGE = [(10, 3, 1024), (16, 4, 1400), (10, 3, 1400), (4, 2, 1024), (16, 4, 1024), (12, 4, 1400)]
+
+
+@pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4, "abi"])
+@pytest.mark.parametrize("k,m,B", RECON_LARGE)
+def test_reconstruct_large_vs_golden(golden, oracle, k, m, B, impl):
+    """Every reconstruct body (-1 auto, 0 row loop, 1 all rows, 2/3/4 exact-e rows on 16-, 8-
+    and 12-B lanes) and the reed_solomon_reconstruct ABI against bytes the reference's own rs.c
+    produced at the bench block sizes (digests in reconstruct_large.npz): the wide-lane bodies
+    and the multi-wave-per-group split are pinned to the reference directly."""
+    from test_oracle_golden import large_case
+    z = golden("reconstruct_large.npz")
+    key, gm, data0, par_i, marks = large_case(z, k, m, B)
+    G = gm.shape[0]
+    par_c = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(oracle.cauchy(k, m), data0, par_c, B)
+    for kind, par in (("cons", par_c), ("incons", par_i)):
+        d = data0.copy()
+        d.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+        if impl == "abi":
+            rc = qa.ReedSolomon(k, m).reconstruct(d, par.copy(), marks, B)
+            assert rc == z[f"rc_{kind}_{key}"][0]
+            out = d
+        else:
+            pitch = round16(B)
+            dd = to_dev(padded(d, pitch))
+            failed = torch.zeros(1, dtype=torch.int32, device=DEV)
+            qa.tune("recon_impl", impl)
+            try:
+                qa.Code.cauchy(k, m).reconstruct(dd, to_dev(padded(par, pitch)), to_dev(marks), B, failed)
+                torch.cuda.synchronize()
+            finally:
+                qa.tune("recon_impl", -1)
+            out = dd.cpu().numpy()[..., :B]
+            assert (int(failed.item()) > 0) == (z[f"rc_{kind}_{key}"][0] == -1)
+        assert hashlib.sha256(np.ascontiguousarray(out).tobytes()).digest() == z[f"{kind}_{key}"].tobytes()
+
+
 FEC_DEC = [(2, 4), (3, 5), (5, 8), (4, 6), (3, 4), (4, 5), (5, 6), (7, 8), (10, 13), (16, 20), (1, 3)]
 
 

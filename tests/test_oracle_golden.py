@@ -97,6 +97,39 @@ def test_rs_reconstruct(oracle, golden, k, m, B):
             assert np.array_equal(d.reshape(G * k, B), z[f"incons_{key}"])
 
 
+RECON_LARGE = [(10, 3, 1024), (16, 4, 1400), (10, 3, 1400), (4, 2, 1024), (16, 4, 1024), (12, 4, 1400)]
+
+
+def large_case(z, k, m, B):
+    """Inputs of one reconstruct_large.npz case, regenerated from its seed (the fixture holds
+    the reference's output digests, oracle/gen_golden.py gen_reconstruct_large)."""
+    key = f"{k}_{m}_{B}"
+    gm = z[f"marks_{key}"]
+    G = gm.shape[0]
+    seed = int(z[f"seed_{key}"][0])
+    data0 = synth_bytes(seed, G * k * B).reshape(G, k, B)
+    par_i = synth_bytes(seed ^ 0xFFFF, G * m * B).reshape(G, m, B)
+    marks = np.concatenate([gm[:, :k].reshape(-1), gm[:, k:].reshape(-1)]).astype(np.uint8)
+    return key, gm, data0, par_i, marks
+
+
+@pytest.mark.parametrize("k,m,B", RECON_LARGE)
+def test_rs_reconstruct_large(oracle, golden, k, m, B):
+    """The oracle against the reference's rs.c reconstruct at the bench block sizes."""
+    z = golden("reconstruct_large.npz")
+    key, gm, data0, par_i, marks = large_case(z, k, m, B)
+    G = gm.shape[0]
+    rows = oracle.cauchy(k, m)
+    par_c = np.zeros((G, m, B), dtype=np.uint8)
+    oracle.rs_encode(rows, data0, par_c, B)
+    for kind, par in (("cons", par_c), ("incons", par_i)):
+        d = data0.copy()
+        d.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+        rc = oracle.rs_reconstruct(rows, d, par.copy(), marks, B)
+        assert rc == z[f"rc_{kind}_{key}"][0]
+        assert hashlib.sha256(d.tobytes()).digest() == z[f"{kind}_{key}"].tobytes()
+
+
 FEC_DEC = [(2, 4), (3, 5), (5, 8), (4, 6), (3, 4), (4, 5), (5, 6), (7, 8), (10, 13), (16, 20), (1, 3)]
 
 
