@@ -128,6 +128,7 @@ struct Tuning {
     int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
     int wire_chunk = 0;     // fused send: groups per body + head launch pair (0: as many as fit)
     int host_chunk = 0;     // qfec_encode_host: groups per pipelined chunk (0: ~32 MiB of data)
+    int wire_rx_split = 1;  // fused receive: k_unpack_v2 (1 auto lanes, 2 16-B, 3 8-B); 0 k_unpack_fused
 };
 Tuning& tuning();
 

@@ -589,6 +589,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_rx_tail") && (value == 0 || value == 1)) { tuning().wire_rx_tail = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
 }

@@ -946,6 +946,382 @@ __global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t*
     }
 }
 
+// ------------------------------------------------------------------ receive, lean single wave
+// k_unpack_v2: k_unpack_fused's rules and layout (one wave per group, the survivors' bytes in
+// register passes), rebuilt after counting what its 675 us go to (rocprofv3 SQ_INSTS_*, r02):
+// ~3 200 VALU and ~1 050 SALU instructions per group, a third of the VALU being v_readlane /
+// v_writelane of 200+ spilled SGPRs (survivor list, sizes, decode tables, checksum words held
+// in SGPR arrays).  The kernel is issue-bound, not HBM-bound.  Here:
+//   * wave-uniform per-row values live in VGPR LANES (v_off, v_rs, v_ss, v_w0), read with one
+//     v_readlane where used; the decode tables are fetched per survivor column next to their
+//     use (an opaque offset keeps them from being hoisted into 150 live SGPRs);
+//   * byte masks only where a pass crosses a boundary (wave-uniform tests), 5 ops per dword;
+//   * a copied row's payload sum is its datagram sum minus its first `head` bytes whenever
+//     the payload reaches the datagram's end (every well-formed datagram); other rows take an
+//     exact slow path.  Decoded rows sum [0, head + size) and subtract the same head bytes.
+// Outputs are identical to k_unpack_fused's.
+__device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+// v with lane l replaced by the wave-uniform x: one v_writelane_b32 (a `lane == l ? x : v`
+// select makes the compiler hoist a 64-bit lane mask per l into SGPRs, which then spill)
+__device__ __forceinline__ uint32_t set_lane(uint32_t v, int l, uint32_t x) {
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(l));
+    return v;
+}
+
+template <int NVA, int NVT>
+struct RxSl {
+    static constexpr int NV = NVA + NVT;
+    int posa, tail, lane;
+    bool acta;
+    int end;  // row bytes at and past `end` are outside the row
+    __device__ __forceinline__ int pos(int d) const { return d < NVA ? posa + 4 * d : tail + 4 * (lane + 64 * (d - NVA)); }
+    __device__ __forceinline__ bool act(int d) const { return d < NVA ? acta : pos(d) < end; }
+    __device__ __forceinline__ void load(uint32_t (&v)[NV], const uint8_t* row) const {
+        if (acta) {
+            if constexpr (NVA == 4) {
+                uint4 w;
+                __builtin_memcpy(&w, row + posa, 16);
+                v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+            } else {
+                uint2 w;
+                __builtin_memcpy(&w, row + posa, 8);
+                v[0] = w.x; v[1] = w.y;
+            }
+        }
+#pragma unroll
+        for (int d = NVA; d < NV; ++d)
+            if (act(d)) __builtin_memcpy(&v[d], row + pos(d), 4);
+    }
+    __device__ __forceinline__ void store(uint8_t* row, const uint32_t (&v)[NV]) const {
+        if (acta) {
+            if constexpr (NVA == 4) {
+                st16(row + posa, make_uint4(v[0], v[1], v[2], v[3]));
+            } else {
+                const u32x2 w = {v[0], v[1]};
+                __builtin_nontemporal_store(w, reinterpret_cast<u32x2*>(row + posa));
+            }
+        }
+#pragma unroll
+        for (int d = NVA; d < NV; ++d)
+            if (act(d)) __builtin_nontemporal_store(v[d], reinterpret_cast<uint32_t*>(row + pos(d)));
+    }
+    // keep the row bytes below n
+    __device__ __forceinline__ void keep_below(uint32_t (&v)[NV], int n) const {
+#pragma unroll
+        for (int d = 0; d < NV; ++d) {
+            const int c = min(max(n - pos(d), 0), 4);
+            v[d] = c >= 4 ? v[d] : v[d] & ((1u << (8 * c)) - 1u);
+        }
+    }
+};
+
+// the round's plan; wave-uniform per-row values in VGPR lanes
+//   v_off  lane c < K: survivor c's shard bytes (offset from the group's first datagram);
+//          lane K + r: checksum-only row r's
+//   v_rs   lane c < K: survivor row | size << 16; lane K + r: checksum-only row | size << 16;
+//          lane K + M + j: decoded (lost) row j
+template <int K, int M>
+struct RxP {
+    uint32_t v_off, v_rs;
+    int ns, e, nx;
+    bool dec, recoverable;
+    uint32_t zero_rows, svmask, lost_data;
+    int min_size, min_xsize;
+    const uint32_t* tab;
+};
+
+template <int K, int M, int NVA, int NVT>
+__device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restrict__ wire_g, uint8_t* __restrict__ out_g,
+                                         uint64_t pitch, const RxSl<NVA, NVT>& sl, bool first, int head, int pass_end,
+                                         uint32_t& v_w0, uint32_t (&dsum)[K], uint32_t (&xsum)[M], uint32_t (&psl)[M]) {
+    constexpr int NV = NVA + NVT;
+    // opaque per pass: the v_readlane results below are not carried across passes in SGPRs
+    asm volatile("" : "+v"(pl.v_off), "+v"(pl.v_rs), "+v"(v_w0));
+    uint32_t x[K][NV];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+#pragma unroll
+        for (int d = 0; d < NV; ++d) x[c][d] = 0;
+        if (c < pl.ns) sl.load(x[c], wire_g + lane_of(pl.v_off, c));
+    }
+    if (pass_end > pl.min_size) {  // some survivor's datagram ends inside this pass
+#pragma unroll
+        for (int c = 0; c < K; ++c) sl.keep_below(x[c], (int)(lane_of(pl.v_rs, c) >> 16));
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) dsum[c] += sum_vec<NV>(x[c]);
+    uint32_t acc[M][NV];
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int d = 0; d < NV; ++d) acc[j][d] = 0;
+    if (pl.dec) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            Sel sc[NV];
+#pragma unroll
+            for (int d = 0; d < NV; ++d) sc[d] = gf_sel(x[c][d]);
+            uint32_t toff = (uint32_t)(c * QFEC_TAB_STRIDE);
+            asm volatile("" : "+s"(toff));  // fetch this column's tables here, not all 5 K M up front
+#pragma unroll
+            for (int j = 0; j < M; ++j) {  // records are padded to M rows: no branch on e
+                const uint32_t* t = pl.tab + toff + j * K * QFEC_TAB_STRIDE;
+                const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
+#pragma unroll
+                for (int d = 0; d < NV; ++d)
+                    acc[j][d] = xor3(acc[j][d], pp0(sc[d], t0, t1), pp1(sc[d], t2, t3)) ^ pp2(sc[d], t4);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+#pragma unroll
+        for (int d = 0; d < NV; ++d) asm volatile("" : "+v"(acc[j][d]));
+    if (first) {  // lane 0, dword 0 of the first pass: bytes 0-3 of every output row
+#pragma unroll
+        for (int c = 0; c < K; ++c) v_w0 = set_lane(v_w0, c, (uint32_t)__builtin_amdgcn_readlane((int)x[c][0], 0));
+#pragma unroll
+        for (int j = 0; j < M; ++j) v_w0 = set_lane(v_w0, K + j, (uint32_t)__builtin_amdgcn_readlane((int)acc[j][0], 0));
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const uint32_t r = lane_of(pl.v_rs, c) & 0xFFFF;
+        if (c < pl.ns && (int)r < K) sl.store(out_g + (uint64_t)r * pitch, x[c]);
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        if (j < pl.e) {
+            sl.store(out_g + (uint64_t)lane_of(pl.v_rs, K + M + j) * pitch, acc[j]);
+            const int hi = head + (int)(lane_of(v_w0, K + j) & 0xFFFF);  // payload end of decoded row j
+            if (pass_end > hi) sl.keep_below(acc[j], hi);
+            psl[j] += sum_vec<NV>(acc[j]);
+        }
+    }
+    if (pl.zero_rows) {
+        uint32_t z[NV];
+#pragma unroll
+        for (int d = 0; d < NV; ++d) z[d] = 0;
+        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) sl.store(out_g + (uint64_t)__builtin_ctz(zr) * pitch, z);
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        if (r < pl.nx) {
+            uint32_t y[NV];
+#pragma unroll
+            for (int d = 0; d < NV; ++d) y[d] = 0;
+            sl.load(y, wire_g + lane_of(pl.v_off, K + r));
+            if (pass_end > pl.min_xsize) sl.keep_below(y, (int)(lane_of(pl.v_rs, K + r) >> 16));
+            xsum[r] += sum_vec<NV>(y);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t head_bytes_sum(uint32_t w0, int head) {
+    return __builtin_amdgcn_sad_u8(head == 4 ? w0 : (w0 & 0xFFFFu), 0u, 0u);
+}
+
+template <int K, int M, int NVA>
+__global__ void __launch_bounds__(256) k_unpack_v2(WireArgs a, const uint8_t* __restrict__ wire,
+                                                   const int32_t* __restrict__ wire_len,
+                                                   const int32_t* __restrict__ lut,
+                                                   const uint32_t* __restrict__ records, uint32_t rec_hdr,
+                                                   uint8_t* __restrict__ shards) {
+    constexpr int N = K + M;
+    constexpr int A = 256 * NVA;  // row bytes per full pass
+    const int lane = threadIdx.x & 63;
+    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (g >= a.groups) return;
+    const int pitch = (int)a.pitch;
+    const uint64_t wp = a.wire_pitch;
+    const uint8_t* wire_g = wire + g * (uint64_t)N * wp;
+    uint8_t* out_g = shards + g * a.group_stride;
+    // ---- headers (unpack_fec_head's checks, FecCodecBuf.cpp:334-411)
+    int len = 0, hdr = 11, size = 0;
+    uint32_t stated = 0;
+    bool okh = false;
+    if (lane < N) {
+        len = wire_len[g * N + lane];
+        const uint4 h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
+        const uint32_t tag = get_byte(h, 0);
+        hdr = tag == 0xED ? 13 : 11;
+        const uint32_t ikn = get_byte(h, 9) | (get_byte(h, 10) << 8);
+        okh = len >= 11 && len <= (int)wp && (tag == 0xEC || tag == 0xED) && len >= hdr &&
+              (int)(ikn & 0xF) == N && (int)((ikn >> 4) & 0xF) == K && (int)((ikn >> 8) & 0xF) == lane &&
+              len - hdr <= pitch;
+        size = okh ? len - hdr : 0;
+        stated = get_byte(h, 11) | (get_byte(h, 12) << 8);
+    }
+    const uint32_t rowmask = (1u << N) - 1u, kmask = (1u << K) - 1u;
+    const uint32_t good = (uint32_t)__ballot(okh) & rowmask;
+    const uint32_t summed = (uint32_t)__ballot(okh && hdr == 13) & rowmask;
+    const uint32_t v_ss = (uint32_t)size | (stated << 16);  // lane r: row r's size | stated checksum
+    // the first round's record, requested before the loads (used unless a survivor fails)
+    const bool rec0_needed = __builtin_popcount(good) >= K && (~good & kmask);
+    const int rec0 = rec0_needed ? __builtin_amdgcn_readfirstlane(lut[~good & rowmask]) : 0;
+    const int head = a.checksum ? 4 : 2;
+    // passes: full passes of A bytes; a remainder of <= 256 bytes rides on the last one as
+    // one tail dword per lane, a longer one is a partial pass of its own
+    const int P = pitch / A, rem = pitch % A;
+    const bool fuse_tail = P > 0 && rem > 0 && rem <= 256;
+    const int passes = P + ((rem > 0 && !fuse_tail) ? 1 : 0);
+    uint32_t bad = 0, verified = 0;
+    RxP<K, M> pl;
+    uint32_t v_w0 = 0, v_dt = 0;  // lane c: survivor c's dword 0 / datagram total; K + j: decoded row j's
+    for (int round = 0; round <= N; ++round) {
+        // ---- plan: survivors = the lowest K good rows (or the good data rows if too few)
+        const uint32_t avail = good & ~bad;
+        pl.lost_data = ~avail & kmask;
+        pl.recoverable = __builtin_popcount(avail) >= K;
+        pl.zero_rows = pl.recoverable ? 0u : pl.lost_data;
+        pl.v_off = pl.v_rs = 0;
+        pl.ns = 0;
+        pl.min_size = pitch;
+        pl.svmask = 0;
+        uint32_t take = pl.recoverable ? avail : (avail & kmask);
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            if (take) {
+                const int r = __builtin_ctz(take);
+                take &= take - 1;
+                const int sz = __builtin_amdgcn_readlane((int)v_ss, r) & 0xFFFF;
+                pl.v_off = set_lane(pl.v_off, c, (uint32_t)((uint64_t)r * wp + (((summed >> r) & 1u) ? 13u : 11u)));
+                pl.v_rs = set_lane(pl.v_rs, c, (uint32_t)(r | (sz << 16)));
+                pl.min_size = min(pl.min_size, sz);
+                pl.ns = c + 1;
+                pl.svmask |= 1u << r;
+            }
+        }
+        pl.dec = pl.recoverable && pl.lost_data;
+        pl.e = 0;
+        pl.tab = records;
+        if (pl.dec) {
+            const int rec = round == 0 ? rec0 : __builtin_amdgcn_readfirstlane(lut[~avail & rowmask]);
+            pl.tab = records + rec + rec_hdr;
+            pl.e = (int)records[rec];
+#pragma unroll
+            for (int j = 0; j < M; ++j)
+                if (j < pl.e) pl.v_rs = set_lane(pl.v_rs, K + M + j, records[rec + 4 + K + j]);
+        }
+        uint32_t extra = good & summed & ~pl.svmask & ~verified & ~bad;  // rows only checksummed
+        pl.nx = 0;
+        pl.min_xsize = pitch;
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            if (extra) {
+                const int rr = __builtin_ctz(extra);
+                extra &= extra - 1;
+                const int sz = __builtin_amdgcn_readlane((int)v_ss, rr) & 0xFFFF;
+                pl.v_off = set_lane(pl.v_off, K + r, (uint32_t)((uint64_t)rr * wp + 13u));
+                pl.v_rs = set_lane(pl.v_rs, K + r, (uint32_t)(rr | (sz << 16)));
+                pl.min_xsize = min(pl.min_xsize, sz);
+                pl.nx = r + 1;
+            }
+        }
+        // ---- the byte passes
+        uint32_t dsum[K], xsum[M], psl[M];
+#pragma unroll
+        for (int c = 0; c < K; ++c) dsum[c] = 0;
+#pragma unroll
+        for (int j = 0; j < M; ++j) xsum[j] = psl[j] = 0;
+        for (int q = 0; q < passes; ++q) {
+            const int base = A * q;
+            if (fuse_tail && q == passes - 1) {
+                RxSl<NVA, 1> sl{base + 4 * NVA * lane, base + A, lane, true, pitch};
+                rx2_pass<K, M, NVA, 1>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, pitch, v_w0, dsum, xsum,
+                                       psl);
+            } else {
+                RxSl<NVA, 0> sl{base + 4 * NVA * lane, 0, lane, base + 4 * NVA * lane < pitch, pitch};
+                rx2_pass<K, M, NVA, 0>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, min(pitch, base + A), v_w0,
+                                       dsum, xsum, psl);
+            }
+        }
+        // ---- verdicts (k_unpack_fused's rules)
+        uint32_t newbad = 0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) {
+            const uint32_t t = wave_total(dsum[c]);
+            v_dt = set_lane(v_dt, c, t);
+            if (c < pl.ns) {
+                const int r = (int)(lane_of(pl.v_rs, c) & 0xFFFF);
+                if ((summed >> r) & 1u) {
+                    if ((t & 0xFFFFu) != (lane_of(v_ss, r) >> 16)) newbad |= 1u << r;
+                    else verified |= 1u << r;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const uint32_t t = wave_total(xsum[j]);
+            if (j < pl.nx) {
+                const int r = (int)(lane_of(pl.v_rs, K + j) & 0xFFFF);
+                if ((t & 0xFFFFu) != (lane_of(v_ss, r) >> 16)) bad |= 1u << r;
+                else verified |= 1u << r;
+            }
+        }
+        if (!(newbad & pl.svmask)) {
+#pragma unroll
+            for (int j = 0; j < M; ++j) v_dt = set_lane(v_dt, K + j, wave_total(psl[j]));
+            break;
+        }
+        bad |= newbad;
+    }
+    // ---- per-row results (k_unpack_fused's)
+    const uint32_t okrows = good & ~bad;
+    if (lane < N) {
+        const bool ok = (okrows >> lane) & 1u;
+        if (lane < K) a.marks[g * K + lane] = ok ? 0 : 1;
+        else a.marks[a.groups * K + g * M + (lane - K)] = ok ? 0 : 1;
+        if (a.rx_size) a.rx_size[g * N + lane] = ok ? size : -1;
+    }
+    int st = 0, psz = 0;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const uint32_t rs = lane_of(pl.v_rs, c);
+        const int r = (int)(rs & 0xFFFF), sz = (int)(rs >> 16);
+        if (c < pl.ns && r < K) {
+            const uint32_t w0 = lane_of(v_w0, c);
+            const int p = (int)(w0 & 0xFFFF);
+            uint32_t ps = lane_of(v_dt, c) - head_bytes_sum(w0, head);
+            if (a.checksum && head + p < sz) {  // bytes after the payload inside the datagram: exact sum
+                uint32_t s = 0;
+                const uint8_t* row = wire_g + lane_of(pl.v_off, c);
+                for (int p0 = 0; p0 < sz; p0 += 1024) {
+                    const int pos = p0 + 16 * lane;
+                    if (pos < sz) {
+                        uint4 v = ldu16(row + pos);
+                        v = mask16(v, head - pos, min(sz, head + p) - pos);
+                        s = sum16(v, s);
+                    }
+                }
+                ps = wave_total(s);
+            }
+            if (lane == r) {
+                psz = p;
+                st = psz >= a.dec_pkt_size || head + psz > pitch ? -1
+                     : a.checksum && (ps & 0xFFFFu) != (w0 >> 16) ? -1 : head;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        if (j < pl.e && lane == (int)lane_of(pl.v_rs, K + M + j)) {
+            const uint32_t w0 = lane_of(v_w0, K + j);
+            const uint32_t ps = lane_of(v_dt, K + j) - head_bytes_sum(w0, head);
+            psz = (int)(w0 & 0xFFFF);
+            st = psz >= a.dec_pkt_size || head + psz > pitch ? -1
+                 : a.checksum && (ps & 0xFFFFu) != (w0 >> 16) ? -1 : head;
+        }
+    }
+    if (lane < K && !pl.recoverable && ((pl.lost_data >> lane) & 1u)) {
+        st = -2;
+        psz = 0;
+    }
+    if (lane < K) {
+        a.status[g * K + lane] = st;
+        a.psize[g * K + lane] = psz;
+    }
+}
+
 // ------------------------------------------------------------------ ProtocolUdp framing
 // The byte stage below FEC on every datagram:
 //   Session::PacketOutput (network/SessionDesc.cpp:69-77): mask = _mask++, push hid, push conv
@@ -1148,6 +1524,8 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
 
 #define QFEC_UNPACK_CASE(KK, MM)                                                                        \
     if (a.k == KK && a.m == MM) {                                                                       \
+        *launched = true;                                                                               \
+        if (rx) return unpack_v2_shape<KK, MM>(a, lut, records, rec_hdr, s, nva);                       \
         if (tuning().wire_rx_tail)                                                                      \
             hipLaunchKernelGGL((k_unpack_fused<KK, MM, true>), dim3(waves_grid(a.groups)), dim3(256), 0, s, a, \
                                a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);    \
@@ -1158,10 +1536,28 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
         return hipGetLastError();                                                                       \
     }
 
+// the lean single-wave receive for one (K, M): 16-B lanes (NVA 4) or 8-B lanes (NVA 2)
+template <int K, int M>
+hipError_t unpack_v2_shape(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
+                           hipStream_t s, int nva) {
+    if (nva == 4)
+        hipLaunchKernelGGL((k_unpack_v2<K, M, 4>), dim3((unsigned)((a.groups + 3) / 4)), dim3(256), 0, s, a,
+                           (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+    else
+        hipLaunchKernelGGL((k_unpack_v2<K, M, 2>), dim3((unsigned)((a.groups + 3) / 4)), dim3(256), 0, s, a,
+                           (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+    return hipGetLastError();
+}
+
 hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
                                hipStream_t s, bool* launched) {
     *launched = false;
     if (!a.groups) return hipSuccess;
+    // the workgroup-per-group path covers shard pitches up to 768 * kRxMaxWaves bytes
+    // 0: k_unpack_fused; k_unpack_v2 with 1: 16-B lanes when one pass covers the row (pitch <=
+    // 1280), else 8-B lanes (fewer VGPRs: 86 vs 124); 2: 16-B lanes; 3: 8-B lanes
+    const int rx = tuning().wire_rx_split;
+    const int nva = rx == 2 ? 4 : rx == 3 ? 2 : (a.pitch <= 1280 ? 4 : 2);
     QFEC_UNPACK_CASE(10, 3)
     QFEC_UNPACK_CASE(4, 1)
     QFEC_UNPACK_CASE(4, 2)
