@@ -1005,13 +1005,21 @@ struct RxSl {
         for (int d = NVA; d < NV; ++d)
             if (act(d)) __builtin_nontemporal_store(v[d], reinterpret_cast<uint32_t*>(row + pos(d)));
     }
-    // keep the row bytes below n
-    __device__ __forceinline__ void keep_below(uint32_t (&v)[NV], int n) const {
+    // keep the row bytes below n: in the NVA part when mask_a, in the tail dwords when mask_t
+    // (wave-uniform flags: a region that lies wholly below n is left alone)
+    __device__ __forceinline__ void keep_below(uint32_t (&v)[NV], int n, bool mask_a, bool mask_t) const {
+        if (mask_a) {
 #pragma unroll
-        for (int d = 0; d < NV; ++d) {
-            const int c = min(max(n - pos(d), 0), 4);
-            v[d] = c >= 4 ? v[d] : v[d] & ((1u << (8 * c)) - 1u);
+            for (int d = 0; d < NVA; ++d) v[d] = keep_dw(v[d], n - pos(d));
         }
+        if (NVT && mask_t) {
+#pragma unroll
+            for (int d = NVA; d < NV; ++d) v[d] = keep_dw(v[d], n - pos(d));
+        }
+    }
+    __device__ __forceinline__ static uint32_t keep_dw(uint32_t x, int nb) {  // the low nb bytes of x
+        const int c = min(max(nb, 0), 4);
+        return c >= 4 ? x : x & ((1u << (8 * c)) - 1u);
     }
 };
 
@@ -1032,7 +1040,8 @@ struct RxP {
 
 template <int K, int M, int NVA, int NVT>
 __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restrict__ wire_g, uint8_t* __restrict__ out_g,
-                                         uint64_t pitch, const RxSl<NVA, NVT>& sl, bool first, int head, int pass_end,
+                                         uint64_t pitch, const RxSl<NVA, NVT>& sl, bool first, int head, int end_a,
+                                         int end_t,
                                          uint32_t& v_w0, uint32_t (&dsum)[K], uint32_t (&xsum)[M], uint32_t (&psl)[M]) {
     constexpr int NV = NVA + NVT;
     // opaque per pass: the v_readlane results below are not carried across passes in SGPRs
@@ -1044,9 +1053,12 @@ __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restric
         for (int d = 0; d < NV; ++d) x[c][d] = 0;
         if (c < pl.ns) sl.load(x[c], wire_g + lane_of(pl.v_off, c));
     }
-    if (pass_end > pl.min_size) {  // some survivor's datagram ends inside this pass
+    // some survivor's datagram ends inside this pass: keep [0, size) (end_a / end_t: where the
+    // pass's NVA part and tail dwords end)
+    if (end_a > pl.min_size || (NVT && end_t > pl.min_size)) {
 #pragma unroll
-        for (int c = 0; c < K; ++c) sl.keep_below(x[c], (int)(lane_of(pl.v_rs, c) >> 16));
+        for (int c = 0; c < K; ++c)
+            sl.keep_below(x[c], (int)(lane_of(pl.v_rs, c) >> 16), end_a > pl.min_size, end_t > pl.min_size);
     }
 #pragma unroll
     for (int c = 0; c < K; ++c) dsum[c] += sum_vec<NV>(x[c]);
@@ -1064,7 +1076,8 @@ __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restric
             uint32_t toff = (uint32_t)(c * QFEC_TAB_STRIDE);
             asm volatile("" : "+s"(toff));  // fetch this column's tables here, not all 5 K M up front
 #pragma unroll
-            for (int j = 0; j < M; ++j) {  // records are padded to M rows: no branch on e
+            for (int j = 0; j < M; ++j) {
+                if (j >= pl.e) continue;  // only the group's e decoded rows (wave-uniform)
                 const uint32_t* t = pl.tab + toff + j * K * QFEC_TAB_STRIDE;
                 const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
 #pragma unroll
@@ -1093,7 +1106,7 @@ __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restric
         if (j < pl.e) {
             sl.store(out_g + (uint64_t)lane_of(pl.v_rs, K + M + j) * pitch, acc[j]);
             const int hi = head + (int)(lane_of(v_w0, K + j) & 0xFFFF);  // payload end of decoded row j
-            if (pass_end > hi) sl.keep_below(acc[j], hi);
+            sl.keep_below(acc[j], hi, end_a > hi, end_t > hi);
             psl[j] += sum_vec<NV>(acc[j]);
         }
     }
@@ -1101,7 +1114,8 @@ __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restric
         uint32_t z[NV];
 #pragma unroll
         for (int d = 0; d < NV; ++d) z[d] = 0;
-        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) sl.store(out_g + (uint64_t)__builtin_ctz(zr) * pitch, z);
+        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1)
+            sl.store(out_g + (uint64_t)__builtin_ctz(zr) * pitch, z);
     }
 #pragma unroll
     for (int r = 0; r < M; ++r) {
@@ -1110,7 +1124,8 @@ __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restric
 #pragma unroll
             for (int d = 0; d < NV; ++d) y[d] = 0;
             sl.load(y, wire_g + lane_of(pl.v_off, K + r));
-            if (pass_end > pl.min_xsize) sl.keep_below(y, (int)(lane_of(pl.v_rs, K + r) >> 16));
+            const int xs = (int)(lane_of(pl.v_rs, K + r) >> 16);
+            sl.keep_below(y, xs, end_a > xs, end_t > xs);
             xsum[r] += sum_vec<NV>(y);
         }
     }
@@ -1227,12 +1242,12 @@ __global__ void __launch_bounds__(256) k_unpack_v2(WireArgs a, const uint8_t* __
             const int base = A * q;
             if (fuse_tail && q == passes - 1) {
                 RxSl<NVA, 1> sl{base + 4 * NVA * lane, base + A, lane, true, pitch};
-                rx2_pass<K, M, NVA, 1>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, pitch, v_w0, dsum, xsum,
-                                       psl);
+                rx2_pass<K, M, NVA, 1>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, base + A, pitch, v_w0,
+                                              dsum, xsum, psl);
             } else {
                 RxSl<NVA, 0> sl{base + 4 * NVA * lane, 0, lane, base + 4 * NVA * lane < pitch, pitch};
-                rx2_pass<K, M, NVA, 0>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, min(pitch, base + A), v_w0,
-                                       dsum, xsum, psl);
+                rx2_pass<K, M, NVA, 0>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, min(pitch, base + A), 0,
+                                              v_w0, dsum, xsum, psl);
             }
         }
         // ---- verdicts (k_unpack_fused's rules)
@@ -1540,12 +1555,13 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
 template <int K, int M>
 hipError_t unpack_v2_shape(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
                            hipStream_t s, int nva) {
+    const dim3 grid((unsigned)((a.groups + 3) / 4)), block(256);
     if (nva == 4)
-        hipLaunchKernelGGL((k_unpack_v2<K, M, 4>), dim3((unsigned)((a.groups + 3) / 4)), dim3(256), 0, s, a,
-                           (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+        hipLaunchKernelGGL((k_unpack_v2<K, M, 4>), grid, block, 0, s, a, (const uint8_t*)a.wire,
+                           (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
     else
-        hipLaunchKernelGGL((k_unpack_v2<K, M, 2>), dim3((unsigned)((a.groups + 3) / 4)), dim3(256), 0, s, a,
-                           (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+        hipLaunchKernelGGL((k_unpack_v2<K, M, 2>), grid, block, 0, s, a, (const uint8_t*)a.wire,
+                           (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
     return hipGetLastError();
 }
 
@@ -1554,10 +1570,12 @@ hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint
     *launched = false;
     if (!a.groups) return hipSuccess;
     // the workgroup-per-group path covers shard pitches up to 768 * kRxMaxWaves bytes
-    // 0: k_unpack_fused; k_unpack_v2 with 1: 16-B lanes when one pass covers the row (pitch <=
-    // 1280), else 8-B lanes (fewer VGPRs: 86 vs 124); 2: 16-B lanes; 3: 8-B lanes
+    // 0: k_unpack_fused; k_unpack_v2 with 1: 16-B lanes when one pass covers the row with most
+    // lanes busy (768 < pitch <= 1280), else 8-B lanes (fewer VGPRs: 85 vs 119); 2: 16-B lanes;
+    // 3: 8-B lanes.  RS(10,13) x 100k, A/B on one box (r02n): 1 KiB payloads 520 us on 16-B
+    // lanes / 566 on 8-B; 1400 B 690 on 8-B / 725 on 16-B; 512 B 337 on 8-B / 411 on 16-B
     const int rx = tuning().wire_rx_split;
-    const int nva = rx == 2 ? 4 : rx == 3 ? 2 : (a.pitch <= 1280 ? 4 : 2);
+    const int nva = rx == 2 ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
     QFEC_UNPACK_CASE(10, 3)
     QFEC_UNPACK_CASE(4, 1)
     QFEC_UNPACK_CASE(4, 2)

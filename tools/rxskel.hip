@@ -119,6 +119,35 @@ __global__ void __launch_bounds__(256) k_w1lds(const uint8_t* __restrict__ wire,
         __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(L + o), reinterpret_cast<u32x4*>(og + o));
 }
 
+// w1x16t, stores: MODE 0 all plain (L2 merges the two halves of a row-boundary line), 1 plain
+// for the boundary lines only (each row's first 64 B and its tail dwords), nt elsewhere
+template <int MODE>
+__global__ void __launch_bounds__(256) k_w1x16t_st(const uint8_t* __restrict__ wire, uint8_t* __restrict__ out,
+                                                   uint64_t groups, int wp, int pitch, int hdr) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= groups) return;
+    const uint8_t* wg = wire + g * N * (uint64_t)wp + hdr;
+    uint8_t* og = out + g * N * (uint64_t)pitch;
+    const int pa = 16 * lane, pt = 1024 + 4 * lane;
+    u32x4 x[K];
+    uint32_t t[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        if (pa < pitch) __builtin_memcpy(&x[c], wg + (uint64_t)c * wp + pa, 16);
+        if (pt < pitch) __builtin_memcpy(&t[c], wg + (uint64_t)c * wp + pt, 4);
+    }
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        u32x4* d = reinterpret_cast<u32x4*>(og + (uint64_t)c * pitch + pa);
+        if (pa < pitch) {
+            if (MODE == 0 || lane < 4) *d = x[c];
+            else __builtin_nontemporal_store(x[c], d);
+        }
+        if (pt < pitch) *reinterpret_cast<uint32_t*>(og + (uint64_t)c * pitch + pt) = t[c];
+    }
+}
+
 // lanes flat over (group, row, 16-B chunk)
 __global__ void __launch_bounds__(256) k_flat(const uint8_t* __restrict__ wire, uint8_t* __restrict__ out,
                                               uint64_t items, int wp, int pitch, int hdr, int cpr) {
@@ -148,12 +177,14 @@ int main() {
         const double bytes = 2.0 * G * K * pitch;  // (pitch 1088 / 1472: 64-B aligned rows, more bytes)
         for (int round = 0; round < 2; ++round) {
             for (int hdr : {13}) {
-                for (int v = 0; v < 5; ++v) {
+                for (int v = 0; v < 7; ++v) {
                     const unsigned W = (pitch + 767) / 768;
                     const int cpr = pitch / 16;
                     auto launch = [&]() {
                         if (v == 0) k_w2x8<<<(unsigned)G, 64 * W>>>(wire, out, wp, pitch, hdr);
                         else if (v == 1) k_w1x16<<<(unsigned)((G + 3) / 4), 256>>>(wire, out, G, wp, pitch, hdr);
+                        else if (v == 5) k_w1x16t_st<0><<<(unsigned)((G + 3) / 4), 256>>>(wire, out, G, wp, pitch, hdr);
+                        else if (v == 6) k_w1x16t_st<1><<<(unsigned)((G + 3) / 4), 256>>>(wire, out, G, wp, pitch, hdr);
                         else if (v == 4) k_w1lds<<<(unsigned)((G + 3) / 4), 256, 4 * K * pitch>>>(wire, out, G, wp, pitch, hdr);
                         else if (v == 3) k_w1x16t<<<(unsigned)((G + 3) / 4), 256>>>(wire, out, G, wp, pitch, hdr);
                         else k_flat<<<(unsigned)((G * K * cpr + 255) / 256), 256>>>(wire, out, G * K * cpr, wp, pitch, hdr, cpr);
@@ -166,7 +197,7 @@ int main() {
                     float ms = 0;
                     CHECK(hipEventElapsedTime(&ms, a, b));
                     ms /= 20;
-                    const char* names[5] = {"w2x8 ", "w1x16", "flat ", "w1x16t", "w1lds"};
+                    const char* names[7] = {"w2x8 ", "w1x16", "flat ", "w1x16t", "w1lds", "w1x16t-plain", "w1x16t-edgeplain"};
                     if (round == 1)
                         printf("pitch %4d hdr %2d %s %8.1f us  %7.1f GB/s (read + write)\n", pitch, hdr, names[v],
                                ms * 1e3, bytes / (ms * 1e-3) / 1e9);
