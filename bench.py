@@ -493,6 +493,68 @@ def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=2
     return out
 
 
+def per_call_leg(reps=2000, ref_lib=None):
+    """The unchanged drop-in's per-call cost: what network/FecCodecBuf.cpp pays per
+    packet when it links libqfec instead of system/fec.c.  RS(10,3) with 1 KiB payloads:
+      fec_encode  one parity packet, sz = 1028 (get_fec_encoded_pkt, FecCodecBuf.cpp:151)
+      fec_decode  3 data packets lost, slots in NetFecCodec order (fec_decode_pkts, :204)
+    timed per call on the GPU path, plus the batched host-buffer encode (qfec_encode_host) at
+    growing batch sizes; with ref_lib (the cpu_baseline leg only) the same calls on the
+    reference's own system/fec.c (oracle/_ref, CPU, 1 thread)."""
+    import ctypes as C
+    k, n, sz = 10, 13, 1028
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, (n, sz), dtype=np.uint8)
+    idx_t = [0, 1, 2, 4, 5, 7, 8, 10, 11, 12]  # data 3, 6, 9 lost; the first k valid rows
+    out = {"shape": "RS(10,3), sz 1028 B per packet"}
+
+    def run(lib, tag):
+        h = C.c_void_p(lib.fec_new(k, n))
+        src = (C.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
+        dst = np.zeros(sz, np.uint8)
+        pk_t = (C.c_void_p * k)(*[data[i].ctypes.data for i in idx_t])
+        pk = (C.c_void_p * k)()
+        ix = (C.c_int * k)()
+        ix_t = (C.c_int * k)(*idx_t)
+
+        def enc():
+            lib.fec_encode(h, src, C.c_void_p(dst.ctypes.data), k, sz)
+
+        def dec():
+            C.memmove(pk, pk_t, C.sizeof(pk))
+            C.memmove(ix, ix_t, C.sizeof(ix))
+            lib.fec_decode(h, pk, ix, sz)
+
+        for f, name in ((enc, "fec_encode_us"), (dec, "fec_decode_us")):
+            for _ in range(50):
+                f()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                f()
+            out[f"{tag}{name}"] = round((time.perf_counter() - t0) / reps * 1e6, 2)
+        lib.fec_free(h)
+
+    if ref_lib is not None:  # the cpu_baseline leg's reference system/fec.c
+        run(ref_lib, "ref_cpu_")
+        return out
+    run(qa.lib(), "gpu_")
+    # batched: qfec_encode_host (pinned host buffers in and out) per group vs 3 reference calls
+    code = qa.Code.vandermonde(k, n - k)
+    batch = []
+    for G in (1, 4, 16, 64, 256, 1024):
+        hd = torch.from_numpy(rng.integers(0, 256, (G, k, 1040), dtype=np.uint8)).pin_memory()
+        hp = torch.empty((G, n - k, 1040), dtype=torch.uint8).pin_memory()
+        for _ in range(5):
+            code.encode_host(hd, hp, sz)
+        r = max(3, min(200, 2000 // G))
+        t0 = time.perf_counter()
+        for _ in range(r):
+            code.encode_host(hd, hp, sz)
+        batch.append({"groups": G, "us_per_group": round((time.perf_counter() - t0) / r / G * 1e6, 3)})
+    out["batched_encode_host"] = batch
+    return out
+
+
 def load_traffic(path, workload_key):
     """PMC bytes per launch for this workload from profiles/traffic.json, or None when absent
     or measured on other kernel sources (the file records their sha256)."""
@@ -661,6 +723,13 @@ def main(argv=None):
             host_line = host_encode_leg(code, data, parity, B)
             ok = ok and bool(host_line.get("verified"))
 
+    per_call = None
+    if rank == 0 and not args.no_host:
+        try:
+            per_call = per_call_leg()
+        except Exception as exc:  # report, never fake
+            per_call = {"error": repr(exc)}
+
     side = None
     if rank == 0 and not args.no_side:
         side = [side_config(fl, sk, sm, sB, sG, sE, rank) for fl, sk, sm, sB, sG, sE in SIDE]
@@ -681,6 +750,16 @@ def main(argv=None):
             cpu["config0"] = cpu_config0(args.cpu_seconds / 5)
         except Exception as exc:
             cpu["config0"] = {"error": repr(exc)}
+        try:  # the reference's per-packet calls, beside the GPU drop-in's (per_call)
+            from oracle.oracle import RefCodec
+            if RefCodec.available():
+                cpu["per_call"] = per_call_leg(ref_lib=RefCodec().fec)
+                if isinstance(per_call, dict) and "batched_encode_host" in per_call:
+                    ref3 = 3 * cpu["per_call"]["ref_cpu_fec_encode_us"]
+                    beat = [b["groups"] for b in per_call["batched_encode_host"] if b["us_per_group"] < ref3]
+                    per_call["batch_beats_reference_encode_at_groups"] = beat[0] if beat else None
+        except Exception as exc:
+            cpu["per_call"] = {"error": repr(exc)}
         # the reference's datagram pipeline (FecCodecBuf.cpp + system/fec.c, oracle/_ref),
         # RS(10,13) 1 KiB payloads, send + receive, 1 thread: the CPU side of DESIGN 3.5
         ref_wire = os.path.join(ROOT, "oracle", "_ref", "ref_wire_bench")
@@ -724,6 +803,7 @@ def main(argv=None):
             "config4": config4,
             "host_to_host_mixed": host_mixed,
             "host_to_host_encode": host_line,
+            "per_call": per_call,
             "verified": ok,
             "cpu_baseline": cpu,
             "cpu_baseline_threads": cpu_mt,

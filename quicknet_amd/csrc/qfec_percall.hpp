@@ -1,0 +1,26 @@
+// qfec_percall.hpp -- the per-packet ABI's (fec_encode / fec_decode, system/fec.h) low-latency
+// kernel: one launch, no DMA copies.  The caller's packets are staged by the CPU into pinned,
+// device-mapped host memory; the kernel reads them over PCIe, multiplies by the decode/encode
+// rows (perm tables passed BY VALUE in the kernel arguments), and writes the outputs back into
+// pinned memory.  Used when e * k <= kPcMaxCoef.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qfec {
+
+constexpr int kPcMaxCoef = 160;  // e * k coefficients: 5 dwords each in the kernarg (3.2 KB)
+
+struct PcArgs {
+    const uint8_t* in;   // k rows of `pitch` bytes (pinned host, device-mapped)
+    uint8_t* out;        // e rows of `pitch` bytes (pinned host, device-mapped)
+    uint32_t pitch;      // multiple of 16
+    uint32_t chunks;     // 16-B chunks per row to compute
+    uint32_t k, e;
+    uint32_t tab[kPcMaxCoef * 5];  // [e][k] perm tables (5 dwords: QFEC_TAB_STRIDE's first 5)
+};
+
+hipError_t launch_percall(const PcArgs& a, hipStream_t s);
+
+}  // namespace qfec

@@ -34,6 +34,7 @@
 #include "../../include/qfec_fec.h"
 #include "../../include/qfec_rs.h"
 #include "qfec_internal.hpp"
+#include "qfec_percall.hpp"
 
 #define QFEC_VERSION_STRING "qfec 0.1.0 (gfx950)"
 
@@ -65,6 +66,7 @@ int hip_fail(hipError_t e, const char* what) {
     } while (0)
 
 std::atomic<int> g_variant{QFEC_VARIANT_PERM};
+std::atomic<int> g_percall_fast{1};  // qfec_tune "percall_fast": fec_encode / fec_decode via k_percall
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -84,6 +86,11 @@ struct DevCtx {
     size_t small_cap = 0;
     uint32_t* h_small = nullptr; // pinned mirror
     unsigned* d_counter = nullptr;
+    // per-packet calls (fec_encode / fec_decode): pinned, device-mapped staging the
+    // k_percall kernel reads and writes directly (qfec_percall.hpp)
+    uint8_t* h_pc = nullptr;
+    uint8_t* d_pc = nullptr;  // the device address of h_pc
+    size_t pc_cap = 0;
     int init_rc = QFEC_ENODEV;
     // qfec_encode_host: two chunk slots, each with its own stream, event, device buffers
     // and pinned staging (created on first use)
@@ -159,6 +166,18 @@ int ensure_stage(DevCtx& c, size_t dbytes, size_t hbytes) {
         HIP_TRY(hipHostMalloc(&c.h_stage, cap, hipHostMallocDefault));
         c.h_cap = cap;
     }
+    return QFEC_OK;
+}
+
+int ensure_pc(DevCtx& c, size_t bytes) {
+    if (bytes <= c.pc_cap) return QFEC_OK;
+    if (c.h_pc) HIP_TRY(hipHostFree(c.h_pc));
+    c.h_pc = c.d_pc = nullptr;
+    c.pc_cap = 0;
+    const size_t cap = round_up(std::max(bytes, (size_t)1 << 16), 1 << 16);
+    HIP_TRY(hipHostMalloc(&c.h_pc, cap, hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&c.d_pc, c.h_pc, 0));
+    c.pc_cap = cap;
     return QFEC_OK;
 }
 
@@ -590,6 +609,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
 }
@@ -1635,6 +1655,24 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
     const bool dev = is_device_ptr(in[0]);
     const size_t pitch = round_up((size_t)sz, 16);
     std::lock_guard<std::mutex> lk(ctx->mu);
+    if (!dev && k * e <= kPcMaxCoef && g_percall_fast.load() && !is_device_ptr(out[0])) {
+        // host packets: CPU staging into mapped pinned memory, one launch, one synchronise
+        if ((rc = ensure_pc(*ctx, (size_t)(k + e) * pitch))) return rc;
+        for (int c = 0; c < k; ++c) memcpy(ctx->h_pc + (size_t)c * pitch, in[c], (size_t)sz);
+        PcArgs a;
+        a.in = ctx->d_pc;
+        a.out = ctx->d_pc + (size_t)k * pitch;
+        a.pitch = (uint32_t)pitch;
+        a.chunks = (uint32_t)(pitch / 16);
+        a.k = (uint32_t)k;
+        a.e = (uint32_t)e;
+        for (int i = 0; i < k * e; ++i) memcpy(&a.tab[i * 5], &tab[(size_t)i * QFEC_TAB_STRIDE], 5 * sizeof(uint32_t));
+        hipError_t he = launch_percall(a, ctx->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+        if (he != hipSuccess) return hip_fail(he, "per-call kernel");
+        for (int j = 0; j < e; ++j) memcpy(out[j], ctx->h_pc + (size_t)(k + j) * pitch, (size_t)sz);
+        return QFEC_OK;
+    }
     if ((rc = ensure_small(*ctx, tab.size()))) return rc;
     const size_t ib = (size_t)k * pitch, ob = (size_t)e * pitch;
     if ((rc = ensure_stage(*ctx, ib + ob, ib + ob))) return rc;

@@ -197,3 +197,42 @@ def test_two_ranks_share_gpu_match_single(oracle):
     oracle.rs_encode(qa.Code.cauchy(k, m).rows, data, ref, B)
     assert b"".join(x[0] for x in out) == ref.tobytes()
     assert all(x[1] for x in out)  # every rank's reconstruct restored its slice
+
+
+@pytest.mark.parametrize("fast", [1, 0])
+@pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 37), (3, 5, 2052), (16, 20, 1400)])
+def test_per_packet_paths_vs_oracle(oracle, fast, k, n, sz):
+    """fec_encode / fec_decode on host packets through the per-call kernel (percall_fast 1:
+    mapped pinned staging, tables in the kernel arguments, one launch) and through the staged
+    DMA path (0), against the oracle's fec.c restatement."""
+    rng = np.random.default_rng(k * 100 + sz)
+    fp = qa.FecParms(k, n)
+    full = fp.matrix
+    data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    qa.tune("percall_fast", fast)
+    try:
+        for idx in range(k, n):
+            dst = np.zeros(sz, np.uint8)
+            fp.encode(data, dst, idx, sz)
+            exp = np.zeros(sz, np.uint8)
+            for c in range(k):
+                exp ^= _gf_row(oracle, int(full[idx, c]), data[c])
+            assert np.array_equal(dst, exp)
+        # decode: the first min(n - k, k) data packets lost, the first k valid ones in group order
+        coded = np.concatenate([data, np.zeros((n - k, sz), np.uint8)])
+        for idx in range(k, n):
+            fp.encode(data, coded[idx], idx, sz)
+        keep = sorted(set(range(n)) - set(range(min(n - k, k))))[:k]
+        rc, pk, ix = fp.decode(coded[keep], keep, sz)
+        rc2, pk2, ix2 = oracle.fec_decode(k, n, full, coded[keep], keep)
+        assert rc == rc2 == 0
+        assert np.array_equal(pk, pk2) and np.array_equal(ix, ix2)
+        assert np.array_equal(pk, data)
+    finally:
+        qa.tune("percall_fast", 1)
+
+
+def _gf_row(oracle, c, row):
+    """c * row over GF(2^8) via the oracle's multiplication table (256 products, then a gather)."""
+    t = np.array([oracle.mul(c, b) for b in range(256)], np.uint8)
+    return t[row]

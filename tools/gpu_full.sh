@@ -12,7 +12,7 @@ R=$GRAFT_REPO_ROOT
 echo "== pytest -m gpu" && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 2; }
 tail -1 $OUT/pytest_gpu.log
 echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 3; }
-echo "== PMC traffic" && timeout -k 10 900 python tools/pmc_traffic.py --out $OUT/pmc --json $OUT/traffic.json > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 6; }
+echo "== PMC traffic" && timeout -k 10 900 python tools/pmc_traffic.py --out $OUT/pmc --json $OUT/traffic.json --tag $TAG > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 6; }
 cp $OUT/traffic.json profiles/traffic.json  # bench.py reads roofline.traffic from here
 echo "== bench" && timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 4; }
 cat $OUT/bench.json
@@ -20,6 +20,6 @@ echo "== rocprofv3 kernel trace" && (cd /tmp && timeout -k 10 600 rocprofv3 --ke
   -d $R/$OUT/prof -o trace -- python3 $R/bench.py --no-cpu > $R/$OUT/bench_prof.json 2> $R/$OUT/prof.err) || { tail -20 $OUT/prof.err; exit 5; }
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 cut -d, -f1-4 $OUT/kernel_stats.csv | head -6
-echo "== A/B" && timeout -k 10 600 python tools/ab.py > $OUT/ab.log 2>&1 || { tail -20 $OUT/ab.log; exit 7; }
-cat $OUT/ab.log
+echo "== bench --gpus 2 (gloo rehearsal: the launcher's own ranks share the one GPU)" && QFEC_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 --no-cpu > $OUT/bench_g2.json 2> $OUT/bench_g2.err || { tail -20 $OUT/bench_g2.err; exit 7; }
+cut -c1-400 $OUT/bench_g2.json
 echo done

@@ -21,10 +21,10 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"encode": "k_encode_perm<", "reconstruct": "k_reconstruct_perm<", "probe": "k_probe_xor"}
+KERNELS = {"encode": "k_encode_perm<{k}, {m}>", "reconstruct": "k_reconstruct_perm<{k}, {m},", "probe": "k_probe_xor"}
 
 
-def run_pass(counter, out, bench_args):
+def run_pass(counter, out, bench_args, k, m):
     d = os.path.abspath(os.path.join(out, counter.lower()))
     os.makedirs(d, exist_ok=True)
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", counter.lower(), "--",
@@ -43,7 +43,7 @@ def run_pass(counter, out, bench_args):
                     continue
                 name = row.get("Kernel_Name", "")
                 for key, pat in KERNELS.items():
-                    if pat in name:
+                    if pat.format(k=k, m=m) in name:
                         per[key].append(float(row["Counter_Value"]))
     return per
 
@@ -59,9 +59,9 @@ def main():
     p.add_argument("--tag", default="PMC run", help="which run produced the numbers (recorded in the JSON)")
     a = p.parse_args()
     bench_args = ["--steps", "5", "--warmup", "1", "--k", str(a.k), "--m", str(a.m), "--block", str(a.block),
-                  "--groups", str(a.groups), "--no-side"]
-    fetch = run_pass("FETCH_SIZE", a.out, bench_args)
-    write = run_pass("WRITE_SIZE", a.out, bench_args)
+                  "--groups", str(a.groups), "--no-side", "--no-config4", "--no-host"]
+    fetch = run_pass("FETCH_SIZE", a.out, bench_args, a.k, a.m)
+    write = run_pass("WRITE_SIZE", a.out, bench_args, a.k, a.m)
     k, m, B, G = a.k, a.m, a.block, a.groups
     probe_alg_read, probe_alg_write = k * B * G, m * B * G
     res = {}
