@@ -24,6 +24,9 @@ EXPORTS = {
                "qfec_last_error", "qfec_version"],
     "qfec_net.h": ["qfec_net_new", "qfec_net_free", "qfec_net_session", "qfec_net_enable", "qfec_net_pack_input", "qfec_net_flush_pack",
                    "qfec_net_unpack_input", "qfec_net_flush_unpack", "qfec_net_stats"],
+    "qfec_zfec.h": ["qfec_zfec_new", "qfec_zfec_free", "qfec_zfec_session", "qfec_zfec_set_kn", "qfec_zfec_enable",
+                    "qfec_zfec_sorted", "qfec_zfec_dynkn", "qfec_zfec_lost_rate", "qfec_zfec_pack_input",
+                    "qfec_zfec_unpack_input", "qfec_zfec_flush", "qfec_zfec_stats"],
 }
 
 QFEC_CAUCHY = 0
@@ -103,11 +106,39 @@ def lib():
         "reed_solomon_reconstruct": (i, [C.POINTER(RSStruct), C.POINTER(vp), vp, i, i]),
         "reed_solomon_error": (i, []),
     }
+    sig.update(ZFEC_SIG)
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
     _lib = L
+    return L
+
+
+_vp, _i = C.c_void_p, C.c_int
+ZFEC_SIG = {  # include/qfec_zfec.h
+    "qfec_zfec_new": (_vp, []),
+    "qfec_zfec_free": (None, [_vp]),
+    "qfec_zfec_session": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i]),
+    "qfec_zfec_set_kn": (_i, [_vp, _i, _i, _i, _i]),
+    "qfec_zfec_enable": (_i, [_vp, _i, _i]),
+    "qfec_zfec_sorted": (_i, [_vp, _i, _i]),
+    "qfec_zfec_dynkn": (_i, [_vp, _i, _i]),
+    "qfec_zfec_lost_rate": (_i, [_vp, _i, C.c_float]),
+    "qfec_zfec_pack_input": (_i, [_vp, _i, _vp, C.c_uint]),
+    "qfec_zfec_unpack_input": (_i, [_vp, _i, _vp, C.c_uint]),
+    "qfec_zfec_flush": (_i, [_vp, _vp, _vp, _vp]),
+    "qfec_zfec_stats": (_i, [_vp, _i, _vp]),
+}
+
+
+def bind_zfec(L):
+    """Declare include/qfec_zfec.h's signatures on another build of the layer (the CPU suite's
+    host-only build, tests/zfec_host)."""
+    for name, (res, args) in ZFEC_SIG.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
     return L
 
 

@@ -18,7 +18,7 @@ from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
 
 __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
            "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count", "frame_udp", "unframe_udp",
-           "NetFec", "Pipe"]
+           "NetFec", "Pipe", "Zfec"]
 
 
 def _stream_handle(stream):
@@ -454,6 +454,87 @@ class NetFec:
         check(lib().qfec_net_stats(self._h, a), "qfec_net_stats")
         keys = ["groups_packed", "datagrams_out", "groups_unpacked", "delivered", "recovered", "undecodable",
                 "foreign", "late"]
+        return dict(zip(keys, list(a)))
+
+
+class Zfec:
+    """The exact NetFecCodec layer (include/qfec_zfec.h): per-session calls are queued in call
+    order and flush() runs them through the reference's zfec_pack_input / zfec_unpack_input
+    state machines, all byte work in batched device launches.  flush() returns
+    (datagrams, deliveries): [(session, bytes)] and [(session, payload, src index)], each
+    session's in the order the reference's PackOutput / UnpackOutput would have seen them."""
+
+    def __init__(self, _lib=None):
+        self._L = _lib or lib()  # (_lib: another build of the layer, for the CPU suite)
+        self._h = self._L.qfec_zfec_new()
+        if not self._h:
+            raise QfecError("qfec_zfec_new failed")
+        self._nsess = 0
+
+    def close(self):
+        if self._h:
+            self._L.qfec_zfec_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def session(self, max_pkt_size=2048, buf_items=48, kmax=10, k=4, n=5, enabled=True, is_sorted=False):
+        """FecTransmission::Init (CreateFecTransmission's defaults); the callback peer is id + 1."""
+        s = self._L.qfec_zfec_session(self._h, C.c_void_p(self._nsess + 1), max_pkt_size, buf_items, kmax, k, n,
+                                    int(bool(enabled)), int(bool(is_sorted)))
+        check(min(s, 0), "qfec_zfec_session")
+        self._nsess += 1
+        return s
+
+    def set_kn(self, session, k, n, add_new=True):
+        rc = self._L.qfec_zfec_set_kn(self._h, session, k, n, int(bool(add_new)))
+        check(rc, f"qfec_zfec_set_kn({k}, {n})")
+
+    def enable(self, session, on=True):
+        check(self._L.qfec_zfec_enable(self._h, session, int(bool(on))), "qfec_zfec_enable")
+
+    def sorted(self, session, on=True):
+        check(self._L.qfec_zfec_sorted(self._h, session, int(bool(on))), "qfec_zfec_sorted")
+
+    def dynkn(self, session, on=True):
+        check(self._L.qfec_zfec_dynkn(self._h, session, int(bool(on))), "qfec_zfec_dynkn")
+
+    def lost_rate(self, session, rate):
+        check(self._L.qfec_zfec_lost_rate(self._h, session, float(rate)), "qfec_zfec_lost_rate")
+
+    def pack_input(self, session, data):
+        b = bytes(data)
+        check(self._L.qfec_zfec_pack_input(self._h, session, b, len(b)), "qfec_zfec_pack_input")
+
+    def unpack_input(self, session, datagram):
+        b = bytes(datagram)
+        check(self._L.qfec_zfec_unpack_input(self._h, session, b, len(b)), "qfec_zfec_unpack_input")
+
+    def flush(self, stream=None):
+        sent, got = [], []
+
+        def pcb(peer, p, size):
+            sent.append((int(peer) - 1, C.string_at(p, size)))
+            return 0
+
+        def ucb(peer, p, size, src):
+            got.append((int(peer) - 1, C.string_at(p, size), src))
+            return 0
+
+        f, g = _PACK_OUT(pcb), _UNPACK_OUT(ucb)
+        rc = self._L.qfec_zfec_flush(self._h, f, g, _stream_handle(stream))
+        check(min(rc, 0), "qfec_zfec_flush")
+        return sent, got
+
+    def stats(self, session):
+        a = (C.c_longlong * 8)()
+        check(self._L.qfec_zfec_stats(self._h, session, a), "qfec_zfec_stats")
+        keys = ["fec_src_count", "fec_restore_count", "i_sent_pkt", "i_recv_pkt", "i_expected_packet", "k", "n",
+                "undefined"]
         return dict(zip(keys, list(a)))
 
 

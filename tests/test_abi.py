@@ -22,7 +22,7 @@ def header_functions(path):
     return sorted(set(n for n in names if n not in ("defined",)))
 
 
-@pytest.mark.parametrize("header", ["qfec.h", "qfec_fec.h", "qfec_rs.h", "qfec_net.h"])
+@pytest.mark.parametrize("header", ["qfec.h", "qfec_fec.h", "qfec_rs.h", "qfec_net.h", "qfec_zfec.h"])
 def test_exports_match_headers(header):
     L = lib()
     declared = header_functions(os.path.join(ROOT, "include", header))
