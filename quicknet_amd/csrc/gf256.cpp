@@ -189,7 +189,8 @@ RecordLayout record_layout(int k, int m) {
     RecordLayout L;
     L.surv_off = 4;
     L.lost_off = 4 + k;
-    L.hdr = (4 + k + m + 7) & ~7;
+    L.coff = (4 + k + m + 7) & ~7;
+    L.hdr = (L.coff + m * k + 7) & ~7;
     return L;
 }
 
@@ -203,11 +204,15 @@ void build_record(const RecordLayout& L, int k, int e, const uint8_t* rows, cons
         for (int c = 0; c < k; ++c) {
             uint32_t* t = out + L.hdr + ((size_t)j * k + c) * QFEC_TAB_STRIDE;
             perm_entry(rows[(size_t)j * k + c], t);
+            out[L.coff + j * k + c] = (uint32_t)rows[(size_t)j * k + c] * (QFEC_TAB_STRIDE * 4);
         }
     // module/rs.c:116-117: a zero column-0 coefficient leaves the output's bytes in place
     if (rs_quirk)
         for (int j = 0; j < e; ++j)
-            if (rows[(size_t)j * k] == 0) out[L.hdr + ((size_t)j * k) * QFEC_TAB_STRIDE + 5] = 1;
+            if (rows[(size_t)j * k] == 0) {
+                out[L.hdr + ((size_t)j * k) * QFEC_TAB_STRIDE + 5] = 1;
+                out[L.coff + j * k] |= 1u;
+            }
 }
 
 }  // namespace qfec

@@ -61,6 +61,9 @@ struct ReconArgs {
     uint32_t cols;            // 16-B columns (vec16) or bytes per row
     int k, m;
     int surv_off, lost_off, hdr;
+    int coff;                 // record word of the coefficient-table byte offsets (RecordLayout::coff)
+    const uint32_t* t256;     // [256][QFEC_TAB_STRIDE] perm tables of every coefficient value (compact mode)
+    int compact;              // tuning "recon_compact": tables via t256 + the record's offsets
     int vec16;
     int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once,
                               // 2 exact-e rows (16-B lanes), 3 exact-e rows (8-B lanes)
@@ -128,6 +131,8 @@ struct Tuning {
     int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
     int wire_chunk = 0;     // fused send: groups per body + head launch pair (0: as many as fit)
     int host_chunk = 0;     // qfec_encode_host: groups per pipelined chunk (0: ~32 MiB of data)
+    int recon_full_lines = 1;  // 8-/12-B reconstruct lanes cover the 16-B columns' span (no partial 64-B lines)
+    int recon_compact = 1;  // LUT reconstruct reads coefficient tables via the record's offsets + t256
     int wire_rx_split = 1;  // fused receive: k_unpack_v2 (1 auto lanes, 2 16-B, 3 8-B); 0 k_unpack_fused
 };
 Tuning& tuning();
@@ -163,8 +168,13 @@ void perm_entry(uint8_t c, uint32_t* out8);
 int decode_rows(const uint8_t* parity_rows, int k, int m, const uint8_t* marks_n,
                 std::vector<uint8_t>& rows, std::vector<int>& survivors, std::vector<int>& lost);
 
+// Record: [0] e, [surv_off + c] survivor shard id, [lost_off + j] erased data row,
+// [coff + j*k + c] byte offset of coefficient (j, c)'s perm table in the 256-entry table
+// (c * 32; bit 0 on column 0 = the rs.c quirk flag), then from [hdr] the tables themselves
+// ([j][c][QFEC_TAB_STRIDE]).  A kernel that reads the offsets touches only the record's
+// first (coff + m*k) words, so the records of every pattern stay cache-resident.
 struct RecordLayout {
-    int surv_off, lost_off, hdr;
+    int surv_off, lost_off, coff, hdr;
     size_t words(int e, int k) const { return (size_t)hdr + (size_t)e * k * QFEC_TAB_STRIDE; }
 };
 RecordLayout record_layout(int k, int m);

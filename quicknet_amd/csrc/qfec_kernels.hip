@@ -231,8 +231,10 @@ __global__ void __launch_bounds__(256) k_encode_ldslog(EncodeArgs a) {
 // host-built LUT to a decode record: e, stale mask, survivor shard ids, erased data ids,
 // then e x k perm tables (gf256.cpp: build_decode_record).  In explicit mode the host
 // supplies the record offset per group instead (n > 24 or host-side marks).
-// Record: [0] e, [surv_off + c] survivor shard id (0..n-1), [lost_off + j] erased data
-// index, [hdr + (j*k + c)*QFEC_TAB_STRIDE] perm table; dword 5 of (j, 0) = stale flag.
+// Record (RecordLayout, qfec_internal.hpp): [0] e, [surv_off + c] survivor shard id (0..n-1),
+// [lost_off + j] erased data index, [coff + j*k + c] byte offset of the coefficient's table in
+// the 256-entry table (bit 0 on column 0 = stale flag), [hdr + (j*k + c)*QFEC_TAB_STRIDE] perm
+// table; dword 5 of (j, 0) = stale flag.
 
 __device__ __forceinline__ const uint8_t* shard_ptr(const ReconArgs& a, uint64_t g, uint32_t s) {
     return s < (uint32_t)a.k ? a.data + g * a.dgs + (uint64_t)s * a.pitch
@@ -382,10 +384,32 @@ __device__ __forceinline__ void ldv_plain(uint32_t (&v)[D], const uint8_t* p) {
     for (int d = 0; d < D; ++d) v[d] = reinterpret_cast<const uint32_t*>(p)[d];
 }
 
-template <int K, int E, int D>
+// where a decode record's coefficient tables are: in the record itself (the tables follow
+// its header), or -- compact -- in the 256-entry table of every coefficient value, at the
+// byte offsets the record's header lists (RecordLayout::coff).  The compact form reads only
+// the record's header, so the records of all patterns stay cache-resident (RS(16,4): 4 844
+// records of 2.4 KB would not fit the 4 MB L2; their headers do).
+template <bool CT>
+struct RTab;
+template <>
+struct RTab<false> {
+    const uint32_t* __restrict__ tab;
+    __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const { return tab + (j * K + c) * QFEC_TAB_STRIDE; }
+    __device__ __forceinline__ bool quirk(int j, int K) const { return tab[(j * K) * QFEC_TAB_STRIDE + 5] != 0; }
+};
+template <>
+struct RTab<true> {
+    const uint32_t* __restrict__ offs;
+    const uint32_t* __restrict__ t256;
+    __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const {
+        return reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t256) + (offs[j * K + c] & ~31u));
+    }
+    __device__ __forceinline__ bool quirk(int j, int K) const { return (offs[j * K] & 1u) != 0; }
+};
+
+template <int K, int E, int D, class TT>
 __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                               uint64_t lost_bits, const uint32_t* __restrict__ tab,
-                                               uint64_t pitch, uint64_t off) {
+                                               uint64_t lost_bits, const TT& T, uint64_t pitch, uint64_t off) {
     uint32_t x[K][D];
 #pragma unroll
     for (int c = 0; c < K; ++c) ldv<D>(x[c], src[c] + off);
@@ -398,7 +422,7 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
         dst[j] = data_g + (uint64_t)l * pitch + off;
 #pragma unroll
         for (int d = 0; d < D; ++d) acc[j][d] = 0;
-        if (tab[(j * K) * QFEC_TAB_STRIDE + 5]) ldv_plain<D>(acc[j], dst[j]);  // rs.c column-0 quirk
+        if (T.quirk(j, K)) ldv_plain<D>(acc[j], dst[j]);  // rs.c column-0 quirk
     }
 #pragma unroll
     for (int c = 0; c + 1 < K; c += 2) {
@@ -407,8 +431,8 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
         for (int d = 0; d < D; ++d) { sa[d] = gf_sel(x[c][d]); sb[d] = gf_sel(x[c + 1][d]); }
 #pragma unroll
         for (int j = 0; j < E; ++j) {
-            const uint32_t* ta = tab + (j * K + c) * QFEC_TAB_STRIDE;
-            const uint32_t* tb = ta + QFEC_TAB_STRIDE;
+            const uint32_t* ta = T.at(j, c, K);
+            const uint32_t* tb = T.at(j, c + 1, K);
             uint32_t a5[5], b5[5];
 #pragma unroll
             for (int i = 0; i < 5; ++i) { a5[i] = ta[i]; b5[i] = tb[i]; }
@@ -422,7 +446,7 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
         for (int d = 0; d < D; ++d) sl[d] = gf_sel(x[K - 1][d]);
 #pragma unroll
         for (int j = 0; j < E; ++j) {
-            const uint32_t* t = tab + (j * K + K - 1) * QFEC_TAB_STRIDE;
+            const uint32_t* t = T.at(j, K - 1, K);
 #pragma unroll
             for (int d = 0; d < D; ++d)
                 acc[j][d] = xor3(acc[j][d], pp0(sl[d], t[0], t[1]), pp1(sl[d], t[2], t[3])) ^ pp2(sl[d], t[4]);
@@ -433,17 +457,16 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
 }
 
 // wave-uniform dispatch on e to the exact-row-count body
-template <int K, int M, int D, int E = M>
+template <int K, int M, int D, class TT, int E = M>
 __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                                  uint64_t lost_bits, const uint32_t* __restrict__ tab, int e,
-                                                  uint64_t pitch, uint64_t off) {
+                                                  uint64_t lost_bits, const TT& T, int e, uint64_t pitch, uint64_t off) {
     if constexpr (E > 1) {
         if (e < E) {
-            recon_column_by_e<K, M, D, E - 1>(src, data_g, lost_bits, tab, e, pitch, off);
+            recon_column_by_e<K, M, D, TT, E - 1>(src, data_g, lost_bits, T, e, pitch, off);
             return;
         }
     }
-    recon_column_e<K, E, D>(src, data_g, lost_bits, tab, pitch, off);
+    recon_column_e<K, E, D>(src, data_g, lost_bits, T, pitch, off);
 }
 
 // LUT mode, compile-time K, M.  The survivor set follows from the erasure mask alone --
@@ -452,7 +475,7 @@ __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K]
 // while the decode record (coefficients only) is still in flight.
 // One wave per 64 16-B columns of a group: a group of `cols` columns gets
 // wpg = ceil(cols / 64) waves (B = 1400 -> 2), all in flight together, no column loop.
-template <int K, int M, int IMPL>
+template <int K, int M, int IMPL, bool CT>
 __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ parity,
                                                           const uint8_t* __restrict__ marks,
@@ -481,6 +504,8 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     }
     const int rec = __builtin_amdgcn_readfirstlane(lut[mask]);
     const uint32_t* tab = records + rec + a.hdr;
+    const RTab<false> TD{tab};
+    const RTab<true> TC{records + rec + a.coff, a.t256};
     const uint64_t pitch = a.pitch;
     uint8_t* data_g = data + g * a.dgs;
     const uint8_t* par_g = parity + g * a.pgs;
@@ -493,9 +518,13 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     }
     const uint32_t col = part * 64u + lane;
     if (col < (IMPL == 3 ? a.cols8 : IMPL == 4 ? a.cols12 : a.cols)) {
-        if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
-        else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 8u);
-        else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 12u);
+        if constexpr (CT) {
+            if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 16u);
+            else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 8u);
+            else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 12u);
+        } else if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 16u);
+        else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 8u);
+        else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 12u);
         else if (IMPL == 1) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
         else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
     }
@@ -653,9 +682,15 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
     return hipGetLastError();
 }
 
-#define QFEC_REC_LAUNCH(KK, MM, AR)                                                                  \
-    hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR>), dim3(pgrid), dim3(256), 0, stream, a, a.data, a.parity, \
-                       a.marks, a.lut, a.records)
+#define QFEC_REC_LAUNCH(KK, MM, AR)                                                                        \
+    do {                                                                                                   \
+        if (AR >= 2 && a.compact && a.t256)                                                                \
+            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, AR >= 2>), dim3(pgrid), dim3(256), 0, stream, a, \
+                               a.data, a.parity, a.marks, a.lut, a.records);                               \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, false>), dim3(pgrid), dim3(256), 0, stream, a, \
+                               a.data, a.parity, a.marks, a.lut, a.records);                               \
+    } while (0)
 
 #define QFEC_REC_CASE(KK, MM)                                                      \
     if (a.k == KK && a.m == MM) {                                                  \

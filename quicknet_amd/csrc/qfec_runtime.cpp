@@ -82,6 +82,7 @@ struct DevCtx {
     uint8_t* h_stage = nullptr;  // pinned
     size_t h_cap = 0;
     uint8_t* d_gf = nullptr;     // exp[512] | log[256] for the LDS variant
+    uint32_t* d_t256 = nullptr;  // perm tables of all 256 coefficient values (compact reconstruct)
     uint32_t* d_small = nullptr; // per-call tables (fec_encode row, fec_decode matrix)
     size_t small_cap = 0;
     uint32_t* h_small = nullptr; // pinned mirror
@@ -117,6 +118,10 @@ int init_ctx(DevCtx& c, int dev) {
     HIP_TRY(hipMemcpy(c.d_gf, f.exp, 512, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c.d_gf + 512, f.log, 256, hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c.d_counter, 256));
+    std::vector<uint32_t> t256(256 * QFEC_TAB_STRIDE);
+    for (int v = 0; v < 256; ++v) perm_entry((uint8_t)v, &t256[(size_t)v * QFEC_TAB_STRIDE]);
+    HIP_TRY(hipMalloc(&c.d_t256, t256.size() * 4));
+    HIP_TRY(hipMemcpy(c.d_t256, t256.data(), t256.size() * 4, hipMemcpyHostToDevice));
     return QFEC_OK;
 }
 
@@ -456,6 +461,9 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.surv_off = L.surv_off;
     a.lost_off = L.lost_off;
     a.hdr = L.hdr;
+    a.coff = L.coff;
+    a.t256 = ctx.d_t256;
+    a.compact = tuning().recon_compact;
     a.dgs = dgs >= 0 ? (uint64_t)dgs : (uint64_t)c->k * pitch;
     a.pgs = pgs >= 0 ? (uint64_t)pgs : (uint64_t)c->m * pitch;
     a.vec16 = vec16_ok(d_data, d_par, block, pitch) && !((a.dgs | a.pgs) & 15) ? 1 : 0;
@@ -463,8 +471,15 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.impl = tuning().recon_impl;
     a.wpg = (a.cols + 63) / 64;
     a.cols8 = (uint32_t)((block + 7) / 8);
-    a.wpg8 = (a.cols8 + 63) / 64;
     a.cols12 = (uint32_t)((block + 11) / 12);
+    if (a.vec16 && tuning().recon_full_lines) {
+        // cover the 16-B columns' span, which the 16-B body writes anyway (it stays inside
+        // the pitch): a row that ends part-way into a 64-B line costs a partial-line write
+        // (B = 1400: 175 -> 176 8-B columns, rows end on 1408 = 22 lines)
+        a.cols8 = 2u * a.cols;
+        a.cols12 = std::max(a.cols12, a.cols * 16u / 12u);
+    }
+    a.wpg8 = (a.cols8 + 63) / 64;
     a.wpg12 = (a.cols12 + 63) / 64;
     hipError_t e = launch_reconstruct(a, s);
     if (e != hipSuccess) return hip_fail(e, "reconstruct kernel launch");
@@ -608,6 +623,8 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_rx_tail") && (value == 0 || value == 1)) { tuning().wire_rx_tail = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_compact") && (value == 0 || value == 1)) { tuning().recon_compact = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_full_lines") && (value == 0 || value == 1)) { tuning().recon_full_lines = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);

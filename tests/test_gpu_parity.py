@@ -251,14 +251,17 @@ def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
     assert rc_ref in (0, -1)
 
 
+@pytest.mark.parametrize("compact", [1, 0])
 @pytest.mark.parametrize("impl", [-1, 0, 1, 2, 3, 4])
 @pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (4, 2, 100), (12, 4, 40), (3, 2, 1400),
                                    (10, 3, 1400), (4, 2, 1012), (16, 4, 1024), (12, 4, 1400), (8, 4, 1024)])
-def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
+def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B, compact):
     """Every LUT reconstruct body (-1 = the auto choice; row loop, all rows, exact-e rows on
-    16-B, 8-B and 12-B lanes) against the oracle's rs.c restatement, on random erasure patterns (0..m+1
-    erasures, so unrecoverable groups too) with random, inconsistent parity: the survivor
-    rule and the stale-row quirk have to match byte for byte."""
+    16-B, 8-B and 12-B lanes), with the coefficient tables read from the decode record or
+    (compact) from the 256-entry table at the record's offsets, against the oracle's rs.c
+    restatement, on random erasure patterns (0..m+1 erasures, so unrecoverable groups too)
+    with random, inconsistent parity: the survivor rule and the stale-row quirk have to match
+    byte for byte.  Bytes past the 16-B span of a row (the pitch's padding) stay untouched."""
     G = 700
     code = qa.Code.cauchy(k, m)
     rng = np.random.default_rng(k * 100 + B)
@@ -272,16 +275,20 @@ def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
     expect.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
     damaged = expect.copy()
     oracle.rs_reconstruct(code.rows, expect, par.copy(), marks, B)
-    pitch = round16(B)
+    pitch = round16(B) + 16  # one spare 16-B column per row that no body may write
     dd = to_dev(padded(damaged, pitch))
     failed = torch.zeros(1, dtype=torch.int32, device=DEV)
     qa.tune("recon_impl", impl)
+    qa.tune("recon_compact", compact)
     try:
         code.reconstruct(dd, to_dev(padded(par, pitch)), to_dev(marks), B, failed)
         torch.cuda.synchronize()
     finally:
         qa.tune("recon_impl", -1)
-    assert np.array_equal(dd.cpu().numpy()[..., :B], expect)
+        qa.tune("recon_compact", 1)
+    out = dd.cpu().numpy()
+    assert np.array_equal(out[..., :B], expect)
+    assert np.array_equal(out[..., round16(B):], padded(damaged, pitch)[..., round16(B):])
     unrecoverable = int(((gm[:, :k].sum(1) > 0) & (gm.sum(1) > m)).sum())
     assert int(failed.item()) == unrecoverable
 

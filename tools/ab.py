@@ -30,6 +30,8 @@ def main():
     p.add_argument("--erasures", type=int, default=3)
     p.add_argument("--recon-only", action="store_true")
     p.add_argument("--encode-only", action="store_true")
+    p.add_argument("--recon8", action="store_true", help="8-B-lane reconstruct variants only")
+    p.add_argument("--patterns", type=int, default=0, help="draw each group's erasures from this many masks")
     p.add_argument("--pairs", action="store_true", help="time reconstruct right after encode, as bench.py does")
     a = p.parse_args()
     k, m, B, G = a.k, a.m, a.block, a.groups
@@ -40,6 +42,10 @@ def main():
     qa.synth_fill(data, 0x5EED0002)
     par = torch.empty((G, m, pitch), dtype=torch.uint8, device=dev)
     gm = erasure_marks(0x5EED0003, G, k + m, a.erasures)
+    if a.patterns:  # only `patterns` distinct erasure masks (their decode records stay cache-resident)
+        import numpy as np
+        pick = np.random.default_rng(7).integers(0, a.patterns, G)
+        gm = gm[:a.patterns][pick]
     marks = torch.from_numpy(marks_to_rs_layout(gm, k)).to(dev)
     work = data.clone()
     code.encode(data, par, B)
@@ -69,11 +75,20 @@ def main():
         ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
         ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
         ("recon impl2 (exact e rows)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),
-        ("recon impl3 (exact e, 8-B lanes)", lambda: qa.tune("recon_impl", 3), rec, dec_bytes),
+        ("recon impl3 (exact e, 8-B lanes)", lambda: (qa.tune("recon_full_lines", 1), qa.tune("recon_impl", 3)), rec,
+         dec_bytes),
+        ("recon impl3 partial last line", lambda: (qa.tune("recon_full_lines", 0), qa.tune("recon_impl", 3)), rec,
+         dec_bytes),
+        ("recon impl3 tables in record", lambda: (qa.tune("recon_compact", 0), qa.tune("recon_impl", 3)), rec,
+         dec_bytes),
+        ("recon impl2 tables in record", lambda: (qa.tune("recon_compact", 0), qa.tune("recon_impl", 2)), rec,
+         dec_bytes),
         ("recon impl4 (exact e, 12-B lanes)", lambda: qa.tune("recon_impl", 4), rec, dec_bytes),
     ]
     if a.recon_only:
         variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]
+    if a.recon8:
+        variants = [v for v in variants if v[0].startswith(("recon impl3", "recon impl2", "probe"))]
     if a.encode_only:
         variants = [v for v in variants if v[0].startswith(("encode impl0", "encode impl1", "probe"))]
     if a.pairs:
@@ -83,6 +98,8 @@ def main():
     for r in range(a.rounds):
         for name, setup, fn, _ in variants:
             qa.set_kernel_variant(0)
+            qa.tune("recon_full_lines", 1)
+            qa.tune("recon_compact", 1)
             setup()
             fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
