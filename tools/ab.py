@@ -31,6 +31,7 @@ def main():
     p.add_argument("--recon-only", action="store_true")
     p.add_argument("--encode-only", action="store_true")
     p.add_argument("--recon8", action="store_true", help="8-B-lane reconstruct variants only")
+    p.add_argument("--only", default="", help="comma-separated variant-name prefixes ('_' for ' ')")
     p.add_argument("--patterns", type=int, default=0, help="draw each group's erasures from this many masks")
     p.add_argument("--pairs", action="store_true", help="time reconstruct right after encode, as bench.py does")
     a = p.parse_args()
@@ -87,8 +88,10 @@ def main():
     ]
     if a.recon_only:
         variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]
+    if a.only:
+        variants = [v for v in variants if v[0].startswith(tuple(x.replace("_", " ") for x in a.only.split(",")))]
     if a.recon8:
-        variants = [v for v in variants if v[0].startswith(("recon impl3", "recon impl2", "probe"))]
+        variants = [v for v in variants if v[0].startswith(("recon impl3", "recon impl2", "recon impl4", "probe"))]
     if a.encode_only:
         variants = [v for v in variants if v[0].startswith(("encode impl0", "encode impl1", "probe"))]
     if a.pairs:
