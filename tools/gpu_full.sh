@@ -16,8 +16,10 @@ echo "== PMC traffic" && timeout -k 10 900 python tools/pmc_traffic.py --out $OU
 cp $OUT/traffic.json profiles/traffic.json  # bench.py reads roofline.traffic from here
 echo "== bench" && timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 4; }
 cat $OUT/bench.json
+# only the timed step's launches (and config 4's) under the profiler, so each kernel's average is
+# the one bench reports (the host / per-call legs launch the same kernels at other sizes)
 echo "== rocprofv3 kernel trace" && (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-  -d $R/$OUT/prof -o trace -- python3 $R/bench.py --no-cpu > $R/$OUT/bench_prof.json 2> $R/$OUT/prof.err) || { tail -20 $OUT/prof.err; exit 5; }
+  -d $R/$OUT/prof -o trace -- python3 $R/bench.py --no-cpu --no-host --no-side > $R/$OUT/bench_prof.json 2> $R/$OUT/prof.err) || { tail -20 $OUT/prof.err; exit 5; }
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 cut -d, -f1-4 $OUT/kernel_stats.csv | head -6
 echo "== bench --gpus 2 (gloo rehearsal: the launcher's own ranks share the one GPU)" && QFEC_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 --no-cpu > $OUT/bench_g2.json 2> $OUT/bench_g2.err || { tail -20 $OUT/bench_g2.err; exit 7; }
