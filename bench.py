@@ -719,6 +719,11 @@ def main(argv=None):
         from quicknet_amd.hoststream import host_encode_leg, host_mixed_leg
         host_mixed = host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather_float)
         ok = ok and bool(host_mixed.get("verified"))
+        # the same stream through the staged copies, for comparison (not the field's value)
+        staged = host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather_float, passes=2, zero_copy=False)
+        ok = ok and bool(staged.get("verified"))
+        host_mixed["staged"] = {x: staged.get(x) for x in ("value", "verified", "pcie_gbs_per_rank", "h2d_gbs_per_rank",
+                                                          "d2h_gbs_per_rank", "error") if x in staged}
         if rank == 0:
             host_line = host_encode_leg(code, data, parity, B)
             ok = ok and bool(host_line.get("verified"))

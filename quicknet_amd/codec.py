@@ -184,19 +184,18 @@ class Code:
         check(lib().qfec_encode_host(self._h, ptr(data), ptr(parity), G, block_size, pitch), "qfec_encode_host")
 
     def reconstruct_host(self, data, parity, marks, block_size=None):
-        """qfec_reconstruct_host: numpy data [G, k, pitch] rewritten in place from parity
-        [G, m, pitch] and rs.c-layout marks [G*(k+m)], all in host memory.  Returns the
-        number of under-determined groups."""
+        """qfec_reconstruct_host: data uint8 [G, k, pitch] rewritten in place from parity
+        [G, m, pitch] and rs.c-layout marks [G*(k+m)], all in HOST memory (numpy arrays, or
+        CPU tensors, pinned or not).  Returns the number of under-determined groups."""
         G, k, pitch = data.shape
-        for a in (data, parity, marks):
-            if not (isinstance(a, np.ndarray) and a.flags["C_CONTIGUOUS"]):
-                raise QfecError("reconstruct_host: contiguous numpy buffers required")
-        if k != self.k or parity.shape != (G, self.m, pitch) or marks.size != G * (self.k + self.m):
+        nmarks = marks.size if isinstance(marks, np.ndarray) else marks.numel()
+        if k != self.k or tuple(parity.shape) != (G, self.m, pitch) or nmarks != G * (self.k + self.m):
             raise QfecError("reconstruct_host: shape mismatch")
         block_size = pitch if block_size is None else block_size
         nf = C.c_longlong(0)
-        check(lib().qfec_reconstruct_host(self._h, data.ctypes.data, parity.ctypes.data, marks.ctypes.data, G,
-                                          block_size, pitch, C.byref(nf)), "qfec_reconstruct_host")
+        check(lib().qfec_reconstruct_host(self._h, _host_ptr(data, "data"), _host_ptr(parity, "parity"),
+                                          _host_ptr(marks, "marks"), G, block_size, pitch, C.byref(nf)),
+              "qfec_reconstruct_host")
         return int(nf.value)
 
     def encode(self, data, parity, block_size=None, stream=None):

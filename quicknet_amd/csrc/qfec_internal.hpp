@@ -132,7 +132,8 @@ struct Tuning {
     int wire_chunk = 0;     // fused send: groups per body + head launch pair (0: as many as fit)
     int host_chunk = 0;     // qfec_encode_host: groups per pipelined chunk (0: ~32 MiB of data)
     int recon_full_lines = 1;  // 8-/12-B reconstruct lanes cover the 16-B columns' span (no partial 64-B lines)
-    int recon_compact = 1;  // LUT reconstruct reads coefficient tables via the record's offsets + t256
+    int recon_compact = 1;
+    int host_zero_copy = 1; // pinned host batches: kernels read/write them directly (0: staged copies)  // LUT reconstruct reads coefficient tables via the record's offsets + t256
     int wire_rx_split = 1;  // fused receive: k_unpack_v2 (1 auto lanes, 2 16-B, 3 8-B); 0 k_unpack_fused
 };
 Tuning& tuning();

@@ -224,6 +224,18 @@ bool is_pinned_host(const void* p) {
     return attr.type == hipMemoryTypeHost;
 }
 
+// the current device's address of pinned host memory (hipHostMalloc'd, or registered mapped):
+// the kernels then read and write it directly over PCIe, with no staging copies ("zero copy")
+bool host_dev(const void* h, uint8_t** d) {
+    void* p = nullptr;
+    if (!h || hipHostGetDevicePointer(&p, const_cast<void*>(h), 0) != hipSuccess || !p) {
+        (void)hipGetLastError();
+        return false;
+    }
+    *d = static_cast<uint8_t*>(p);
+    return true;
+}
+
 int ensure_host_slot(DevCtx::HostSlot& h, size_t in_bytes, size_t out_bytes) {
     if (!h.stream) {
         HIP_TRY(hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking));
@@ -623,6 +635,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_rx_tail") && (value == 0 || value == 1)) { tuning().wire_rx_tail = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
+    if (!strcmp(key, "host_zero_copy") && (value == 0 || value == 1)) { tuning().host_zero_copy = value; return QFEC_OK; }
     if (!strcmp(key, "recon_compact") && (value == 0 || value == 1)) { tuning().recon_compact = value; return QFEC_OK; }
     if (!strcmp(key, "recon_full_lines") && (value == 0 || value == 1)) { tuning().recon_full_lines = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
@@ -710,6 +723,16 @@ int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char
     gc = std::min(gc, groups);
     const bool pin_in = is_pinned_host(h_data), pin_out = is_pinned_host(h_parity);
     std::lock_guard<std::mutex> lk(ctx->host_mu);
+    uint8_t *z_in = nullptr, *z_out = nullptr;
+    if (tuning().host_zero_copy && pin_in && pin_out && host_dev(h_data, &z_in) && host_dev(h_parity, &z_out)) {
+        // zero copy: one launch reads the data and writes the parity in host memory
+        if ((rc = ensure_host_slot(ctx->host[0], 0, 0))) return rc;
+        hipStream_t st = ctx->host[0].stream;
+        rc = run_encode(*ctx, code, tab, m, z_in, z_out, groups, block_size, pitch, st);
+        const hipError_t e = hipStreamSynchronize(st);
+        if (!rc && e != hipSuccess) rc = hip_fail(e, "qfec_encode_host: zero-copy encode");
+        return rc;
+    }
     for (auto& h : ctx->host)
         if ((rc = ensure_host_slot(h, (size_t)gc * in_g, (size_t)gc * out_g))) return rc;
     long long pending[2] = {-1, -1};  // chunk whose parity sits in the slot's staging
@@ -785,6 +808,29 @@ int qfec_reconstruct_host(qfec_code* code, unsigned char* h_data, const unsigned
     const size_t mk_off = (size_t)gc * (dg + pg), cnt_off = round_up(mk_off + (size_t)gc * (k + m), 16);
     const size_t slot_bytes = cnt_off + 16;
     std::lock_guard<std::mutex> lk(ctx->host_mu);
+    uint8_t *z_data = nullptr, *z_par = nullptr;
+    if (tuning().host_zero_copy && is_pinned_host(h_data) && host_dev(h_data, &z_data) &&
+        (m == 0 || (is_pinned_host(h_parity) && host_dev(h_parity, &z_par)))) {
+        // zero copy: the kernel reads the survivors and writes the erased data rows in host
+        // memory (k + e rows per group over PCIe, not n in and k out); only the marks (one
+        // byte per shard) and the failed counter are staged
+        DevCtx::HostSlot& h = ctx->host[0];
+        const size_t mbytes = (size_t)groups * (k + m), zc_cnt = round_up(mbytes, 16);
+        if ((rc = ensure_host_slot(h, zc_cnt + 16, zc_cnt + 16))) return rc;
+        memcpy(h.h_in, h_marks, mbytes);
+        memset(h.h_in + zc_cnt, 0, 16);
+        HIP_TRY(hipMemcpyAsync(h.d_buf, h.h_in, zc_cnt + 16, hipMemcpyHostToDevice, h.stream));
+        rc = run_reconstruct(*ctx, code, d->d_lut, nullptr, d->d_rec, z_data, z_par, h.d_buf, groups, block_size, pitch,
+                             reinterpret_cast<unsigned*>(h.d_buf + zc_cnt), h.stream);
+        if (!rc) {
+            const hipError_t e1 = hipMemcpyAsync(h.h_out, h.d_buf + zc_cnt, 16, hipMemcpyDeviceToHost, h.stream);
+            if (e1 != hipSuccess) rc = hip_fail(e1, "qfec_reconstruct_host: counter");
+        }
+        const hipError_t e = hipStreamSynchronize(h.stream);
+        if (!rc && e != hipSuccess) rc = hip_fail(e, "qfec_reconstruct_host: zero-copy reconstruct");
+        if (!rc && failed) *failed = *reinterpret_cast<const unsigned*>(h.h_out);
+        return rc;
+    }
     for (auto& h : ctx->host)
         if ((rc = ensure_host_slot(h, slot_bytes, slot_bytes))) return rc;
     long long pending[2] = {-1, -1};
@@ -1097,6 +1143,16 @@ int qfec_pipe_encode(qfec_pipe* p, qfec_code* code, const unsigned char* h_data,
             rc = ensure_enc(code, s->device, &tab);
         }
         if (rc) break;
+        uint8_t *z_in = nullptr, *z_out = nullptr;
+        if (tuning().host_zero_copy && host_dev(h_data, &z_in) && host_dev(h_parity, &z_out)) {
+            // zero copy: the piece's kernel reads and writes the pinned host buffers directly
+            s->busy = true;
+            if ((rc = run_encode(*s->ctx, code, tab, m, z_in + (size_t)g0 * in_g, z_out + (size_t)g0 * out_g, gn,
+                                 block_size, pitch, s->stream)))
+                break;
+            if (hipEventRecord(s->done, s->stream) != hipSuccess) { rc = hip_fail(hipGetLastError(), "event"); break; }
+            continue;
+        }
         uint8_t* d_in = s->d_buf;
         uint8_t* d_out = s->d_buf + (size_t)gn * in_g;
         if (hipMemcpyAsync(d_in, h_data + (size_t)g0 * in_g, (size_t)gn * in_g, hipMemcpyHostToDevice, s->stream) !=
@@ -1154,6 +1210,25 @@ int qfec_pipe_reconstruct(qfec_pipe* p, qfec_code* code, unsigned char* h_data, 
         if (rc) break;
         // slot layout: data [gn][k][pitch] | parity [gn][m][pitch] | marks in rs.c layout
         // for the piece: gn*k data marks, then gn*m parity marks (module/rs.c:609-612)
+        uint8_t *z_data = nullptr, *z_par = nullptr;
+        if (tuning().host_zero_copy && host_dev(h_data, &z_data) && (m == 0 || host_dev(h_parity, &z_par))) {
+            // zero copy: survivors read and erased rows written in host memory; the piece's
+            // marks (rs.c layout for gn groups) staged into the slot
+            uint8_t* dm = s->d_buf;
+            s->busy = true;
+            if (hipMemcpyAsync(dm, h_marks + (size_t)g0 * k, (size_t)gn * k, hipMemcpyHostToDevice, s->stream) ||
+                (m && hipMemcpyAsync(dm + (size_t)gn * k, h_marks + (size_t)groups * k + (size_t)g0 * m, (size_t)gn * m,
+                                     hipMemcpyHostToDevice, s->stream))) {
+                rc = hip_fail(hipGetLastError(), "qfec_pipe_reconstruct: marks H2D");
+                break;
+            }
+            if ((rc = run_reconstruct(*s->ctx, code, d->d_lut, nullptr, d->d_rec, z_data + (size_t)g0 * dg,
+                                      m ? z_par + (size_t)g0 * pg : nullptr, dm, gn, block_size, pitch, s->d_failed,
+                                      s->stream)))
+                break;
+            if (hipEventRecord(s->done, s->stream) != hipSuccess) { rc = hip_fail(hipGetLastError(), "event"); break; }
+            continue;
+        }
         uint8_t* dd = s->d_buf;
         uint8_t* dp = dd + (size_t)gn * dg;
         uint8_t* dm = dp + (size_t)gn * pg;

@@ -69,9 +69,20 @@ def make_case(oracle, k, m, B, G, seed):
             "rx_marks": torch.from_numpy(marks).pin_memory(), "rx_ref": rx_ref, "nfail": nfail}
 
 
+@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("devices,streams,slot", [([0], 3, 1 << 20), ([0, 0], 3, 1 << 20), ([0], 1, 64 << 20),
                                                   (None, 4, 256 << 10)])
-def test_pipe_mixed_vs_oracle(oracle, devices, streams, slot):
+def test_pipe_mixed_vs_oracle(oracle, devices, streams, slot, zero_copy):
+    """zero_copy 1: each piece's kernel reads and writes the pinned batches in place (only the
+    marks are staged); 0: H2D -> kernel -> D2H through the slot's device staging."""
+    qa.tune("host_zero_copy", zero_copy)
+    try:
+        _pipe_mixed(oracle, devices, streams, slot)
+    finally:
+        qa.tune("host_zero_copy", 1)
+
+
+def _pipe_mixed(oracle, devices, streams, slot):
     pipe = qa.Pipe(devices=devices, streams=streams, slot_bytes=slot)
     assert pipe.slots == streams * (len(devices) if devices else torch.cuda.device_count())
     cases = [make_case(oracle, k, m, B, G, 1000 + 7 * k + B) for k, m, B, G in MIXED]

@@ -315,12 +315,13 @@ def test_encode_impls_vs_oracle(oracle, impl, flavour, k, m, B):
     assert np.array_equal(p.cpu().numpy()[..., :B], expect)
 
 
-@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("pinned,zero_copy", [(False, 1), (True, 1), (True, 0)])
 @pytest.mark.parametrize("k,m,B,chunk", [(10, 3, 1024, 7), (16, 4, 1400, 0), (4, 2, 37, 5)])
-def test_encode_host_vs_oracle(oracle, k, m, B, chunk, pinned):
-    """qfec_encode_host (host in, host out, chunked over two streams) against the oracle;
-    chunk = groups per pipelined chunk (0: the ~32 MiB default, one chunk here), pageable
-    numpy buffers or pinned torch tensors."""
+def test_encode_host_vs_oracle(oracle, k, m, B, chunk, pinned, zero_copy):
+    """qfec_encode_host (host in, host out) against the oracle: pageable numpy buffers through
+    pinned staging chunked over two streams (chunk = groups per chunk, 0: the ~32 MiB
+    default), pinned torch tensors read and written by the kernel directly (zero copy), or
+    pinned through the staged path."""
     G = 101
     code = qa.Code.cauchy(k, m)
     pitch = B if B % 16 else round16(B)
@@ -334,18 +335,23 @@ def test_encode_host_vs_oracle(oracle, k, m, B, chunk, pinned):
     else:
         hp = np.full((G, m, pitch), 0x5A, np.uint8)
     qa.tune("host_chunk", chunk)
+    qa.tune("host_zero_copy", zero_copy)
     try:
         code.encode_host(hd, hp, B)
     finally:
         qa.tune("host_chunk", 0)
+        qa.tune("host_zero_copy", 1)
     got = hp.numpy() if pinned else hp
     assert np.array_equal(got[..., :B], expect)
 
 
+@pytest.mark.parametrize("pinned,zero_copy", [(False, 1), (True, 1), (True, 0)])
 @pytest.mark.parametrize("k,m,B,chunk", [(10, 3, 1024, 7), (16, 4, 1400, 0), (4, 2, 37, 5)])
-def test_reconstruct_host_vs_oracle(oracle, k, m, B, chunk):
-    """qfec_reconstruct_host (host buffers, chunked over two streams) against the oracle's
-    rs.c restatement on random patterns with inconsistent parity, incl. unrecoverable groups."""
+def test_reconstruct_host_vs_oracle(oracle, k, m, B, chunk, pinned, zero_copy):
+    """qfec_reconstruct_host against the oracle's rs.c restatement on random patterns with
+    inconsistent parity, incl. unrecoverable groups: pageable buffers staged in chunks over two
+    streams, pinned ones read and written by the kernel in place (zero copy: only the erased
+    rows are written back), or pinned through the staged path."""
     G = 211
     code = qa.Code.cauchy(k, m)
     pitch = B if B % 16 else round16(B)
@@ -359,12 +365,19 @@ def test_reconstruct_host_vs_oracle(oracle, k, m, B, chunk):
     expect = data.copy()
     expect.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
     work = padded(expect, pitch, 0xC3)
+    hpar = padded(par, pitch)
+    if pinned:
+        work, hpar = torch.from_numpy(work).pin_memory(), torch.from_numpy(hpar).pin_memory()
     oracle.rs_reconstruct(code.rows, expect, par.copy(), marks, B)
     qa.tune("host_chunk", chunk)
+    qa.tune("host_zero_copy", zero_copy)
     try:
-        nf = code.reconstruct_host(work, padded(par, pitch), np.ascontiguousarray(marks), B)
+        nf = code.reconstruct_host(work, hpar, np.ascontiguousarray(marks), B)
     finally:
         qa.tune("host_chunk", 0)
+        qa.tune("host_zero_copy", 1)
+    if pinned:
+        work = work.numpy()
     assert np.array_equal(work[..., :B], expect)
     assert nf == int(((gm[:, :k].sum(1) > 0) & (gm.sum(1) > m)).sum())
 

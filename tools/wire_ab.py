@@ -29,6 +29,7 @@ def main():
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--variants", default="base;wire_store_nt=0;wire_store_nt=1;wire_fused=0")
     p.add_argument("--unpack", action="store_true", help="time qfec_unpack_datagrams (n - k losses per group)")
+    p.add_argument("--align", type=int, default=16, help="shard and wire row pitches rounded to this (16 or 64)")
     a = p.parse_args()
     k, n, G, S = a.k, a.n, a.groups, a.size
     dev = torch.device("cuda:0")
@@ -40,8 +41,10 @@ def main():
     seq = torch.stack([torch.arange(G, dtype=torch.int32, device=dev) * n,
                        torch.arange(G, dtype=torch.int32, device=dev) * k], 1).contiguous()
     head = 4
-    pitch = (S + head + 15) // 16 * 16
-    wpitch = (pitch + 13 + 15) // 16 * 16
+    A = a.align
+    pitch = (S + head + A - 1) // A * A
+    wpitch = (pitch + 13 + A - 1) // A * A
+    row16 = (S + head + 15) // 16 * 16  # the shard bytes a row carries, for the traffic count
     shards = torch.empty((G, n, pitch), dtype=torch.uint8, device=dev)
     wire = torch.zeros((G, n, wpitch), dtype=torch.uint8, device=dev)
     wlen = torch.empty((G, n), dtype=torch.int32, device=dev)
@@ -108,8 +111,9 @@ def main():
     setup("base")
     nbytes = G * k * S + int(wlen.sum().item())
     if a.unpack:  # received datagrams in, data rows out
-        nbytes = int(rx_len.sum().item()) + G * k * pitch
-    print(f"{'unpack' if a.unpack else 'pack'} RS({k},{n}) payload {S} B, G={G}: {a.rounds} rounds x {a.reps}")
+        nbytes = int(rx_len.sum().item()) + G * k * row16
+    print(f"{'unpack' if a.unpack else 'pack'} RS({k},{n}) payload {S} B, G={G}, pitch {pitch} / wire {wpitch}: "
+          f"{a.rounds} rounds x {a.reps}")
     for v in variants:
         t = times[v]
         med = statistics.median(t)
