@@ -60,17 +60,19 @@ int qfec_code_shape(const qfec_code *code, int *k, int *m);
 int qfec_encode(qfec_code *code, const unsigned char *d_data, unsigned char *d_parity,
                 long long groups, int block_size, long long pitch, void *stream);
 
-/* qfec_encode on HOST buffers (the network path starts and ends in host memory): the batch
- * runs in ~32 MiB chunks over two internal streams, H2D -> encode -> D2H of one chunk
- * overlapping the staging of the next.  Pageable buffers are staged through pinned memory;
- * hipHostMalloc'd / registered buffers are DMA'd directly.  Returns after the last parity
- * chunk is in h_parity.  Layouts as qfec_encode. */
+/* qfec_encode on HOST buffers (the network path starts and ends in host memory).  Pinned
+ * buffers the device can address (hipHostMalloc'd, or registered mapped) are read and written
+ * in place by one launch over PCIe ("zero copy"); pageable ones run in ~32 MiB chunks over two
+ * internal streams, staged through pinned memory, H2D -> encode -> D2H of one chunk overlapping
+ * the staging of the next.  Returns after the parity is in h_parity.  Layouts as qfec_encode. */
 int qfec_encode_host(qfec_code *code, const unsigned char *h_data, unsigned char *h_parity,
                      long long groups, int block_size, long long pitch);
 
-/* qfec_reconstruct on HOST buffers, chunked like qfec_encode_host: h_data is rewritten in
- * place, h_marks is in the rs.c layout over all `groups` (G*k data marks, then G*m parity
- * marks); *failed (may be NULL) = groups left under-determined.  k + m <= 24. */
+/* qfec_reconstruct on HOST buffers: h_data is rewritten in place, h_marks is in the rs.c
+ * layout over all `groups` (G*k data marks, then G*m parity marks); *failed (may be NULL) =
+ * groups left under-determined.  k + m <= 24.  Pinned data and parity are worked on in place
+ * (zero copy: the survivors are read and only the erased rows written, over PCIe; the marks are
+ * staged); otherwise chunked and staged like qfec_encode_host. */
 int qfec_reconstruct_host(qfec_code *code, unsigned char *h_data, const unsigned char *h_parity,
                           const unsigned char *h_marks, long long groups, int block_size, long long pitch,
                           long long *failed);
@@ -81,8 +83,9 @@ int qfec_reconstruct_host(qfec_code *code, unsigned char *h_data, const unsigned
  * a device may be listed more than once).  qfec_pipe_encode / qfec_pipe_reconstruct split a
  * batch into pieces that fit a slot and spread over all slots; each piece takes the next
  * slot round-robin (devices interleaved), waits for that slot's previous piece, and queues
- * H2D -> kernel -> D2H on its stream, so the copies of one piece overlap the kernels and
- * copies of the others.  They return once the pieces are queued.  Host buffers must be
+ * its kernel on the pinned buffers in place (zero copy; only the piece's marks are staged)
+ * -- or, with qfec_tune("host_zero_copy", 0) or a device that cannot address the buffers,
+ * H2D -> kernel -> D2H through the slot's staging -- so the pieces overlap each other.  They return once the pieces are queued.  Host buffers must be
  * PINNED (hipHostMalloc'd or hipHostRegister'ed; DMA'd directly) and must not be touched
  * until qfec_pipe_wait returns.  Layouts as qfec_encode / qfec_reconstruct_host (marks in
  * the rs.c layout over the batch's `groups`).  Any number of codes may share a pipe.
@@ -184,9 +187,20 @@ int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long s
 int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long long groups, int k, int m,
                       int block_size, long long pitch, void *stream);
 
-/* Experiment knobs for interleaved A/B timing (tools/ab.py, tools/wire_ab.py): "encode_impl"
- * 0|1, "recon_impl" -1 (auto) | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B lanes, "wire_fused" 1 (fused datagram send where a (k, m)
- * instance exists) | 0 (staged build -> encode -> emit), "wire_store_nt" 0-3.  Defaults are the measured best; results are identical. */
+/* Experiment knobs for interleaved A/B timing (tools/ab.py, tools/wire_ab.py).  Defaults are
+ * the measured best; results are identical either way.
+ *   "encode_impl"      0 all rows | 1 row loop
+ *   "recon_impl"       -1 auto | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B
+ *   "recon_compact"    1 tables via the 256-entry table at the record header's offsets | 0 from the record
+ *   "recon_full_lines" 1 8-/12-B lanes cover the 16-B columns' span | 0 stop at B
+ *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies
+ *   "host_chunk"       groups per staged host chunk (0: ~32 MiB)
+ *   "wire_fused"       1 fused datagram send where a (k, m) instance exists | 0 staged build -> encode -> emit
+ *   "wire_fused_rx"    1 fused datagram receive | 0 staged parse -> reconstruct -> check
+ *   "wire_rx_split"    1 k_unpack_v2, lanes by pitch | 2 16-B | 3 8-B | 0 the round-1 k_unpack_fused
+ *   "wire_store_nt"    0-3 non-temporal datagram stores (bit 0 body, bit 1 head)
+ *   "wire_chunk"       groups per fused send launch pair (0: as many as fit)
+ *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged */
 int qfec_tune(const char *key, int value);
 
 int qfec_set_kernel_variant(int variant);
