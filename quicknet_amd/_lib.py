@@ -50,6 +50,14 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                            "or `make -C quicknet_amd/csrc` (there is no CPU fallback)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7,
+    # but libtorch_hip asks for "libamdhip64.so").  Loaded first, it also satisfies libqfec's
+    # libamdhip64.so.7; loaded after /opt/rocm's, it comes in as a second runtime, and the
+    # first one then sees no device ("no ROCm-capable device is detected").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i, ll, u64 = C.c_void_p, C.c_int, C.c_longlong, C.c_ulonglong
     sig = {

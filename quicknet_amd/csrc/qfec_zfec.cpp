@@ -15,15 +15,24 @@
 // A decode's inputs can depend on earlier decodes' verdicts (sorted mode resets delivered slots,
 // :437), so the receive machine is replayed from the flush's starting state until every decode
 // it calls for has a device result (one replay when no decoded packet fails its checksum).
+//
+// Bytes are never copied on the host beyond what the device needs: datagrams, shards and
+// payloads are views into the queued datagrams (reference-counted, so window slots can hold
+// them across flushes), the device's inputs and outputs go through persistent pinned arenas
+// with one copy each way per launch, and a verdict launch returns only the per-row verdicts
+// (a received source packet's payload is the datagram's own bytes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
-#include <deque>
+#include <chrono>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <tuple>
 #include <utility>
 #include <vector>
@@ -37,6 +46,13 @@ inline size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
 inline uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24; }
 inline int packed_size(int size) { return size < 0 ? 0 : size + 4 + 12 + 4; }  // getPackedPktSize, FecCodecBuf.cpp:16-25
 inline int cmod(int a, int b) { return a % b; }                                   // C's % (truncating), as in :277
+
+using Buf = std::shared_ptr<const std::vector<uint8_t>>;
+struct View {  // bytes [off, off + len) of a shared buffer
+    Buf b;
+    uint32_t off = 0, len = 0;
+    const uint8_t* p() const { return b ? b->data() + off : nullptr; }
+};
 
 // ---- FecCodecList: std::map<float 1 - k/n, FecCodec*> (FecCodec.cpp:18-95)
 struct CodecEntry {
@@ -84,59 +100,36 @@ struct CodecList {
     }
 };
 
-// ---- one dec_pkts_buf entry (FecPacket.h): its FecBuf allocation is modelled byte for byte
-// (MaxBufSize bytes), since dec_src_pkt_info may read past BufSize of a stale copy
+// ---- one dec_pkts_buf entry (FecPacket.h).  Its FecBuf is the received shard (a view): the
+// decode reads its BufSize bytes, zero-padded (set_fec_dec_buf, FecCodecBuf.cpp:171-172), and
+// flush_avail_pkts delivers the payload dec_src_pkt_info found in it when it was received
+// (only source packets that passed are stored, NetFecCodec.cpp:240-245; dec_pkt_size only grows)
 struct Slot {
     int64_t iPacket = -1;
-    std::vector<uint8_t> fec_buf;
     int BufSize = 0;
     bool bValid = false;
-    int MaxBufSize = 0;
     bool bSourcePkt = true;
     uint32_t i_source_pkt = 0;
     bool bUsed = false;
-    uint64_t uid = 0;   // which received datagram filled it (decode cache key)
-    int ik = 0;         // the ik it was received with
-    // dec_src_pkt_info's result on it, from the device verdict when it was received: only
-    // source packets that passed it are stored (NetFecCodec.cpp:240-245), and a later
-    // flush_avail_pkts check (:421) sees the same bytes under a dec_pkt_size that only grew
-    std::vector<uint8_t> payload;
-    void resize(int n) { fec_buf.resize((size_t)n, 0); }
-    void set_packet(const uint8_t* p, int size, uint64_t id, int row, const std::vector<uint8_t>& pay) {  // SetPacket (:78-98)
-        if (size > MaxBufSize) MaxBufSize = size;
-        resize(MaxBufSize);
-        std::fill(fec_buf.begin(), fec_buf.end(), 0);
-        if (size) memcpy(fec_buf.data(), p, (size_t)size);
-        BufSize = size;
+    uint64_t uid = 0;  // which received datagram filled it (decode cache key)
+    int ik = 0;        // the ik it was received with
+    View shard, payload;
+    void set_packet(const View& sh, uint64_t id, int row, const View& pay) {  // SetPacket (FecPacket.h:78-98)
+        shard = sh;
+        BufSize = (int)sh.len;
         bValid = true;
         bUsed = false;
         uid = id;
         ik = row;
         payload = pay;
     }
-    void reset(int max_size) {  // Reset (:99-122)
+    void reset() {  // Reset (:99-122)
         iPacket = -1;
         BufSize = 0;
-        resize(max_size);
-        std::fill(fec_buf.begin(), fec_buf.end(), 0);
-        MaxBufSize = max_size;
         bValid = false;
         bUsed = false;
     }
-    void assign(const Slot& o) {  // operator= (:42-68): o's first BufSize bytes only
-        iPacket = o.iPacket;
-        MaxBufSize = o.MaxBufSize;
-        resize(MaxBufSize);
-        if (o.BufSize) memcpy(fec_buf.data(), o.fec_buf.data(), (size_t)o.BufSize);
-        BufSize = o.BufSize;
-        bValid = o.bValid;
-        bSourcePkt = o.bSourcePkt;
-        i_source_pkt = o.i_source_pkt;
-        bUsed = o.bUsed;
-        uid = o.uid;
-        ik = o.ik;
-        payload = o.payload;
-    }
+    // operator= (:42-68) copies every field the machine reads: the plain copy
 };
 
 // receive state of one NetFecCodecLayer plus the FecCodecBuf fields its decisions read
@@ -154,9 +147,10 @@ struct RxState {
 enum OpType { OP_PACK, OP_UNPACK, OP_SETKN, OP_ENABLE, OP_SORTED, OP_DYNKN, OP_LOST };
 struct Op {
     OpType t;
-    std::vector<uint8_t> data;
+    Buf data;  // OP_PACK payload / OP_UNPACK datagram
     int a = 0, b = 0, c = 0;
     float f = 0;
+    uint64_t uid = 0;  // OP_UNPACK: the datagram's id (decode cache keys)
 };
 
 // send state (zfec_pack_input) and the open group carried across flushes
@@ -170,7 +164,7 @@ struct TxState {
     // the open group: (k, n) it started with, first indices, payloads so far, rows emitted
     int gk = 0, gn = 0;
     uint32_t g_sent0 = 0, g_src0 = 0;
-    std::vector<std::vector<uint8_t>> g_pay;
+    std::vector<Buf> g_pay;
     int g_emitted = 0;
 };
 
@@ -184,11 +178,57 @@ struct Session {
 
 // an output of one op, filled in after the device work
 struct Emit {
-    int kind = 0;        // 0 datagram from a send batch, 1 plain bytes, 2 delivery (bytes + src)
+    int kind = 0;  // 0 datagram of a send batch, 1 owned bytes, 2 delivery (view + src),
+                   // 3 delivery of a decoded row whose result is pending (batch = request, row)
     int batch = -1, row = 0;
     long long group = 0;
-    std::vector<uint8_t> bytes;
+    View v;
     uint32_t src = 0;
+};
+
+// persistent pinned host + device memory, grow-only, re-made when the current device changes
+struct Arena {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t hcap = 0, dcap = 0;
+    int dev = -1;
+    void release() {
+        if (h) (void)hipHostFree(h);
+        if (d) (void)hipFree(d);
+        h = d = nullptr;
+        hcap = dcap = 0;
+    }
+    int ensure(size_t hbytes, size_t dbytes) {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return QFEC_ENODEV;
+        if (cur != dev) release();
+        dev = cur;
+        if (hbytes > hcap) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+            hcap = 0;
+            const size_t cap = round16(hbytes + (hbytes >> 2) + 4096);
+            if (hipHostMalloc(reinterpret_cast<void**>(&h), cap, hipHostMallocDefault) != hipSuccess) {
+                fprintf(stderr, "[qfec] qfec_zfec_flush: hipHostMalloc(%zu) failed\n", cap);
+                h = nullptr;
+                return QFEC_ENOMEM;
+            }
+            hcap = cap;
+        }
+        if (dbytes > dcap) {
+            if (d) (void)hipFree(d);
+            d = nullptr;
+            dcap = 0;
+            const size_t cap = round16(dbytes + (dbytes >> 2) + 4096);
+            if (hipMalloc(reinterpret_cast<void**>(&d), cap) != hipSuccess) {
+                fprintf(stderr, "[qfec] qfec_zfec_flush: hipMalloc(%zu) failed\n", cap);
+                d = nullptr;
+                return QFEC_ENOMEM;
+            }
+            dcap = cap;
+        }
+        return QFEC_OK;
+    }
 };
 
 }  // namespace
@@ -198,6 +238,7 @@ struct qfec_zfec {
     std::vector<Session> sessions;
     std::map<std::pair<int, int>, qfec_code*> codes;  // (k, n) -> fec_new(k, n) matrix on the device
     uint64_t next_uid = 1;
+    Arena pack_arena, rx_arena, dec_arena;
 };
 
 namespace {
@@ -209,158 +250,206 @@ qfec_code* code_for(qfec_zfec* z, int k, int n) {
 }
 
 // ---------------------------------------------------------------- device batches
-struct HostDev {
-    std::vector<uint8_t> h;
-    void* d = nullptr;
-    size_t cap = 0;
-    bool ensure(size_t bytes) {
-        if (bytes <= cap) return true;
-        if (d) (void)hipFree(d);
-        d = nullptr;
-        cap = 0;
-        if (hipMalloc(&d, bytes + 4096) != hipSuccess) return false;
-        cap = bytes + 4096;
-        return true;
-    }
-    ~HostDev() {
-        if (d) (void)hipFree(d);
-    }
-};
-
 // send: complete or partial groups of one (k, n); payloads of missing rows are empty
 struct PackGroup {
     uint32_t sent0, src0;
-    std::vector<const std::vector<uint8_t>*> pay;  // k entries (nullptr = not yet given)
+    std::vector<Buf> pay;  // k entries (null = not yet given)
 };
 struct PackBatch {
     int k, n;
     std::vector<PackGroup> groups;
-    std::vector<uint8_t> wire;   // results: [G][n][wp]
-    std::vector<int> wlen;
-    size_t wp = 0;
+    // layout in the pack arena (host and device alike; shards device-only, last)
+    size_t base = 0, total = 0, sp = 0, wp = 0;
+    size_t o_offs = 0, o_sizes = 0, o_seq = 0, o_wlen = 0, o_wire = 0, o_end = 0, o_shards = 0;
+    const uint8_t* wire = nullptr;  // results, in the pinned arena
+    const int* wlen = nullptr;
 };
 
-int run_pack(qfec_zfec* z, PackBatch& b, hipStream_t s) {
+void pack_layout(PackBatch& b, size_t base) {
     const size_t G = b.groups.size();
-    if (!G) return 0;
     size_t maxp = 1, total = 0;
     for (auto& g : b.groups)
-        for (auto* p : g.pay)
+        for (auto& p : g.pay)
             if (p) {
                 maxp = std::max(maxp, p->size());
                 total += p->size();
             }
-    const size_t sp = round16(maxp + 4), wp = round16(sp + 13);
-    std::vector<uint8_t> payload(round16(total + 16), 0);
-    std::vector<long long> offs(G * b.k);
-    std::vector<int> sizes(G * b.k);
-    std::vector<uint32_t> seq(2 * G);
+    b.total = total;
+    b.sp = round16(maxp + 4);
+    b.wp = round16(b.sp + 13);
+    b.base = base;
+    size_t o = base + round16(total + 16);  // payload (16 readable bytes past the last)
+    b.o_offs = o;
+    o += round16(G * b.k * 8);
+    b.o_sizes = o;
+    o += round16(G * b.k * 4);
+    b.o_seq = o;
+    o += round16(G * 8);
+    b.o_wlen = o;
+    o += round16(G * b.n * 4);
+    b.o_wire = o;
+    o += G * b.n * b.wp;
+    b.o_end = o;
+    b.o_shards = o;  // device only
+}
+
+int run_pack(qfec_zfec* z, PackBatch& b, hipStream_t s) {
+    const size_t G = b.groups.size();
+    Arena& A = z->pack_arena;
+    uint8_t* h = A.h;
+    long long* offs = reinterpret_cast<long long*>(h + b.o_offs);
+    int* sizes = reinterpret_cast<int*>(h + b.o_sizes);
+    uint32_t* seq = reinterpret_cast<uint32_t*>(h + b.o_seq);
     size_t o = 0;
     for (size_t g = 0; g < G; ++g) {
         seq[2 * g] = b.groups[g].sent0;
         seq[2 * g + 1] = b.groups[g].src0;
         for (int i = 0; i < b.k; ++i) {
-            const std::vector<uint8_t>* p = b.groups[g].pay[i];
+            const Buf& p = b.groups[g].pay[(size_t)i];
             offs[g * b.k + i] = (long long)o;
             sizes[g * b.k + i] = p ? (int)p->size() : 0;
-            if (p && !p->empty()) memcpy(payload.data() + o, p->data(), p->size());
+            if (p && !p->empty()) memcpy(h + b.base + o, p->data(), p->size());
             o += p ? p->size() : 0;
         }
     }
-    HostDev dp, da, dsh, dw, dl;
-    const size_t ob = offs.size() * 8, zb = sizes.size() * 4, qb = seq.size() * 4;
-    if (!dp.ensure(payload.size()) || !da.ensure(ob + zb + qb) || !dsh.ensure(G * b.n * sp) || !dw.ensure(G * b.n * wp) ||
-        !dl.ensure(G * b.n * 4))
-        return QFEC_ENOMEM;
-    uint8_t* a = static_cast<uint8_t*>(da.d);
-    if (hipMemcpyAsync(dp.d, payload.data(), payload.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(a, offs.data(), ob, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(a + ob, sizes.data(), zb, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(a + ob + zb, seq.data(), qb, hipMemcpyHostToDevice, s) != hipSuccess)
+    memset(h + b.base + o, 0, 16);
+    if (hipMemcpyAsync(A.d + b.base, h + b.base, b.o_wlen - b.base, hipMemcpyHostToDevice, s) != hipSuccess)
         return QFEC_EHIP;
-    int rc = qfec_pack_datagrams(code_for(z, b.k, b.n), static_cast<unsigned char*>(dp.d),
-                                 reinterpret_cast<const long long*>(a), reinterpret_cast<const int*>(a + ob),
-                                 reinterpret_cast<const unsigned int*>(a + ob + zb), (long long)G, 1 /* is_send_checksum */,
-                                 static_cast<unsigned char*>(dsh.d), (long long)sp, static_cast<unsigned char*>(dw.d),
-                                 (long long)wp, static_cast<int*>(dl.d), s);
+    uint8_t* d = A.d;
+    int rc = qfec_pack_datagrams(code_for(z, b.k, b.n), d + b.base, reinterpret_cast<const long long*>(d + b.o_offs),
+                                 reinterpret_cast<const int*>(d + b.o_sizes),
+                                 reinterpret_cast<const unsigned int*>(d + b.o_seq), (long long)G, 1 /* is_send_checksum */,
+                                 d + b.o_shards, (long long)b.sp, d + b.o_wire, (long long)b.wp,
+                                 reinterpret_cast<int*>(d + b.o_wlen), s);
     if (rc) return rc;
-    b.wire.resize(G * b.n * wp);
-    b.wlen.resize(G * b.n);
-    b.wp = wp;
-    if (hipMemcpyAsync(b.wire.data(), dw.d, b.wire.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(b.wlen.data(), dl.d, b.wlen.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+    if (hipMemcpyAsync(h + b.o_wlen, d + b.o_wlen, b.o_end - b.o_wlen, hipMemcpyDeviceToHost, s) != hipSuccess)
         return QFEC_EHIP;
-    return 0;
+    b.wire = h + b.o_wire;
+    b.wlen = reinterpret_cast<const int*>(h + b.o_wlen);
+    return QFEC_OK;
 }
 
 // receive: pseudo-groups of wire rows (datagrams, or 0xEC-wrapped shards for decodes)
 struct UnpackRow {
     int group, ik;
-    std::vector<uint8_t> bytes;  // the datagram
+    View hdr_src;    // bytes written from the row start: the datagram (verdicts) ...
+    int wrap = 0;    // ... or, for decodes, a synthesized 11-byte 0xEC header (wrap = 1) + the shard
 };
 struct UnpackBatch {
     int k, n, checksum, dec_pkt_size;
     int groups = 0;
+    bool want_shards = false;  // decodes: the data rows come back
+    size_t need = 0;           // row bytes dec_src_pkt_info may read (head + size field), if known
     std::vector<UnpackRow> rows;
-    // results
-    std::vector<uint8_t> shards;  // [G][n][sp]
-    std::vector<int> rx, status, psize;
-    size_t sp = 0;
+    // layout in an arena (host and device alike up to o_hend; marks and the device's shard
+    // matrix after it); results in its host side
+    size_t base = 0, sp = 0, wp = 0;
+    size_t o_wlen = 0, o_rx = 0, o_st = 0, o_ps = 0, o_hsh = 0, o_hend = 0, o_marks = 0, o_dsh = 0, o_dend = 0;
+    const int *rx = nullptr, *status = nullptr, *psize = nullptr;
+    const uint8_t* shards = nullptr;  // want_shards: the data rows, [G][k][sp]
 };
 
-int run_unpack(qfec_zfec* z, UnpackBatch& b, hipStream_t s) {
+// shard rows hold every shard and every byte dec_src_pkt_info may read (the reference's buffers
+// are dec_pkt_size long, zero-filled): `need` (verdicts: the largest head + size field among the
+// rows; decodes: 0 -- a decoded row is zero past its inputs' longest shard, so a genuine packet
+// fits; a row the pitch cuts short is re-decoded at dec_pkt_size + 4, see the decode loop)
+void unpack_layout(UnpackBatch& b, size_t base) {
     const size_t G = (size_t)b.groups;
-    if (!G) return 0;
     size_t maxd = 16;
-    for (auto& r : b.rows) maxd = std::max(maxd, r.bytes.size());
-    // shard rows hold any datagram's shard and dec_pkt_size + 4 bytes, so dec_src_pkt_info's
-    // reads stay inside the row (the reference's buffers are dec_pkt_size long, zero-filled)
-    const size_t sp = round16(std::max(maxd, (size_t)b.dec_pkt_size + 4)), wp = round16(sp + 13);
-    std::vector<uint8_t> wire(G * b.n * wp, 0);
-    std::vector<int> wlen(G * b.n, 0);
-    for (auto& r : b.rows) {
-        memcpy(wire.data() + ((size_t)r.group * b.n + r.ik) * wp, r.bytes.data(), r.bytes.size());
-        wlen[(size_t)r.group * b.n + r.ik] = (int)r.bytes.size();
+    for (auto& r : b.rows) maxd = std::max(maxd, (size_t)r.hdr_src.len + (r.wrap ? 11u : 0u));
+    b.sp = round16(std::max(maxd, std::min(b.need, (size_t)b.dec_pkt_size + 4)));
+    b.wp = round16(b.sp + 13);
+    b.base = base;
+    size_t o = base + G * b.n * b.wp;  // wire
+    b.o_wlen = o;
+    o += round16(G * b.n * 4);
+    b.o_rx = o;
+    o += round16(G * b.n * 4);
+    b.o_st = o;
+    o += round16(G * b.k * 4);
+    b.o_ps = o;
+    o += round16(G * b.k * 4);
+    b.o_hsh = o;
+    if (b.want_shards) o += G * b.k * b.sp;
+    b.o_hend = o;
+    b.o_marks = o;
+    o += round16(G * b.n);
+    b.o_dsh = o;
+    o += G * b.n * b.sp;
+    b.o_dend = o;
+}
+
+// rows copied into the pinned wire on several threads when there are many bytes
+template <class F>
+void parallel_rows(size_t nrows, size_t bytes, F&& f) {
+    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const unsigned T = bytes > ((size_t)8 << 20) ? hw : 1u;
+    if (T <= 1) {
+        f(0, nrows);
+        return;
     }
-    HostDev dw, dl, dsh, dsm;
-    const size_t smb = round16(G * b.n) + (G * b.n + 2 * G * b.k) * 4;
-    if (!dw.ensure(wire.size()) || !dl.ensure(wlen.size() * 4) || !dsh.ensure(G * b.n * sp) || !dsm.ensure(smb))
-        return QFEC_ENOMEM;
-    uint8_t* marks = static_cast<uint8_t*>(dsm.d);
-    int* rx = reinterpret_cast<int*>(marks + round16(G * b.n));
-    int* st = rx + G * b.n;
-    int* ps = st + G * b.k;
-    if (hipMemcpyAsync(dw.d, wire.data(), wire.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(dl.d, wlen.data(), wlen.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; ++t) th.emplace_back(f, nrows * t / T, nrows * (t + 1) / T);
+    for (auto& x : th) x.join();
+}
+
+int run_unpack(qfec_zfec* z, Arena& A, UnpackBatch& b, hipStream_t s) {
+    const size_t G = (size_t)b.groups;
+    uint8_t* h = A.h;
+    uint8_t* wire = h + b.base;
+    int* wlen = reinterpret_cast<int*>(h + b.o_wlen);
+    memset(wlen, 0, G * b.n * 4);
+    size_t bytes = 0;
+    for (auto& r : b.rows) bytes += r.hdr_src.len;
+    parallel_rows(b.rows.size(), bytes, [&](size_t r0, size_t r1) {
+        for (size_t i = r0; i < r1; ++i) {
+            const UnpackRow& r = b.rows[i];
+            uint8_t* row = wire + ((size_t)r.group * b.n + r.ik) * b.wp;
+            size_t len = r.hdr_src.len;
+            if (r.wrap) {  // [0xEC][sent 0][src 0][n | k << 4 | ik << 8][shard]
+                memset(row, 0, 11);
+                row[0] = 0xEC;
+                const uint32_t ikn = (uint32_t)b.n | (uint32_t)b.k << 4 | (uint32_t)r.ik << 8;
+                row[9] = (uint8_t)(ikn & 0xFF);
+                row[10] = (uint8_t)(ikn >> 8);
+                if (len) memcpy(row + 11, r.hdr_src.p(), len);
+                len += 11;
+            } else if (len) {
+                memcpy(row, r.hdr_src.p(), len);
+            }
+            wlen[(size_t)r.group * b.n + r.ik] = (int)len;
+        }
+    });
+    uint8_t* d = A.d;
+    if (hipMemcpyAsync(d + b.base, h + b.base, b.o_rx - b.base, hipMemcpyHostToDevice, s) != hipSuccess)
         return QFEC_EHIP;
-    int rc = qfec_unpack_datagrams(code_for(z, b.k, b.n), static_cast<unsigned char*>(dw.d), (long long)wp,
-                                   static_cast<int*>(dl.d), (long long)G, b.checksum, b.dec_pkt_size,
-                                   static_cast<unsigned char*>(dsh.d), (long long)sp, marks, rx, st, ps, s);
+    int rc = qfec_unpack_datagrams(code_for(z, b.k, b.n), d + b.base, (long long)b.wp, reinterpret_cast<int*>(d + b.o_wlen),
+                                   (long long)G, b.checksum, b.dec_pkt_size, d + b.o_dsh, (long long)b.sp,
+                                   d + b.o_marks, reinterpret_cast<int*>(d + b.o_rx), reinterpret_cast<int*>(d + b.o_st),
+                                   reinterpret_cast<int*>(d + b.o_ps), s);
     if (rc) return rc;
-    b.shards.resize(G * b.n * sp);
-    b.rx.resize(G * b.n);
-    b.status.resize(G * b.k);
-    b.psize.resize(G * b.k);
-    b.sp = sp;
-    if (hipMemcpyAsync(b.shards.data(), dsh.d, b.shards.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(b.rx.data(), rx, b.rx.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(b.status.data(), st, b.status.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(b.psize.data(), ps, b.psize.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
+    if (hipMemcpyAsync(h + b.o_rx, d + b.o_rx, b.o_hsh - b.o_rx, hipMemcpyDeviceToHost, s) != hipSuccess)
         return QFEC_EHIP;
-    return 0;
+    if (b.want_shards &&  // the k data rows of each group only
+        hipMemcpy2DAsync(h + b.o_hsh, (size_t)b.k * b.sp, d + b.o_dsh, (size_t)b.n * b.sp, (size_t)b.k * b.sp, G,
+                         hipMemcpyDeviceToHost, s) != hipSuccess)
+        return QFEC_EHIP;
+    b.rx = reinterpret_cast<const int*>(h + b.o_rx);
+    b.status = reinterpret_cast<const int*>(h + b.o_st);
+    b.psize = reinterpret_cast<const int*>(h + b.o_ps);
+    b.shards = b.want_shards ? h + b.o_hsh : nullptr;
+    return QFEC_OK;
 }
 
 // ---------------------------------------------------------------- receive verdicts and decodes
 struct Verdict {  // of one received FEC datagram
-    bool fec = false;      // tag 0xEC / 0xED and size >= 11
-    bool ok = false;       // unpack_fec_head returned the shard (header + shard checksum)
-    bool usable = false;   // a header qfec_zfec can check (1 <= k < n <= 15, ik < n)
-    std::vector<uint8_t> shard;  // the unpacked shard (after header and checksum)
-    bool src_ok = false;   // dec_src_pkt_info on it (source packets)
-    int src_size = 0;      // its size field
-    std::vector<uint8_t> payload;
+    bool fec = false;     // tag 0xEC / 0xED and size >= 11
+    bool ok = false;      // unpack_fec_head returned the shard (header + shard checksum)
+    bool usable = false;  // a header qfec_zfec can check (1 <= k < n <= 15, ik < n)
+    View shard;           // the unpacked shard (after header and checksum)
+    bool src_ok = false;  // dec_src_pkt_info on it (source packets)
+    int src_size = 0;     // its size field
+    View payload;
 };
 
 struct DecodeKey {
@@ -372,17 +461,16 @@ struct DecodeKey {
 };
 struct DecodeOut {
     bool ok[16] = {};
-    std::vector<uint8_t> payload[16];
+    View payload[16];
 };
 struct DecodeReq {
     DecodeKey key;
-    std::vector<std::pair<std::vector<uint8_t>, int>> shards;  // (shard bytes, ik)
+    std::vector<std::pair<View, int>> shards;  // (shard, ik)
 };
 
 struct RxPass {
     std::map<DecodeKey, DecodeOut>* cache;
     std::vector<DecodeReq>* missing;
-    bool emit;
 };
 
 // the receive side of one session over its queued ops (NetFecCodec.cpp:189-371)
@@ -411,11 +499,23 @@ class RxMachine {
     std::vector<std::vector<Emit>>& out;
     std::vector<Emit>* cur = nullptr;
 
-    void deliver(const uint8_t* p, size_t n, uint32_t src) {
-        if (!pass.emit) return;
+    void deliver(const View& v, uint32_t src) {
         Emit e;
         e.kind = 2;
-        e.bytes.assign(p, p + n);
+        e.v = v;
+        e.src = src;
+        cur->push_back(std::move(e));
+    }
+    // a decoded row: its payload, or a placeholder (kind 3) naming the request and row
+    void deliver_decoded(const DecodeOut* res, int req, int i, uint32_t src) {
+        if (res) {
+            deliver(res->payload[i], src);
+            return;
+        }
+        Emit e;
+        e.kind = 3;
+        e.batch = req;
+        e.row = i;
         e.src = src;
         cur->push_back(std::move(e));
     }
@@ -438,8 +538,8 @@ class RxMachine {
             const int ns = (int)(end - R.second);
             const int span = (int)(R.second - R.first);
             for (int is = ns; is < span; ++is) {
-                R.slots[is - ns].assign(R.slots[is]);
-                R.slots[is].reset(R.slots[is].MaxBufSize);
+                R.slots[is - ns] = R.slots[is];
+                R.slots[is].reset();
             }
             R.first += (uint32_t)ns;
             R.second += (uint32_t)ns;
@@ -453,10 +553,10 @@ class RxMachine {
                 if (s.bValid && s.bSourcePkt) {  // (a stored source packet passed dec_src_pkt_info)
                     if (!used(i)) {
                         R.fec_src_count++;
-                        deliver(s.payload.data(), s.payload.size(), s.i_source_pkt);
+                        deliver(s.payload, s.i_source_pkt);
                         set_used(i, true);
                     }
-                    s.reset(s.MaxBufSize);
+                    s.reset();
                     ret = true;
                 }
             }
@@ -465,10 +565,10 @@ class RxMachine {
     }
     // add_packet_fec_buf :485-535; fills `rows` with the first k valid slots (iValid order)
     bool add_packet(uint32_t ipkt, uint32_t isrc, const Verdict& vd, uint64_t uid, int ik, int k, int n,
-                    uint32_t seg_beg, int* max_size, std::vector<int>* rows, bool* undefined) {
+                    uint32_t seg_beg, int* max_size, int* rows, int* nrows, bool* undefined) {
         if (ipkt >= R.first && ipkt < R.second) {
             Slot& s = R.slots[ipkt - R.first];
-            s.set_packet(vd.shard.data(), (int)vd.shard.size(), uid, ik, vd.payload);
+            s.set_packet(vd.shard, uid, ik, vd.payload);
             s.iPacket = (int64_t)ipkt;
             s.bSourcePkt = ipkt - seg_beg < (uint32_t)k;
             s.i_source_pkt = isrc;
@@ -478,7 +578,6 @@ class RxMachine {
         int valid = 0;
         bool all_src = true;
         *undefined = false;
-        rows->clear();
         for (int i = 0; valid < k && i < n; ++i) {
             const int ck = (int)(seg_beg - R.first + (uint32_t)i);
             if (ck < 0 || ck >= (int)R.slots.size()) continue;
@@ -490,21 +589,22 @@ class RxMachine {
                 if (i > R.dec_kmax && s.BufSize > 0) R.dec_kmax = i;
                 if (s.BufSize > R.dec_pkt_size) R.dec_pkt_size = s.BufSize;
                 if (valid >= R.dec_kmax || i >= R.dec_kmax) *undefined = true;
-                rows->push_back(ck);
+                rows[valid] = ck;
                 *max_size = valid == 0 ? s.BufSize : std::max(*max_size, s.BufSize);
                 ++valid;
                 if (ck >= k) all_src = false;  // (sic: the window index, :523)
             }
         }
+        *nrows = valid;
         return valid == k && !all_src;
     }
 
     void unpack(const Op& op, const Verdict& vd) {  // zfec_unpack_input :189-371
-        const uint8_t* d = op.data.data();
-        const uint32_t size = (uint32_t)op.data.size();
+        const uint8_t* d = op.data->data();
+        const uint32_t size = (uint32_t)op.data->size();
         if (size > (uint32_t)R.dec_pkt_size) R.dec_pkt_size = (int)size;  // unpack_fec_head realloc (:345-352)
         if (!vd.fec) {  // not an FEC datagram: handed over minus its tag, source index 0 (:201-209)
-            if (size >= 1) deliver(d + 1, size - 1, 0u);
+            if (size >= 1) deliver(View{op.data, 1, size - 1}, 0u);
             return;
         }
         R.is_checksum = d[0] == 0xED;  // (:364)
@@ -522,23 +622,22 @@ class RxMachine {
             if (!R.is_sorted) {
                 if (!used(i_recv)) {
                     R.fec_src_count++;
-                    deliver(vd.payload.data(), vd.payload.size(), seg_src_beg + (uint32_t)cur_ni);
+                    deliver(vd.payload, seg_src_beg + (uint32_t)cur_ni);
                 }
                 bused = true;
             }
             if (i_recv == R.i_expected_packet && R.is_sorted) {
                 R.fec_src_count++;
-                deliver(vd.payload.data(), vd.payload.size(), seg_src_beg + (uint32_t)cur_ni);
+                deliver(vd.payload, seg_src_beg + (uint32_t)cur_ni);
                 bused = true;
                 R.i_expected_packet++;
                 if (cmod((int)(R.i_expected_packet - seg_beg), cur_n) == cur_k) R.i_expected_packet = seg_beg + (uint32_t)cur_n;
             }
         }
-        int max_size = 0;
-        std::vector<int> rows;
+        int max_size = 0, rows[16], nrows = 0;
         bool undefined = false;
-        const bool dec = add_packet(i_recv, src, vd, (uint64_t)(uint32_t)op.b << 32 | (uint32_t)op.c, cur_ni, cur_k,
-                                    cur_n, seg_beg, &max_size, &rows, &undefined);
+        const bool dec = add_packet(i_recv, src, vd, op.uid, cur_ni, cur_k, cur_n, seg_beg, &max_size, rows, &nrows,
+                                    &undefined);
         set_used(i_recv, bused);
         if (!dec && i_recv - R.i_expected_packet >= (uint32_t)(2 * cur_n) && R.is_sorted) {  // :289-293
             flush_avail(R.i_expected_packet, seg_beg);
@@ -560,17 +659,17 @@ class RxMachine {
         key.n = cur_n;
         key.mode = R.is_checksum ? 1 : 0;
         key.dec_pkt_size = R.dec_pkt_size;
-        for (int ck : rows) key.rows.emplace_back(R.slots[ck].uid, R.slots[ck].ik);
+        key.rows.reserve((size_t)nrows);
+        for (int r = 0; r < nrows; ++r) key.rows.emplace_back(R.slots[rows[r]].uid, R.slots[rows[r]].ik);
         auto it = pass.cache->find(key);
         const DecodeOut* res = it == pass.cache->end() ? nullptr : &it->second;
+        int req = -1;  // index of this decode's request (placeholders refer to it)
         if (!res) {
             DecodeReq q;
-            q.key = key;
-            for (int ck : rows)
-                q.shards.emplace_back(std::vector<uint8_t>(R.slots[ck].fec_buf.begin(),
-                                                           R.slots[ck].fec_buf.begin() + R.slots[ck].BufSize),
-                                      R.slots[ck].ik);
+            q.key = std::move(key);
+            for (int r = 0; r < nrows; ++r) q.shards.emplace_back(R.slots[rows[r]].shard, R.slots[rows[r]].ik);
             pass.missing->push_back(std::move(q));
+            req = (int)pass.missing->size() - 1;
         }
         for (int i = 0; i < cur_k; ++i) {  // :308-366
             // an unknown result counts as a good packet for this pass (it is not emitted)
@@ -578,7 +677,7 @@ class RxMachine {
             const uint32_t pk = seg_beg + (uint32_t)i;
             if (!R.is_sorted) {
                 if (!used(pk)) {
-                    if (res) deliver(res->payload[i].data(), res->payload[i].size(), seg_src_beg + (uint32_t)i);
+                    deliver_decoded(res, req, i, seg_src_beg + (uint32_t)i);
                     set_used(pk, true);
                     R.fec_src_count++;
                     R.fec_restore_count++;
@@ -586,7 +685,7 @@ class RxMachine {
             }
             if (pk >= R.i_expected_packet && R.is_sorted) {
                 if (!used(pk)) {
-                    if (res) deliver(res->payload[i].data(), res->payload[i].size(), seg_src_beg + (uint32_t)i);
+                    deliver_decoded(res, req, i, seg_src_beg + (uint32_t)i);
                     set_used(pk, true);
                     R.fec_src_count++;
                     R.fec_restore_count++;
@@ -599,9 +698,8 @@ class RxMachine {
     }
 };
 
-void init_rx(RxState& R, int max_pkt, int buf_items, int kmax) {
-    R.slots.assign((size_t)buf_items, Slot());
-    for (auto& s : R.slots) s.reset(max_pkt + 16);  // init_zfec_layer :653-664
+void init_rx(RxState& R, int buf_items, int max_pkt, int kmax) {
+    R.slots.assign((size_t)buf_items, Slot());  // init_zfec_layer :653-664
     R.first = 0;
     R.second = (uint32_t)buf_items;
     R.dec_pkt_size = packed_size(max_pkt);  // init_fec_buf :433-434
@@ -618,6 +716,9 @@ qfec_zfec* qfec_zfec_new(void) { return new (std::nothrow) qfec_zfec(); }
 void qfec_zfec_free(qfec_zfec* z) {
     if (!z) return;
     for (auto& kv : z->codes) qfec_code_free(kv.second);
+    z->pack_arena.release();
+    z->rx_arena.release();
+    z->dec_arena.release();
     delete z;
 }
 
@@ -630,7 +731,7 @@ int qfec_zfec_session(qfec_zfec* z, void* peer, int max_pkt_size, int buf_items,
     S.peer = peer;
     S.max_pkt = max_pkt_size;
     S.kmax = kmax;
-    init_rx(S.rx, max_pkt_size, buf_items, kmax);
+    init_rx(S.rx, buf_items, max_pkt_size, kmax);
     S.rx.is_sorted = true;  // init_zfec_layer :634, then enable_sorted_zfec below
     // FecTransmission::Init (FecTransmission.cpp:240-257): the candidate list, then (k, n)
     const int ka[8] = {2, 3, 5, 4, 3, 4, 5, 7}, na[8] = {4, 5, 8, 6, 4, 5, 6, 8};
@@ -641,37 +742,32 @@ int qfec_zfec_session(qfec_zfec* z, void* peer, int max_pkt_size, int buf_items,
         S.tx.k = rk;
         S.tx.n = rn;
     }
-    z->sessions.push_back(std::move(S));
-    const int s = (int)z->sessions.size() - 1;
-    Session& T = z->sessions[s];
-    T.rx.codecs = T.tx.codecs;
-    // the same set_zfec_kn(k, n) both sides see, queued like any later call
+    S.rx.codecs = S.tx.codecs;
+    // the same set_zfec_kn(k, n) both sides see, then enable_zfec and enable_sorted_zfec,
+    // queued like any later call
     Op o;
     o.t = OP_SETKN;
     o.a = k;
     o.b = n;
     o.c = 1;
-    T.ops.push_back(o);
+    S.ops.push_back(o);
     Op e;
     e.t = OP_ENABLE;
     e.a = enabled ? 1 : 0;
-    T.ops.push_back(e);
+    S.ops.push_back(e);
     Op so;
     so.t = OP_SORTED;
     so.a = is_sorted ? 1 : 0;
-    T.ops.push_back(so);
-    return s;
+    S.ops.push_back(so);
+    z->sessions.push_back(std::move(S));
+    return (int)z->sessions.size() - 1;
 }
 
 static int push_op(qfec_zfec* z, int s, Op&& op) {
     if (!z) return QFEC_EINVAL;
     std::lock_guard<std::mutex> lk(z->mu);
     if (s < 0 || s >= (int)z->sessions.size()) return QFEC_EINVAL;
-    if (op.t == OP_UNPACK) {  // a uid for the datagram (decode cache keys), in the spare fields
-        const uint64_t uid = z->next_uid++;
-        op.b = (int)(uid >> 32);
-        op.c = (int)(uint32_t)uid;
-    }
+    if (op.t == OP_UNPACK) op.uid = z->next_uid++;
     z->sessions[s].ops.push_back(std::move(op));
     return QFEC_OK;
 }
@@ -714,62 +810,75 @@ int qfec_zfec_lost_rate(qfec_zfec* z, int s, float lost) {
     o.f = lost;
     return push_op(z, s, std::move(o));
 }
+static Buf copy_bytes(const void* p, unsigned int size) {
+    return std::make_shared<const std::vector<uint8_t>>(static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + size);
+}
 int qfec_zfec_pack_input(qfec_zfec* z, int s, const void* data, unsigned int size) {
     if (!data && size) return QFEC_EINVAL;
     Op o;
     o.t = OP_PACK;
-    o.data.assign(static_cast<const uint8_t*>(data), static_cast<const uint8_t*>(data) + size);
+    o.data = copy_bytes(data, size);
     return push_op(z, s, std::move(o));
 }
 int qfec_zfec_unpack_input(qfec_zfec* z, int s, const void* datagram, unsigned int size) {
     if (!datagram && size) return QFEC_EINVAL;
     Op o;
     o.t = OP_UNPACK;
-    o.data.assign(static_cast<const uint8_t*>(datagram), static_cast<const uint8_t*>(datagram) + size);
+    o.data = copy_bytes(datagram, size);
     return push_op(z, s, std::move(o));
 }
 
 int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn unpack_out, void* stream) {
     if (!z) return QFEC_EINVAL;
     std::lock_guard<std::mutex> lk(z->mu);
+    // QFEC_ZFEC_TIMING=1: phase times of each flush on stderr (profiling aid)
+    static const bool timing = getenv("QFEC_ZFEC_TIMING") != nullptr;
+    auto t_prev = std::chrono::steady_clock::now();
+    auto phase = [&](const char* name) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[qfec] zfec flush %-12s %8.3f ms\n", name, std::chrono::duration<double, std::milli>(t - t_prev).count());
+        t_prev = t;
+    };
     hipStream_t st = (hipStream_t)stream;
     const size_t NS = z->sessions.size();
     std::vector<std::vector<std::vector<Emit>>> outs(NS);
     // ---- send: zfec_pack_input (NetFecCodec.cpp:68-175) over every queue; groups to pack
-    std::map<std::pair<int, int>, PackBatch> packs;
-    std::deque<std::vector<uint8_t>> hold;  // payload copies the batches point at (stable addresses)
+    std::vector<PackBatch> packs;
+    std::map<std::pair<int, int>, int> pack_of;  // (k, n) -> index in packs
+    auto batch_for = [&](int k, int n) -> int {
+        auto it = pack_of.find(std::make_pair(k, n));
+        if (it != pack_of.end()) return it->second;
+        PackBatch b;
+        b.k = k;
+        b.n = n;
+        packs.push_back(std::move(b));
+        pack_of.emplace(std::make_pair(k, n), (int)packs.size() - 1);
+        return (int)packs.size() - 1;
+    };
     for (size_t si = 0; si < NS; ++si) {
         Session& S = z->sessions[si];
         TxState& T = S.tx;
         outs[si].resize(S.ops.size());
-        // a group whose rows span this flush: (batch, index) of its pack entry
-        auto open_entry = [&](std::vector<Emit>& out, int row) {
+        std::vector<std::pair<size_t, int>> pending;  // (op, index in its outputs) of the open group's rows
+        auto open_entry = [&](std::vector<Emit>& out, size_t oi, int row) {
             Emit e;
             e.kind = 0;
             e.row = row;
-            e.batch = T.gk << 4 | T.gn;
+            e.batch = batch_for(T.gk, T.gn);
             out.push_back(e);
+            pending.emplace_back(oi, (int)out.size() - 1);
         };
-        std::vector<std::pair<size_t, int>> pending;  // (op, row) of the open group's rows in this flush
-        auto close_group = [&](bool complete) {
-            if (T.g_pay.empty() && !complete) return;
-            PackBatch& b = packs[std::make_pair(T.gk, T.gn)];
-            b.k = T.gk;
-            b.n = T.gn;
+        auto close_group = [&]() {  // the open group's rows so far, as one group of its batch
+            PackBatch& b = packs[(size_t)batch_for(T.gk, T.gn)];
             PackGroup g;
             g.sent0 = T.g_sent0;
             g.src0 = T.g_src0;
             g.pay.assign((size_t)T.gk, nullptr);
-            for (size_t i = 0; i < T.g_pay.size() && i < (size_t)T.gk; ++i) {
-                hold.push_back(T.g_pay[i]);
-                g.pay[i] = &hold.back();
-            }
+            for (size_t i = 0; i < T.g_pay.size() && i < (size_t)T.gk; ++i) g.pay[i] = T.g_pay[i];
             const long long gi = (long long)b.groups.size();
             b.groups.push_back(std::move(g));
-            for (auto& pr : pending) {
-                Emit& e = outs[si][pr.first][(size_t)pr.second];
-                e.group = gi;
-            }
+            for (auto& pr : pending) outs[si][pr.first][(size_t)pr.second].group = gi;
             pending.clear();
         };
         for (size_t oi = 0; oi < S.ops.size(); ++oi) {
@@ -797,11 +906,13 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 T.lost_rate = op.f;
             } else if (op.t == OP_PACK) {
                 if (!T.enabled || !T.have_codec) {  // :75-94: [0x13][payload], numbering unchanged
+                    auto v = std::make_shared<std::vector<uint8_t>>();
+                    v->reserve(op.data->size() + 1);
+                    v->push_back(0x13);
+                    v->insert(v->end(), op.data->begin(), op.data->end());
                     Emit e;
                     e.kind = 1;
-                    e.bytes.reserve(op.data.size() + 1);
-                    e.bytes.push_back(0x13);
-                    e.bytes.insert(e.bytes.end(), op.data.begin(), op.data.end());
+                    e.v = View{v, 0, (uint32_t)v->size()};
                     out.push_back(std::move(e));
                     continue;
                 }
@@ -815,18 +926,16 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 const int ik = (int)((T.i_sent_pkt - T.i_cur_segment_beg) % (uint32_t)n);
                 if (ik < k) {
                     T.g_pay.push_back(op.data);
-                    open_entry(out, ik);
-                    pending.emplace_back(oi, (int)out.size() - 1);
+                    open_entry(out, oi, ik);
                     T.i_sent_pkt++;
                     T.i_sent_src_pkt++;
                 }
                 if (ik == k - 1) {  // the check packets (:133-172)
                     for (int j = k; j < n; ++j) {
-                        open_entry(out, j);
-                        pending.emplace_back(oi, (int)out.size() - 1);
+                        open_entry(out, oi, j);
                         T.i_sent_pkt++;
                     }
-                    close_group(true);
+                    close_group();
                     T.g_pay.clear();
                     T.g_emitted = 0;
                     if (T.dynkn) {  // recalc_zfec_kn (:51-65)
@@ -843,60 +952,90 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         // a group still open: its source rows of this flush go out now (they do not depend on
         // the rest of the group); the group is packed again, whole, when it completes
         if (!pending.empty()) {
-            close_group(false);
+            close_group();
             T.g_emitted = (int)T.g_pay.size();
         }
     }
+    phase("tx machine");
     int rc = 0;
-    for (auto& kv : packs)
-        if ((rc = run_pack(z, kv.second, st))) return rc;
+    {
+        // batches laid out back to back at their device extents (the device-only shard
+        // scratch is each batch's last region), so no two batches share arena bytes
+        size_t hend = 0, dend = 0;
+        for (auto& b : packs) {
+            pack_layout(b, dend);
+            hend = b.o_end;
+            dend = b.o_shards + b.groups.size() * b.n * b.sp;
+        }
+        if (!packs.empty()) {
+            if ((rc = z->pack_arena.ensure(hend, dend))) return rc;
+            for (auto& b : packs)
+                if ((rc = run_pack(z, b, st))) return rc;
+        }
+    }
+    phase("pack launch");
     // ---- receive: verdicts of this flush's FEC datagrams (pseudo-groups by (k, n, tag, dec_pkt_size))
     std::vector<std::vector<Verdict>> verd(NS);
-    std::map<std::tuple<int, int, int, int>, UnpackBatch> vb;
+    std::vector<UnpackBatch> vb;
+    std::map<std::tuple<int, int, int, int>, int> vb_of;
     struct Where {
-        std::tuple<int, int, int, int> b;
-        int group, ik;
+        int batch = -1, group = -1, ik = 0;
     };
     std::vector<std::vector<Where>> where(NS);
     // rows taken in each pseudo-group (shared by all sessions: a row's verdict is its own)
-    std::map<std::tuple<int, int, int, int>, std::vector<std::vector<bool>>> open;
+    std::vector<std::vector<uint16_t>> taken;  // per batch, per group: bit ik
     for (size_t si = 0; si < NS; ++si) {
         Session& S = z->sessions[si];
         int dps = S.rx.dec_pkt_size;  // its growth over the queue (unpack_fec_head realloc)
         for (auto& op : S.ops) {
             if (op.t != OP_UNPACK) continue;
             Verdict v;
-            const uint8_t* d = op.data.data();
-            const size_t size = op.data.size();
+            const uint8_t* d = op.data->data();
+            const size_t size = op.data->size();
             if ((int)size > dps) dps = (int)size;
             v.fec = size >= 11 && (d[0] == 0xEC || d[0] == 0xED);
-            Where w{};
-            w.group = -1;
+            Where w;
             if (v.fec) {
                 const uint32_t ikn = (uint32_t)d[9] | (uint32_t)d[10] << 8;
                 const int n = (int)(ikn & 0xF), k = (int)((ikn >> 4) & 0xF), ik = (int)((ikn >> 8) & 0xF);
                 v.usable = k >= 1 && k < n && n <= 15 && ik < n;
                 if (v.usable) {
-                    const auto key = std::make_tuple(k, n, d[0] == 0xED ? 1 : 0, dps);
-                    UnpackBatch& b = vb[key];
-                    b.k = k;
-                    b.n = n;
-                    b.checksum = d[0] == 0xED ? 1 : 0;
-                    b.dec_pkt_size = dps;
-                    auto& used = open[key];
+                    const int cs = d[0] == 0xED ? 1 : 0;
+                    const auto key = std::make_tuple(k, n, cs, dps);
+                    auto it = vb_of.find(key);
+                    int bi;
+                    if (it == vb_of.end()) {
+                        UnpackBatch b;
+                        b.k = k;
+                        b.n = n;
+                        b.checksum = cs;
+                        b.dec_pkt_size = dps;
+                        vb.push_back(std::move(b));
+                        taken.emplace_back();
+                        bi = (int)vb.size() - 1;
+                        vb_of.emplace(key, bi);
+                    } else {
+                        bi = it->second;
+                    }
+                    UnpackBatch& b = vb[(size_t)bi];
+                    auto& used = taken[(size_t)bi];
                     int g = -1;
-                    for (size_t gi = 0; gi < used.size(); ++gi)
-                        if (!used[gi][(size_t)ik]) {
+                    for (size_t gi = used.size() > 8 ? used.size() - 8 : 0; gi < used.size(); ++gi)
+                        if (!((used[gi] >> ik) & 1u)) {
                             g = (int)gi;
                             break;
                         }
                     if (g < 0) {
-                        used.emplace_back((size_t)n, false);
+                        used.push_back(0);
                         g = b.groups++;
                     }
-                    used[(size_t)g][(size_t)ik] = true;
-                    b.rows.push_back(UnpackRow{g, ik, op.data});
-                    w.b = key;
+                    used[(size_t)g] |= (uint16_t)(1u << ik);
+                    b.rows.push_back(UnpackRow{g, ik, View{op.data, 0, (uint32_t)size}, 0});
+                    // the row bytes dec_src_pkt_info may read: head + the shard's size field
+                    const size_t hdr = cs ? 13 : 11;
+                    if (ik < k && size >= hdr + 2)
+                        b.need = std::max(b.need, (size_t)(cs ? 4 : 2) + (d[hdr] | (size_t)d[hdr + 1] << 8));
+                    w.batch = bi;
                     w.group = g;
                     w.ik = ik;
                 }
@@ -905,8 +1044,19 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             where[si].push_back(w);
         }
     }
-    for (auto& kv : vb)
-        if ((rc = run_unpack(z, kv.second, st))) return rc;
+    phase("rx grouping");
+    if (!vb.empty()) {
+        size_t hend = 0, dend = 0;
+        for (auto& b : vb) {
+            unpack_layout(b, dend);
+            hend = b.o_hend;
+            dend = b.o_dend;
+        }
+        if ((rc = z->rx_arena.ensure(hend, dend))) return rc;
+        for (auto& b : vb)
+            if ((rc = run_unpack(z, z->rx_arena, b, st))) return rc;
+        if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
+    }
     for (size_t si = 0; si < NS; ++si) {
         size_t v = 0;
         for (auto& op : z->sessions[si].ops) {
@@ -915,81 +1065,129 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             const Where& w = where[si][v];
             ++v;
             if (w.group < 0) continue;
-            const UnpackBatch& b = vb[w.b];
+            const UnpackBatch& b = vb[(size_t)w.batch];
             const size_t row = (size_t)w.group * b.n + w.ik;
-            const uint8_t* d = op.data.data();
-            const int hdr = d[0] == 0xED ? 13 : 11;
+            const uint32_t size = (uint32_t)op.data->size();
+            const uint32_t hdr = op.data->data()[0] == 0xED ? 13 : 11;
             vd.ok = b.rx[row] >= 0;
-            if (vd.ok) vd.shard.assign(d + hdr, d + op.data.size());
+            if (vd.ok) vd.shard = View{op.data, hdr, size - hdr};
             if (w.ik < b.k && vd.ok) {
                 const int stt = b.status[(size_t)w.group * b.k + w.ik];
                 vd.src_ok = stt >= 0;
                 vd.src_size = b.psize[(size_t)w.group * b.k + w.ik];
-                if (vd.src_ok) {
-                    const uint8_t* sh = b.shards.data() + row * b.sp;
-                    vd.payload.assign(sh + stt, sh + stt + vd.src_size);
-                }
+                // a received row's payload is the datagram's own bytes
+                if (vd.src_ok) vd.payload = View{op.data, hdr + (uint32_t)stt, (uint32_t)vd.src_size};
             }
         }
     }
-    // ---- the receive machines: replay until every decode they call for has its device result
+    phase("verdicts");
+    // ---- the receive machines.  A pass that meets a decode without a device result assumes
+    // every row of it decoded and passed (the common case) and leaves placeholders for its
+    // deliveries; after the launches the placeholders are filled when that held for every such
+    // decode, and otherwise the machines are replayed from the flush's starting state.
     std::map<DecodeKey, DecodeOut> cache;
     std::vector<RxState> start(NS);
     for (size_t si = 0; si < NS; ++si) start[si] = z->sessions[si].rx;
-    for (;;) {
+    for (int pass_no = 0;; ++pass_no) {
         std::vector<DecodeReq> missing;
-        RxPass pass{&cache, &missing, true};
+        RxPass pass{&cache, &missing};
         for (size_t si = 0; si < NS; ++si) {
             Session& S = z->sessions[si];
-            S.rx = start[si];
-            for (auto& o : outs[si])
-                o.erase(std::remove_if(o.begin(), o.end(), [](const Emit& e) { return e.kind == 2; }), o.end());
+            if (pass_no) S.rx = start[si];
+            if (pass_no)
+                for (auto& o : outs[si])
+                    o.erase(std::remove_if(o.begin(), o.end(), [](const Emit& e) { return e.kind >= 2; }), o.end());
             RxMachine m(S, (int)si, verd[si], pass, outs[si]);
             m.run();
         }
+        phase("rx machine");
         if (missing.empty()) break;
         // one launch per (k, n, mode, dec_pkt_size): each decode is a group holding exactly its k
-        // shards, wrapped as 0xEC datagrams (no shard checksum to re-check)
-        std::map<std::tuple<int, int, int, int>, UnpackBatch> db;
-        std::map<std::tuple<int, int, int, int>, std::vector<const DecodeReq*>> reqs;
-        for (auto& q : missing) {
-            if (cache.count(q.key)) continue;
-            const auto key = std::make_tuple(q.key.k, q.key.n, q.key.mode, q.key.dec_pkt_size);
-            UnpackBatch& b = db[key];
-            b.k = q.key.k;
-            b.n = q.key.n;
-            b.checksum = q.key.mode;
-            b.dec_pkt_size = q.key.dec_pkt_size;
-            const int g = b.groups++;
-            for (auto& sh : q.shards) {
-                std::vector<uint8_t> dg(11 + sh.first.size(), 0);
-                dg[0] = 0xEC;
-                const uint32_t ikn = (uint32_t)b.n | (uint32_t)b.k << 4 | (uint32_t)sh.second << 8;
-                dg[9] = (uint8_t)(ikn & 0xFF);
-                dg[10] = (uint8_t)(ikn >> 8);
-                if (!sh.first.empty()) memcpy(dg.data() + 11, sh.first.data(), sh.first.size());
-                b.rows.push_back(UnpackRow{g, sh.second, std::move(dg)});
+        // shards, wrapped as 0xEC datagrams (no shard checksum to re-check).  Round 0 decodes at
+        // the shards' own length; a row whose size field reaches past that pitch (only a corrupt
+        // one can) is decoded again at dec_pkt_size + 4 in round 1, as the reference reads it.
+        std::vector<const DecodeReq*> todo;
+        for (auto& q : missing)
+            if (!cache.count(q.key)) {
+                cache[q.key];  // filled below
+                todo.push_back(&q);
             }
-            reqs[key].push_back(&q);
-            cache[q.key];  // placeholder, filled below
-        }
-        for (auto& kv : db) {
-            UnpackBatch& b = kv.second;
-            if ((rc = run_unpack(z, b, st))) return rc;
-            const auto& rq = reqs[kv.first];
-            for (size_t g = 0; g < rq.size(); ++g) {
-                DecodeOut& o = cache[rq[g]->key];
-                for (int i = 0; i < b.k; ++i) {
-                    const int stt = b.status[g * b.k + i];
-                    o.ok[i] = stt >= 0;
-                    if (stt >= 0) {
-                        const uint8_t* sh = b.shards.data() + (g * b.n + i) * b.sp;
-                        o.payload[i].assign(sh + stt, sh + stt + b.psize[g * b.k + i]);
+        for (int round = 0; round < 2 && !todo.empty(); ++round) {
+            std::vector<UnpackBatch> db;
+            std::map<std::tuple<int, int, int, int>, int> db_of;
+            std::vector<std::vector<const DecodeReq*>> reqs;
+            for (const DecodeReq* q : todo) {
+                const auto key = std::make_tuple(q->key.k, q->key.n, q->key.mode, q->key.dec_pkt_size);
+                auto it = db_of.find(key);
+                int bi;
+                if (it == db_of.end()) {
+                    UnpackBatch b;
+                    b.k = q->key.k;
+                    b.n = q->key.n;
+                    b.checksum = q->key.mode;
+                    b.dec_pkt_size = q->key.dec_pkt_size;
+                    b.want_shards = true;
+                    b.need = round ? (size_t)b.dec_pkt_size + 4 : 0;
+                    db.push_back(std::move(b));
+                    reqs.emplace_back();
+                    bi = (int)db.size() - 1;
+                    db_of.emplace(key, bi);
+                } else {
+                    bi = it->second;
+                }
+                UnpackBatch& b = db[(size_t)bi];
+                const int g = b.groups++;
+                for (auto& sh : q->shards) b.rows.push_back(UnpackRow{g, sh.second, sh.first, 1});
+                reqs[(size_t)bi].push_back(q);
+            }
+            size_t hend = 0, dend = 0;
+            for (auto& b : db) {
+                unpack_layout(b, dend);
+                hend = b.o_hend;
+                dend = b.o_dend;
+            }
+            if ((rc = z->dec_arena.ensure(hend, dend))) return rc;
+            for (auto& b : db)
+                if ((rc = run_unpack(z, z->dec_arena, b, st))) return rc;
+            if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
+            std::vector<const DecodeReq*> again;
+            for (size_t bi = 0; bi < db.size(); ++bi) {
+                const UnpackBatch& b = db[bi];
+                // the decoded data rows outlive this round's arena: one owned copy per batch
+                Buf keep = std::make_shared<const std::vector<uint8_t>>(b.shards, b.shards + (size_t)b.groups * b.k * b.sp);
+                const auto& rq = reqs[bi];
+                const int head = b.checksum ? 4 : 2;
+                for (size_t g = 0; g < rq.size(); ++g) {
+                    bool cut = false;
+                    DecodeOut& o = cache[rq[g]->key];
+                    for (int i = 0; i < b.k; ++i) {
+                        const int stt = b.status[g * b.k + i], ps = b.psize[g * b.k + i];
+                        cut |= stt == -1 && ps < b.dec_pkt_size && (size_t)(head + ps) > b.sp;
+                        o.ok[i] = stt >= 0;
+                        o.payload[i] = stt >= 0 ? View{keep, (uint32_t)((g * b.k + i) * b.sp + stt), (uint32_t)ps} : View{};
                     }
+                    if (cut && round == 0) again.push_back(rq[g]);
                 }
             }
+            todo.swap(again);
         }
+        phase("decodes");
+        bool all_ok = true;
+        for (auto& q : missing) {
+            const DecodeOut& o = cache[q.key];
+            for (int i = 0; i < q.key.k; ++i) all_ok &= o.ok[i];
+        }
+        if (!all_ok) continue;  // replay with the results
+        for (size_t si = 0; si < NS; ++si)  // the assumption held: fill the placeholders
+            for (auto& o : outs[si])
+                for (auto& e : o)
+                    if (e.kind == 3) {
+                        e.kind = 2;
+                        e.v = cache[missing[(size_t)e.batch].key].payload[e.row];
+                    }
+        break;
     }  // (terminates: a pass that asks for decodes adds their keys to the cache)
+    if (!packs.empty() && hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
     // ---- callbacks, session by session, op by op
     int calls = 0;
     for (size_t si = 0; si < NS; ++si) {
@@ -997,20 +1195,21 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         for (size_t oi = 0; oi < S.ops.size(); ++oi) {
             for (auto& e : outs[si][oi]) {
                 if (e.kind == 0) {
-                    const PackBatch& b = packs[std::make_pair(e.batch >> 4, e.batch & 15)];
+                    const PackBatch& b = packs[(size_t)e.batch];
                     const size_t row = (size_t)e.group * b.n + e.row;
                     if (b.wlen[row] > 0 && pack_out)
-                        pack_out(S.peer, reinterpret_cast<const char*>(b.wire.data() + row * b.wp), (unsigned)b.wlen[row]);
+                        pack_out(S.peer, reinterpret_cast<const char*>(b.wire + row * b.wp), (unsigned)b.wlen[row]);
                 } else if (e.kind == 1) {
-                    if (pack_out) pack_out(S.peer, reinterpret_cast<const char*>(e.bytes.data()), (unsigned)e.bytes.size());
+                    if (pack_out) pack_out(S.peer, reinterpret_cast<const char*>(e.v.p()), e.v.len);
                 } else if (unpack_out) {
-                    unpack_out(S.peer, reinterpret_cast<const char*>(e.bytes.data()), (unsigned)e.bytes.size(), e.src);
+                    unpack_out(S.peer, reinterpret_cast<const char*>(e.v.p()), e.v.len, e.src);
                 }
                 ++calls;
             }
         }
         S.ops.clear();
     }
+    phase("callbacks");
     return calls;
 }
 

@@ -50,3 +50,14 @@ def test_zfec_loopback_one_session():
     assert [g[1] for g in got] == pay
     assert [g[2] for g in got] == list(range(50))
     z.close()
+
+
+def test_zfec_forged_check_packets():
+    """As tests/test_zfec_host.py::test_host_forged_check_packets, on the device."""
+    scripts = [make_script(7000 + i, phases=6, pair=p) for i, p in enumerate(PAIRS)]
+    for sc in scripts:
+        for ph in sc["phases"]:
+            ph["chan"]["forge"] = 0.5
+    z = qa.Zfec()
+    replay(z, scripts, [run_oracle(s) for s in scripts], "one_flush")
+    z.close()

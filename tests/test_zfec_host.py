@@ -79,3 +79,18 @@ def test_host_many_small_flushes(host_layer):
     assert (s["fec_src_count"], s["fec_restore_count"], s["i_expected_packet"]) == \
         (st["fec_src_count"], st["fec_restore_count"], st["i_expected_packet"])
     z.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_host_forged_check_packets(host_layer, seed):
+    """Half the check datagrams forged (shard bytes changed, datagram checksum recomputed):
+    decodes then produce arbitrary size fields, some beyond the decode's first pitch, which the
+    layer decodes again at dec_pkt_size + 4 as the reference reads them."""
+    import quicknet_amd as qa
+    scripts = [make_script(5000 + 1000 * seed + i, phases=6, pair=p) for i, p in enumerate(PAIRS)]
+    for sc in scripts:
+        for ph in sc["phases"]:
+            ph["chan"]["forge"] = 0.5
+    z = qa.Zfec(_lib=host_layer)
+    replay(z, scripts, [run_oracle(s) for s in scripts], "one_flush")
+    z.close()

@@ -139,6 +139,24 @@ hipError_t hipMemcpyAsync(void* dst, const void* src, size_t n, hipMemcpyKind, h
     memcpy(dst, src, n);
     return hipSuccess;
 }
+hipError_t hipMemcpy2DAsync(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t height,
+                            hipMemcpyKind, hipStream_t) {
+    for (size_t r = 0; r < height; ++r)
+        memcpy(static_cast<uint8_t*>(dst) + r * dpitch, static_cast<const uint8_t*>(src) + r * spitch, width);
+    return hipSuccess;
+}
 hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+hipError_t hipHostMalloc(void** p, size_t n, unsigned int) {
+    *p = malloc(n);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipHostFree(void* p) {
+    free(p);
+    return hipSuccess;
+}
+hipError_t hipGetDevice(int* d) {
+    *d = 0;
+    return hipSuccess;
+}
 
 }  // extern "C"

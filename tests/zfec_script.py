@@ -20,7 +20,7 @@ PAIRS = [dict(), dict(is_sorted=True), dict(k=3, n=5, buf_items=24), dict(k=7, n
          dict(max_pkt_size=1400, k=2, n=4), dict(enabled=False, is_sorted=True)]
 
 
-def make_script(seed, phases=8, pair=None):
+def make_script(seed, phases=8, pair=None, forge=True):
     """-> dict(config, phases=[dict(tx=[op], rx_cfg=[op], chan=[...])]); ops are tuples."""
     rng = random.Random(seed)
     cfg = dict(max_pkt_size=2048, buf_items=48, kmax=10, k=4, n=5, enabled=True, is_sorted=False)
@@ -48,7 +48,7 @@ def make_script(seed, phases=8, pair=None):
         chan = dict(seed=rng.getrandbits(32), loss=rng.choice([0.0, 0.05, 0.2, 0.35]),
                     dup=rng.choice([0.0, 0.05]), swap=rng.choice([0.0, 0.1, 0.4]),
                     corrupt=rng.choice([0.0, 0.03]), late=rng.choice([0.0, 0.05]),
-                    burst=rng.random() < 0.2)
+                    burst=rng.random() < 0.2, forge=rng.choice([0.0, 0.0, 0.1]) if forge else 0.0)
         out.append(dict(tx=tx, rx_cfg=rx_cfg, chan=chan))
     return dict(config=cfg, phases=out)
 
@@ -70,6 +70,17 @@ def channel(datagrams, chan, carry):
             j = rng.randint(13, len(b) - 1)  # shard bytes only: the datagram checksum catches it
             b[j] ^= 1 << rng.randint(0, 7)
             d = bytes(b)
+        if rng.random() < chan.get("forge", 0.0) and len(d) > 16 and d[0] == 0xED:
+            # a forged check packet: shard bytes changed and the datagram checksum recomputed,
+            # so it passes unpack_fec_head and poisons its group's decode (check packets carry
+            # no payload checksum); the decoded rows' size fields are then arbitrary
+            ikn = d[9] | d[10] << 8
+            if (ikn >> 8) & 15 >= (ikn >> 4) & 15:
+                b = bytearray(d)
+                b[13 + rng.randint(0, min(3, len(b) - 14))] ^= rng.randint(1, 255)
+                cs = sum(b[13:]) & 0xFFFF
+                b[11], b[12] = cs & 0xFF, cs >> 8
+                d = bytes(b)
         if rng.random() < chan["late"]:
             carry.append(d)
             continue
