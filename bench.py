@@ -493,6 +493,62 @@ def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=2
     return out
 
 
+def wire_leg(rank, G=100_000, k=10, m=3, S=1024, steps=10, warmup=3):
+    """SURVEY 8(f) ranks 2-3 in the line: the FEC datagram batches of network/FecCodecBuf.cpp on
+    the device, RS(10,13) with 1 KiB payloads (the fec.c matrix the network layer links), 3 of 13
+    datagrams lost per group.  Send = qfec_pack_datagrams (shards, checksums, headers, check
+    packets); receive = qfec_unpack_datagrams (header and datagram checksums, decode of the first
+    k valid rows, dec_src_pkt_info).  Rates count payload bytes; the fractions count the minimal
+    traffic (payload in + datagrams out; datagrams received in + data shard rows out) against
+    8 TB/s.  Verified: every payload restored byte for byte with status 4 (checksummed)."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = k + m
+    code = qa.Code.vandermonde(k, m)
+    payload = torch.empty(G * k * S + 16, dtype=torch.uint8, device=dev)
+    qa.synth_fill(payload, rank_seed(SEED_ENCODE ^ 0x77, rank))
+    offsets = torch.arange(G * k, dtype=torch.int64, device=dev) * S
+    sizes = torch.full((G * k,), S, dtype=torch.int32, device=dev)
+    seq = torch.stack([torch.arange(G, dtype=torch.int32, device=dev) * n,
+                       torch.arange(G, dtype=torch.int32, device=dev) * k], 1).contiguous()
+    lost = torch.from_numpy(erasure_marks(rank_seed(SEED_DECODE ^ 0x77, rank), G, n, m).astype(bool)).to(dev)
+    s = torch.cuda.current_stream()
+    out = {}
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(steps):
+            r = fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / steps, r
+
+    sp = (S + 4 + 15) // 16 * 16
+    pack_ms, (shards, wire, wlen) = timed(lambda: code.pack_datagrams(payload, offsets, sizes, seq, shard_pitch=sp,
+                                                                       wire_pitch=(sp + 13 + 15) // 16 * 16))
+    rx_len = torch.where(lost, torch.zeros_like(wlen), wlen).contiguous()
+    pitch = shards.shape[2]
+    unpack_ms, (osh, status, psize, _) = timed(lambda: code.unpack_datagrams(wire, rx_len, shard_pitch=pitch))
+    ok = bool((status == 4).all().item()) and bool((psize == S).all().item())
+    ok = ok and bool(torch.equal(osh[:, :k, 4:4 + S].reshape(-1), payload[:G * k * S]))
+    pay = G * k * S
+    pack_traffic = pay + int(wlen.sum().item())
+    unpack_traffic = int(rx_len.sum().item()) + G * k * ((S + 4 + 15) // 16 * 16)
+    out = {"config": f"RS({k},{n}) fec_new (system/fec.c), {G:,} groups x {k} x {S} B payloads, checksums on, "
+                     f"{m} of {n} datagrams lost per group",
+           "pack_gibs": round(pay / (pack_ms * 1e-3) / GIB, 2), "unpack_gibs": round(pay / (unpack_ms * 1e-3) / GIB, 2),
+           "pack_avg_ms": round(pack_ms, 4), "unpack_avg_ms": round(unpack_ms, 4),
+           "pack_frac": round(pack_traffic / (pack_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "unpack_frac": round(unpack_traffic / (unpack_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "traffic_basis": "min traffic: payload in + datagrams out / datagrams received in + data shard rows out",
+           "verified": ok}
+    del payload, shards, wire, wlen, osh, rx_len
+    torch.cuda.empty_cache()
+    return out
+
+
 def per_call_leg(reps=2000, ref_lib=None):
     """The unchanged drop-in's per-call cost: what network/FecCodecBuf.cpp pays per
     packet when it links libqfec instead of system/fec.c.  RS(10,3) with 1 KiB payloads:
@@ -735,9 +791,14 @@ def main(argv=None):
         except Exception as exc:  # report, never fake
             per_call = {"error": repr(exc)}
 
-    side = None
+    side = wire = None
     if rank == 0 and not args.no_side:
         side = [side_config(fl, sk, sm, sB, sG, sE, rank) for fl, sk, sm, sB, sG, sE in SIDE]
+        try:
+            wire = wire_leg(rank)
+        except Exception as exc:  # report, never fake
+            wire = {"error": repr(exc), "verified": False}
+        ok = ok and bool(wire.get("verified"))
         ok = ok and all(x["verified"] for x in side)
 
     cpu = cpu_mt = None
@@ -813,6 +874,7 @@ def main(argv=None):
             "cpu_baseline": cpu,
             "cpu_baseline_threads": cpu_mt,
             "side_configs": side,
+            "wire": wire,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
