@@ -571,7 +571,7 @@ def wire_leg(rank, G=100_000, k=10, m=3, S=1024, steps=20, warmup=10, spinup_ms=
     return out
 
 
-def per_call_leg(reps=2000, ref_lib=None):
+def per_call_leg(reps=2000, ref_lib=None, batched=True):
     """The unchanged drop-in's per-call cost: what network/FecCodecBuf.cpp pays per
     packet when it links libqfec instead of system/fec.c.  RS(10,3) with 1 KiB payloads:
       fec_encode  one parity packet, sz = 1028 (get_fec_encoded_pkt, FecCodecBuf.cpp:151)
@@ -616,6 +616,8 @@ def per_call_leg(reps=2000, ref_lib=None):
         run(ref_lib, "ref_cpu_")
         return out
     run(qa.lib(), "gpu_")
+    if not batched:
+        return out
     # batched: qfec_encode_host (pinned host buffers in and out) per group vs 3 reference calls
     code = qa.Code.vandermonde(k, n - k)
     batch = []

@@ -200,7 +200,9 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "wire_rx_split"    1 k_unpack_v2, lanes by pitch | 2 16-B | 3 8-B | 0 the round-1 k_unpack_fused
  *   "wire_store_nt"    0-3 non-temporal datagram stores (bit 0 body, bit 1 head)
  *   "wire_chunk"       groups per fused send launch pair (0: as many as fit)
- *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged */
+ *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged
+ *   "percall_spin"     1 a per-call launch of one block is waited for by spinning on the completion
+ *                      word the kernel stores in coherent pinned memory | 0 hipStreamSynchronize */
 int qfec_tune(const char *key, int value);
 
 int qfec_set_kernel_variant(int variant);

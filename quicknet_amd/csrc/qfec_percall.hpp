@@ -18,6 +18,11 @@ struct PcArgs {
     uint32_t pitch;      // multiple of 16
     uint32_t chunks;     // 16-B chunks per row to compute
     uint32_t k, e;
+    // completion word in coherent pinned host memory (nullable): a one-block launch stores
+    // `seq` into it after all of its output is visible to the host, so the caller can spin
+    // on that word instead of waiting for the runtime's completion signal
+    uint32_t* done;
+    uint32_t seq;
     uint32_t tab[kPcMaxCoef * 5];  // [e][k] perm tables (5 dwords: QFEC_TAB_STRIDE's first 5)
 };
 

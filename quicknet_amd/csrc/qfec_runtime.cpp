@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -67,6 +68,7 @@ int hip_fail(hipError_t e, const char* what) {
 
 std::atomic<int> g_variant{QFEC_VARIANT_PERM};
 std::atomic<int> g_percall_fast{1};  // qfec_tune "percall_fast": fec_encode / fec_decode via k_percall
+std::atomic<int> g_percall_spin{1};  // qfec_tune "percall_spin": wait on k_percall's completion word
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -92,6 +94,10 @@ struct DevCtx {
     uint8_t* h_pc = nullptr;
     uint8_t* d_pc = nullptr;  // the device address of h_pc
     size_t pc_cap = 0;
+    uint32_t* h_pc_done = nullptr;  // k_percall's completion word (coherent pinned)
+    uint32_t* d_pc_done = nullptr;
+    uint32_t pc_seq = 0;
+    uint32_t pc_unsynced = 0;       // spin-completed launches since the last stream query
     int init_rc = QFEC_ENODEV;
     // qfec_encode_host: two chunk slots, each with its own stream, event, device buffers
     // and pinned staging (created on first use)
@@ -175,7 +181,13 @@ int ensure_stage(DevCtx& c, size_t dbytes, size_t hbytes) {
 }
 
 int ensure_pc(DevCtx& c, size_t bytes) {
+    if (!c.h_pc_done) {
+        HIP_TRY(hipHostMalloc((void**)&c.h_pc_done, 256, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer((void**)&c.d_pc_done, c.h_pc_done, 0));
+        __atomic_store_n(c.h_pc_done, 0u, __ATOMIC_RELEASE);
+    }
     if (bytes <= c.pc_cap) return QFEC_OK;
+    if (c.h_pc) HIP_TRY(hipStreamSynchronize(c.stream));  // no launch may still use the old block
     if (c.h_pc) HIP_TRY(hipHostFree(c.h_pc));
     c.h_pc = c.d_pc = nullptr;
     c.pc_cap = 0;
@@ -640,6 +652,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "recon_full_lines") && (value == 0 || value == 1)) { tuning().recon_full_lines = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_spin") && (value == 0 || value == 1)) { g_percall_spin = value; return QFEC_OK; }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
 }
@@ -1759,8 +1772,32 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
         a.k = (uint32_t)k;
         a.e = (uint32_t)e;
         for (int i = 0; i < k * e; ++i) memcpy(&a.tab[i * 5], &tab[(size_t)i * QFEC_TAB_STRIDE], 5 * sizeof(uint32_t));
+        // one block: wait on the kernel's completion word (its outputs are visible in host
+        // memory once it is stored), not on the runtime's completion signal
+        const bool spin = a.chunks <= 256 && g_percall_spin.load();
+        a.done = spin ? ctx->d_pc_done : nullptr;
+        a.seq = spin ? ++ctx->pc_seq : 0;
+        if (spin && a.seq == 0) a.seq = ++ctx->pc_seq;  // 0 is the word's initial value
         hipError_t he = launch_percall(a, ctx->stream);
-        if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+        bool seen = false;
+        if (he == hipSuccess && spin) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t it = 1;; ++it) {
+                if (__atomic_load_n(ctx->h_pc_done, __ATOMIC_ACQUIRE) == a.seq) {
+                    seen = true;
+                    break;
+                }
+                __builtin_ia32_pause();
+                // after 2 s the stream synchronise below reports what happened
+                if ((it & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+            }
+            // let the runtime retire finished launches now and then (nothing to wait for)
+            if (seen && ++ctx->pc_unsynced >= 256) {
+                ctx->pc_unsynced = 0;
+                (void)hipStreamQuery(ctx->stream);
+            }
+        }
+        if (he == hipSuccess && !seen) he = hipStreamSynchronize(ctx->stream);
         if (he != hipSuccess) return hip_fail(he, "per-call kernel");
         for (int j = 0; j < e; ++j) memcpy(out[j], ctx->h_pc + (size_t)(k + j) * pitch, (size_t)sz);
         return QFEC_OK;

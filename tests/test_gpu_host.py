@@ -210,17 +210,20 @@ def test_two_ranks_share_gpu_match_single(oracle):
     assert all(x[1] for x in out)  # every rank's reconstruct restored its slice
 
 
-@pytest.mark.parametrize("fast", [1, 0])
-@pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 37), (3, 5, 2052), (16, 20, 1400)])
-def test_per_packet_paths_vs_oracle(oracle, fast, k, n, sz):
+@pytest.mark.parametrize("fast,spin", [(1, 1), (1, 0), (0, 1)])
+@pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 37), (3, 5, 2052), (16, 20, 1400), (3, 5, 8200)])
+def test_per_packet_paths_vs_oracle(oracle, fast, spin, k, n, sz):
     """fec_encode / fec_decode on host packets through the per-call kernel (percall_fast 1:
-    mapped pinned staging, tables in the kernel arguments, one launch) and through the staged
-    DMA path (0), against the oracle's fec.c restatement."""
+    mapped pinned staging, tables in the kernel arguments, one launch; percall_spin 1: the
+    caller waits on the kernel's completion word, 0: on the stream) and through the staged DMA
+    path (percall_fast 0), against the oracle's fec.c restatement.  sz 8200 needs a
+    multi-block launch, which is always waited for on the stream."""
     rng = np.random.default_rng(k * 100 + sz)
     fp = qa.FecParms(k, n)
     full = fp.matrix
     data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
     qa.tune("percall_fast", fast)
+    qa.tune("percall_spin", spin)
     try:
         for idx in range(k, n):
             dst = np.zeros(sz, np.uint8)
@@ -241,6 +244,29 @@ def test_per_packet_paths_vs_oracle(oracle, fast, k, n, sz):
         assert np.array_equal(pk, data)
     finally:
         qa.tune("percall_fast", 1)
+        qa.tune("percall_spin", 1)
+
+
+def test_per_packet_spin_back_to_back(oracle):
+    """2 000 back-to-back fec_encode calls on fresh data each, waited for on the kernel's
+    completion word: every output is the oracle's (a stale completion word or an output read
+    before it landed would show up as a mismatch)."""
+    k, n, sz = 10, 13, 1028
+    fp = qa.FecParms(k, n)
+    full = fp.matrix
+    mul = np.array([[oracle.mul(a, b) for b in range(256)] for a in sorted(set(full[k:].ravel().tolist()))], np.uint8)
+    row_of = {c: i for i, c in enumerate(sorted(set(full[k:].ravel().tolist())))}
+    rng = np.random.default_rng(2024)
+    qa.tune("percall_spin", 1)
+    for call in range(2000):
+        data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+        idx = k + call % (n - k)
+        dst = np.zeros(sz, np.uint8)
+        fp.encode(data, dst, idx, sz)
+        exp = np.zeros(sz, np.uint8)
+        for c in range(k):
+            exp ^= mul[row_of[int(full[idx, c])]][data[c]]
+        assert np.array_equal(dst, exp), call
 
 
 def _gf_row(oracle, c, row):
