@@ -528,7 +528,7 @@ def wire_leg(rank, G=100_000, k=10, m=3, S=1024, steps=20, warmup=10, spinup_ms=
 
     # preallocated outputs, launches straight through the C ABI (no per-call allocation)
     sp = (S + 4 + 15) // 16 * 16
-    wp = (sp + 13 + 15) // 16 * 16
+    wp = (sp + 13 + 63) // 64 * 64  # 64-B multiple: the send writes whole lines
     L = qa.lib()
     shards = torch.empty((G, n, sp), dtype=torch.uint8, device=dev)
     wire = torch.empty((G, n, wp), dtype=torch.uint8, device=dev)

@@ -233,8 +233,8 @@ class Code:
         head = 4 if checksum else 2
         if shard_pitch is None:
             shard_pitch = (int(sizes.max().item()) + head + 15) // 16 * 16 if G else 16
-        if wire_pitch is None:
-            wire_pitch = (shard_pitch + 13 + 15) // 16 * 16
+        if wire_pitch is None:  # the 64-B multiple: the fused send then writes whole lines
+            wire_pitch = (shard_pitch + 13 + 63) // 64 * 64
         dev = payload.device
         shards = torch.empty((G, n, shard_pitch), dtype=torch.uint8, device=dev)
         wire = torch.empty((G, n, wire_pitch), dtype=torch.uint8, device=dev)

@@ -644,6 +644,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
     if (!strcmp(key, "wire_chunk") && value >= 0) { tuning().wire_chunk = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_line") && (value == 0 || value == 1)) { tuning().wire_line = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_tail") && (value == 0 || value == 1)) { tuning().wire_rx_tail = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
@@ -1350,7 +1351,7 @@ int qfec_pack_datagrams(qfec_code* code, const unsigned char* d_payload, const l
     if (tuning().wire_fused) {
         bool launched = false;
         // the fused path never materialises shards; their buffer holds its partial sums
-        // ((pitch + 13) / 256 + 1) * 8 u32 per group  <<  n * pitch bytes
+        // ((wire_pitch + 63) / 256 + 2) * 8 u32 per group  <<  n * pitch bytes
         hipError_t e = launch_pack_fused(a, tab, reinterpret_cast<uint32_t*>(d_shards), s, &launched);
         if (e != hipSuccess) return hip_fail(e, "pack_fused launch");
         if (launched) return QFEC_OK;

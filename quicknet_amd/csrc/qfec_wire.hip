@@ -397,7 +397,7 @@ __device__ __forceinline__ void put_header(uint4& v, uint32_t sent, uint32_t src
     }
 }
 
-template <int K, int M, int HDR>
+template <int K, int M, int HDR, bool LINE>
 __global__ void __launch_bounds__(256) k_pack_body(WireArgs a, const uint8_t* __restrict__ payload,
                                                    const int64_t* __restrict__ offsets,
                                                    const int32_t* __restrict__ sizes,
@@ -406,20 +406,24 @@ __global__ void __launch_bounds__(256) k_pack_body(WireArgs a, const uint8_t* __
                                                    uint64_t g0, uint32_t lanes, uint32_t lpg, DivMagic lpg_div,
                                                    uint64_t row0) {
     constexpr int N = K + M, HEAD = HDR == 13 ? 4 : 2, P = (N + 1) / 2;
-    constexpr int TS = HDR == 13 ? 1 : 0;            // first chunk of the body
-    constexpr int PS = 16 * TS - HDR - HEAD;          // its payload offset (< 0)
+    // first chunk of the body: 1 (HDR 13: k_pack_head writes chunk 0 and byte 16), 4 (HDR 13,
+    // LINE: k_pack_line0 writes the whole first 64-B line), 0 (HDR 11: the body writes all)
+    constexpr int TS = HDR == 13 ? (LINE ? 4 : 1) : 0;
+    constexpr int PS = 16 * TS - HDR - HEAD;  // its payload offset (< 0 unless LINE with HDR 13)
     const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
     const bool live = flat < lanes;  // dead lanes still join the row sums (with zeros)
     const uint32_t gl = (uint32_t)fast_div(flat, lpg_div);
     const uint32_t rem = flat - gl * lpg;
     const uint64_t g = g0 + gl;
     const int t = TS + (int)rem;
-    const bool first = t == TS;          // holds shard byte 0 (HDR 11) / byte 3 (HDR 13)
+    const bool first = PS < 0 && t == TS;  // holds shard byte 0 (HDR 11) / byte 3 (HDR 13)
     const int p = 16 * t - HDR - HEAD;   // payload offset of this chunk's first byte
     int size[K], gmax = 0;
     bool ok = false;
     if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
-    const bool act = ok && 16 * t < HDR + gmax;
+    // LINE: every chunk up to the (64-B multiple) wire pitch is stored, zeros past a datagram,
+    // so each 64-B line of a row is written whole by one store instruction
+    const bool act = ok && (LINE || 16 * t < HDR + gmax);
     uint8_t* out = a.wire + g * (uint64_t)N * a.wire_pitch + 16 * t;
     // all K loads back to back, addresses clamped into the packet (+16 readable bytes)
     uint4 x[K];
@@ -470,7 +474,7 @@ __global__ void __launch_bounds__(256) k_pack_body(WireArgs a, const uint8_t* __
                            ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu, 0);
             v = pick16(true, h, v);
         }
-        if (act && 16 * t < HDR + len) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
+        if (act && (LINE || 16 * t < HDR + len)) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
         if (HDR == 11 && act && first) a.wire_len[g * N + r] = HDR + len;
         if (HDR == 13 && r >= K) {
             const uint32_t s = sum16(v, 0);  // check-shard bytes 0-3 are the head's: zero here
@@ -562,6 +566,107 @@ __global__ void __launch_bounds__(256) k_pack_head(WireArgs a, const int32_t* __
         stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 2);
         if (HDR + len > 16) out[(uint64_t)r * a.wire_pitch + 16] = (uint8_t)(w >> 24);
         wire_len[g * N + r] = HDR + len;
+    }
+}
+
+// HDR 13 with LINE bodies: the first 64-B line (datagram chunks 0-3) of every row, one quad of
+// lanes per group, lane q = chunk q, so each row's line 0 is one store instruction.  Chunk 0
+// is the header + shard bytes 0-2, chunk 1 starts with shard byte 3, chunks 1-3 carry payload
+// bytes 0-46 (and their check-shard bytes); the row sums are the body's partial records plus
+// the quad's own chunks, reduced across the quad.
+__device__ __forceinline__ uint32_t quad_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    return v;
+}
+
+template <int K, int M>
+__global__ void __launch_bounds__(256) k_pack_line0(WireArgs a, const uint8_t* __restrict__ payload,
+                                                    const int64_t* __restrict__ offsets,
+                                                    const int32_t* __restrict__ sizes,
+                                                    const uint32_t* __restrict__ tab,
+                                                    const uint32_t* __restrict__ part,
+                                                    const uint32_t* __restrict__ seq, uint8_t* __restrict__ wire,
+                                                    int32_t* __restrict__ wire_len, uint64_t g0, uint32_t groups,
+                                                    uint32_t lpg, uint64_t row0) {
+    constexpr int N = K + M, HDR = 13, HEAD = 4, P = (N + 1) / 2;
+    const uint32_t flat = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t gl = flat >> 2;
+    const int q = (int)(flat & 3u);
+    const bool live = gl < groups;  // a quad is live or dead as a whole; dead quads still
+                                    // run the DPP reductions (no early return inside a quad)
+    const uint64_t g = g0 + (live ? gl : 0u);
+    int size[K], gmax = 0;
+    bool ok = false;
+    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+    // chunk q: datagram bytes [16q, 16q + 16), payload offset p = 16q - 17
+    const int p = 16 * q - HDR - HEAD;
+    uint4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
+    if (ok && q > 0) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + offsets[g * K + i] + min(max(p, 0), size[i]));
+#pragma unroll
+        for (int i = 0; i < K; ++i) {  // chunk 1: payload byte 0 sits at chunk byte 1
+            const uint4 sh = window(make_uint4(0, 0, 0, 0), x[i], 15);
+            x[i] = mask16(pick16(q == 1, sh, x[i]), q == 1 ? 1 : 0, size[i] - p);
+        }
+    }
+    uint4 acc[M];
+    encode_cols<K, M>(x, acc, tab);
+    // row sums: own chunk (payload / check bytes; shard bytes 0-3 are still zero here) plus the
+    // body's 16-lane records of this group, spread over the quad's lanes
+    uint32_t tot[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) tot[r] = sum16(r < K ? x[r] : acc[r - K], 0);
+    if (live) {
+        const uint64_t flat0 = (uint64_t)gl * lpg;
+        for (uint64_t row = (flat0 >> 4) + (uint64_t)q; row <= (flat0 + lpg - 1) >> 4; row += 4) {
+            const uint32_t* rec = part + (row0 + row) * 2 * P + ((row << 4) >= flat0 ? 0 : P);
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const uint32_t v = rec[j];
+                tot[2 * j] += v & 0xFFFF;
+                if (2 * j + 1 < N) tot[2 * j + 1] += v >> 16;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r) tot[r] = quad_sum(tot[r]);
+    if (!live) return;
+    if (!ok) {
+        if (q == 0)
+            for (int r = 0; r < N; ++r) wire_len[g * N + r] = -1;
+        return;
+    }
+    const uint32_t sent0 = seq[2 * g], src0 = seq[2 * g + 1];
+    uint32_t d[K];  // shard bytes 0-3 of the data rows: [size lo][size hi][cksum lo][cksum hi]
+#pragma unroll
+    for (int i = 0; i < K; ++i) d[i] = ((uint32_t)size[i] & 0xFFFFu) | ((tot[i] & 0xFFFFu) << 16);
+    uint8_t* out = wire + g * (uint64_t)N * a.wire_pitch + 16 * q;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        uint32_t w = d[r < K ? r : 0];  // shard bytes 0-3 of row r
+        if (r >= K) {
+            w = 0;
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const uint32_t* e = tab + ((r - K) * K + i) * QFEC_TAB_STRIDE;
+                w ^= gf_mul4(gf_sel(d[i]), e[0], e[1], e[2], e[3], e[4]);
+            }
+        }
+        const uint32_t dsum = tot[r] + (w & 0xFF) + ((w >> 8) & 0xFF) + ((w >> 16) & 0xFF) + (w >> 24);
+        uint4 v = r < K ? x[r] : acc[r - K];
+        if (q == 0) {
+            v = make_uint4(0, 0, 0, w << 8);
+            put_header<HDR>(v, sent0 + (uint32_t)r, src0 + (uint32_t)(r < K ? r : K - 1),
+                            ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu, dsum);
+        } else if (q == 1) {
+            put_byte(v, 0, w >> 24);
+        }
+        stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 2);
+        if ((r & 3) == q) wire_len[g * N + r] = HDR + (r < K ? size[r] + HEAD : gmax);
     }
 }
 
@@ -1489,9 +1594,15 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s) {
 template <int K, int M, int HDR>
 hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s) {
     // body lanes per group cover chunks [TS, tn): the longest datagram the shard pitch allows;
-    // groups are packed back to back (no rounding), partial sums go per 16-lane row
-    constexpr uint32_t TS = HDR == 13 ? 1 : 0;
-    const uint32_t tn = (uint32_t)((HDR + a.pitch + 15) / 16);
+    // groups are packed back to back (no rounding), partial sums go per 16-lane row.
+    // LINE (tuning "wire_line", when the wire pitch is the 64-B multiple just above HDR + shard
+    // pitch): chunks [TS, wire_pitch / 16), so lanes per group is a multiple of 4 and every
+    // 64-B line of a row is one store instruction (a line written in two parts costs the
+    // memory a read-modify-write: tools/wrskel.hip, profiles/r02zn_wrskel.txt)
+    const bool line = tuning().wire_line && a.wire_pitch % 64 == 0 &&
+                      a.wire_pitch == (HDR + a.pitch + 63) / 64 * 64 && a.wire_pitch / 16 >= (HDR == 13 ? 20u : 16u);
+    const uint32_t TS = HDR == 13 ? (line ? 4 : 1) : 0;
+    const uint32_t tn = line ? (uint32_t)(a.wire_pitch / 16) : (uint32_t)((HDR + a.pitch + 15) / 16);
     const uint32_t lpg = std::max(16u, tn - TS);
     const DivMagic lpg_div = make_div_magic(lpg);
     // groups per body + head launch pair (keeps g0 * lpg % 16 == 0); tuning "wire_chunk"
@@ -1503,9 +1614,17 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
         const uint64_t gn = std::min(per, a.groups - g0);
         const uint32_t lanes = (uint32_t)(gn * lpg);  // the grid covers whole 16-lane rows past it
         const uint64_t row0 = g0 * lpg / 16;
-        hipLaunchKernelGGL((k_pack_body<K, M, HDR>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
-                           a.offsets, a.sizes, a.seq, tab, part, g0, lanes, lpg, lpg_div, row0);
-        if (HDR == 13)
+        if (line)
+            hipLaunchKernelGGL((k_pack_body<K, M, HDR, true>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
+                               a.offsets, a.sizes, a.seq, tab, part, g0, lanes, lpg, lpg_div, row0);
+        else
+            hipLaunchKernelGGL((k_pack_body<K, M, HDR, false>), dim3((lanes + 255) / 256), dim3(256), 0, s, a, a.payload,
+                               a.offsets, a.sizes, a.seq, tab, part, g0, lanes, lpg, lpg_div, row0);
+        if (HDR == 13 && line)
+            hipLaunchKernelGGL((k_pack_line0<K, M>), dim3((unsigned)((gn * 4 + 255) / 256)), dim3(256), 0, s, a,
+                               a.payload, a.offsets, a.sizes, tab, (const uint32_t*)part, a.seq, a.wire, a.wire_len,
+                               g0, (uint32_t)gn, lpg, row0);
+        else if (HDR == 13)
             hipLaunchKernelGGL((k_pack_head<K, M>), dim3((unsigned)((gn + 255) / 256)), dim3(256), 0, s, a, a.sizes,
                                tab, (const uint32_t*)part, a.seq, a.wire, a.wire_len, g0, (uint32_t)gn, lpg, row0);
     }

@@ -37,17 +37,30 @@ def wire_fused(request):
     qa.tune("wire_fused_rx", 1)
 
 
+@pytest.fixture(params=[64, 16], ids=["wire64", "wire16"])
+def wire_align(request):
+    """Wire row pitch rounded to 64 B (the fused send writes whole 64-B lines: body from chunk
+    4 or 0 up to the pitch, k_pack_line0 for the first line) or to 16 B (body + k_pack_head)."""
+    return request.param
+
+
+def wire_pitch_for(shard_pitch, align):
+    return (shard_pitch + 13 + align - 1) // align * align
+
+
 @pytest.mark.parametrize("k,n", WIRE)
 @pytest.mark.parametrize("checksum", [1, 0])
-def test_pack_vs_reference(golden, wire_fused, k, n, checksum):
+def test_pack_vs_reference(golden, wire_fused, wire_align, k, n, checksum):
     z = golden("wire.npz")
     key = f"{k}_{n}_{checksum}"
     sizes, payload, seq = z[f"sizes_{key}"], z[f"payload_{key}"], z[f"seq_{key}"]
     dg, dl = z[f"dgrams_{key}"], z[f"dlen_{key}"]
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     code = qa.Code.vandermonde(k, n - k)
+    sp = (int(sizes.max()) + (4 if checksum else 2) + 15) // 16 * 16
     shards, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq.astype(np.uint32)),
-                                             checksum=bool(checksum))
+                                             checksum=bool(checksum), shard_pitch=sp,
+                                             wire_pitch=wire_pitch_for(sp, wire_align))
     torch.cuda.synchronize()
     wlen = wlen.cpu().numpy()
     wire = wire.cpu().numpy()
@@ -93,8 +106,8 @@ def test_unpack_vs_reference(golden, wire_fused, k, n, checksum):
                     assert status[g, i] == srcinfo[g, i, 0], (g, i)
 
 
-@pytest.mark.parametrize("k,n,checksum", [(10, 13, 1), (4, 6, 1), (14, 15, 0), (5, 8, 1)])
-def test_lossy_roundtrip_vs_oracle(oracle, wire_fused, k, n, checksum):
+@pytest.mark.parametrize("k,n,checksum", [(10, 13, 1), (4, 6, 1), (14, 15, 0), (5, 8, 1), (10, 13, 0), (8, 12, 1)])
+def test_lossy_roundtrip_vs_oracle(oracle, wire_fused, wire_align, k, n, checksum):
     """Pack G groups, drop and corrupt datagrams, unpack: every data packet comes back exactly
     when its group has k valid datagrams; the verdicts match the reference rules (oracle)."""
     rng = np.random.default_rng(k * 100 + n)
@@ -105,7 +118,9 @@ def test_lossy_roundtrip_vs_oracle(oracle, wire_fused, k, n, checksum):
     seq = np.stack([np.arange(G, dtype=np.uint32) * n + 3, np.arange(G, dtype=np.uint32) * k + 9], 1)
     code = qa.Code.vandermonde(k, m)
     full = np.concatenate([np.eye(k, dtype=np.uint8), code.rows])
-    shards, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq), bool(checksum))
+    sp = (int(sizes.max()) + (4 if checksum else 2) + 15) // 16 * 16
+    shards, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq), bool(checksum),
+                                             shard_pitch=sp, wire_pitch=wire_pitch_for(sp, wire_align))
     torch.cuda.synchronize()
     w = wire.cpu().numpy()
     wl = wlen.cpu().numpy()

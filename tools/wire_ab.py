@@ -16,7 +16,8 @@ import torch  # noqa: E402
 
 import quicknet_amd as qa  # noqa: E402
 
-KNOBS = {"wire_fused": 1, "wire_store_nt": 3, "wire_fused_rx": 1, "wire_rx_tail": 1, "wire_chunk": 0, "wire_rx_split": 1}
+KNOBS = {"wire_fused": 1, "wire_store_nt": 3, "wire_fused_rx": 1, "wire_rx_tail": 1, "wire_chunk": 0, "wire_rx_split": 1,
+         "wire_line": 1}
 
 
 def main():
@@ -30,6 +31,7 @@ def main():
     p.add_argument("--variants", default="base;wire_store_nt=0;wire_store_nt=1;wire_fused=0")
     p.add_argument("--unpack", action="store_true", help="time qfec_unpack_datagrams (n - k losses per group)")
     p.add_argument("--align", type=int, default=16, help="shard and wire row pitches rounded to this (16 or 64)")
+    p.add_argument("--wire-align", type=int, default=0, help="wire row pitch rounded to this instead (e.g. 64)")
     a = p.parse_args()
     k, n, G, S = a.k, a.n, a.groups, a.size
     dev = torch.device("cuda:0")
@@ -43,7 +45,8 @@ def main():
     head = 4
     A = a.align
     pitch = (S + head + A - 1) // A * A
-    wpitch = (pitch + 13 + A - 1) // A * A
+    WA = a.wire_align or A
+    wpitch = (pitch + 13 + WA - 1) // WA * WA
     row16 = (S + head + 15) // 16 * 16  # the shard bytes a row carries, for the traffic count
     shards = torch.empty((G, n, pitch), dtype=torch.uint8, device=dev)
     wire = torch.zeros((G, n, wpitch), dtype=torch.uint8, device=dev)
