@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <map>
@@ -276,7 +277,7 @@ void pack_layout(PackBatch& b, size_t base) {
             }
     b.total = total;
     b.sp = round16(maxp + 4);
-    b.wp = round16(b.sp + 13);
+    b.wp = (b.sp + 13 + 63) & ~(size_t)63;  // the 64-B multiple: the fused send writes whole lines
     b.base = base;
     size_t o = base + round16(total + 16);  // payload (16 readable bytes past the last)
     b.o_offs = o;
@@ -1088,17 +1089,46 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     std::map<DecodeKey, DecodeOut> cache;
     std::vector<RxState> start(NS);
     for (size_t si = 0; si < NS; ++si) start[si] = z->sessions[si].rx;
+    // sessions are independent: their machines run on several threads (the decode cache is
+    // only read during a pass), each session collecting its own decode requests; the requests
+    // are then numbered in session order, as one thread would have numbered them
+    size_t rx_ops = 0;
+    for (size_t si = 0; si < NS; ++si) rx_ops += verd[si].size();
+    unsigned rx_threads =
+        rx_ops < 4096 ? 1u : std::max(1u, std::min({8u, std::thread::hardware_concurrency(), (unsigned)NS}));
+    if (const char* e = getenv("QFEC_ZFEC_RX_THREADS"))  // tests: force the threaded machines
+        rx_threads = (unsigned)std::max(1, std::min(64, atoi(e)));
     for (int pass_no = 0;; ++pass_no) {
         std::vector<DecodeReq> missing;
-        RxPass pass{&cache, &missing};
-        for (size_t si = 0; si < NS; ++si) {
+        std::vector<std::vector<DecodeReq>> miss_s(NS);
+        auto run_session = [&](size_t si) {
             Session& S = z->sessions[si];
             if (pass_no) S.rx = start[si];
             if (pass_no)
                 for (auto& o : outs[si])
                     o.erase(std::remove_if(o.begin(), o.end(), [](const Emit& e) { return e.kind >= 2; }), o.end());
+            RxPass pass{&cache, &miss_s[si]};
             RxMachine m(S, (int)si, verd[si], pass, outs[si]);
             m.run();
+        };
+        if (rx_threads <= 1) {
+            for (size_t si = 0; si < NS; ++si) run_session(si);
+        } else {
+            std::atomic<size_t> next{0};
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < rx_threads; ++t)
+                th.emplace_back([&]() {
+                    for (size_t si; (si = next.fetch_add(1)) < NS;) run_session(si);
+                });
+            for (auto& x : th) x.join();
+        }
+        for (size_t si = 0; si < NS; ++si) {
+            const int base = (int)missing.size();
+            if (base)
+                for (auto& o : outs[si])
+                    for (auto& e : o)
+                        if (e.kind == 3) e.batch += base;
+            for (auto& q : miss_s[si]) missing.push_back(std::move(q));
         }
         phase("rx machine");
         if (missing.empty()) break;
@@ -1153,20 +1183,51 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             std::vector<const DecodeReq*> again;
             for (size_t bi = 0; bi < db.size(); ++bi) {
                 const UnpackBatch& b = db[bi];
-                // the decoded data rows outlive this round's arena: one owned copy per batch
-                Buf keep = std::make_shared<const std::vector<uint8_t>>(b.shards, b.shards + (size_t)b.groups * b.k * b.sp);
                 const auto& rq = reqs[bi];
                 const int head = b.checksum ? 4 : 2;
+                // A decode's input rows come back unchanged (zero past their shard), so a
+                // delivered payload that lies inside its input shard is a view of that shard;
+                // only the rebuilt rows (and payloads reaching past an input's shard) outlive
+                // this round's arena as one owned copy per batch.
+                std::vector<std::pair<size_t, size_t>> copy;  // (row in b.shards, bytes)
+                std::vector<const View*> src_of((size_t)b.k);
+                size_t keep_bytes = 0;
                 for (size_t g = 0; g < rq.size(); ++g) {
                     bool cut = false;
                     DecodeOut& o = cache[rq[g]->key];
+                    std::fill(src_of.begin(), src_of.end(), nullptr);
+                    for (auto& sh : rq[g]->shards)
+                        if (sh.second < b.k) src_of[(size_t)sh.second] = &sh.first;
                     for (int i = 0; i < b.k; ++i) {
                         const int stt = b.status[g * b.k + i], ps = b.psize[g * b.k + i];
                         cut |= stt == -1 && ps < b.dec_pkt_size && (size_t)(head + ps) > b.sp;
                         o.ok[i] = stt >= 0;
-                        o.payload[i] = stt >= 0 ? View{keep, (uint32_t)((g * b.k + i) * b.sp + stt), (uint32_t)ps} : View{};
+                        o.payload[i] = View{};
+                        if (stt < 0) continue;
+                        const View* in = src_of[(size_t)i];
+                        if (in && (size_t)stt + (size_t)ps <= in->len) {
+                            o.payload[i] = View{in->b, in->off + (uint32_t)stt, (uint32_t)ps};
+                        } else {
+                            o.payload[i] = View{nullptr, (uint32_t)keep_bytes, (uint32_t)ps};  // buffer set below
+                            copy.emplace_back((g * b.k + i) * b.sp + (size_t)stt, (size_t)ps);
+                            keep_bytes += (size_t)ps;
+                        }
                     }
                     if (cut && round == 0) again.push_back(rq[g]);
+                }
+                if (!copy.empty()) {
+                    auto keep = std::make_shared<std::vector<uint8_t>>(keep_bytes);
+                    size_t o = 0;
+                    for (auto& c : copy) {
+                        if (c.second) memcpy(keep->data() + o, b.shards + c.first, c.second);
+                        o += c.second;
+                    }
+                    const Buf kb = keep;
+                    for (size_t g = 0; g < rq.size(); ++g) {
+                        DecodeOut& o2 = cache[rq[g]->key];
+                        for (int i = 0; i < b.k; ++i)
+                            if (o2.ok[i] && !o2.payload[i].b) o2.payload[i].b = kb;
+                    }
                 }
             }
             todo.swap(again);

@@ -47,6 +47,18 @@ def test_host_sequences_vs_oracle(host_layer, seed, mode):
     z.close()
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_host_threaded_machines_vs_oracle(host_layer, seed, monkeypatch):
+    """The receive machines of a flush's sessions on 3 threads (QFEC_ZFEC_RX_THREADS; large
+    flushes use threads by themselves): the same sequences as the oracle's."""
+    import quicknet_amd as qa
+    monkeypatch.setenv("QFEC_ZFEC_RX_THREADS", "3")
+    scripts = [make_script(5000 + 1000 * seed + i, phases=6, pair=p) for i, p in enumerate(PAIRS)]
+    z = qa.Zfec(_lib=host_layer)
+    replay(z, scripts, [run_oracle(s) for s in scripts], "one_flush")
+    z.close()
+
+
 def test_host_many_small_flushes(host_layer):
     """A flush after every queued call: open groups and the receive window carried across
     hundreds of flushes."""
