@@ -596,31 +596,21 @@ __global__ void __launch_bounds__(256) k_pack_line0(WireArgs a, const uint8_t* _
     const bool live = gl < groups;  // a quad is live or dead as a whole; dead quads still
                                     // run the DPP reductions (no early return inside a quad)
     const uint64_t g = g0 + (live ? gl : 0u);
+    // every load that does not depend on another is issued first: sizes, offsets, seq and the
+    // body's partial-sum records of this group (one 16-lane record row per quad lane and pass)
     int size[K], gmax = 0;
+    int64_t off[K];
     bool ok = false;
-    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
-    // chunk q: datagram bytes [16q, 16q + 16), payload offset p = 16q - 17
-    const int p = 16 * q - HDR - HEAD;
-    uint4 x[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
-    if (ok && q > 0) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + offsets[g * K + i] + min(max(p, 0), size[i]));
-#pragma unroll
-        for (int i = 0; i < K; ++i) {  // chunk 1: payload byte 0 sits at chunk byte 1
-            const uint4 sh = window(make_uint4(0, 0, 0, 0), x[i], 15);
-            x[i] = mask16(pick16(q == 1, sh, x[i]), q == 1 ? 1 : 0, size[i] - p);
-        }
-    }
-    uint4 acc[M];
-    encode_cols<K, M>(x, acc, tab);
-    // row sums: own chunk (payload / check bytes; shard bytes 0-3 are still zero here) plus the
-    // body's 16-lane records of this group, spread over the quad's lanes
     uint32_t tot[N];
 #pragma unroll
-    for (int r = 0; r < N; ++r) tot[r] = sum16(r < K ? x[r] : acc[r - K], 0);
+    for (int r = 0; r < N; ++r) tot[r] = 0;
+    uint32_t sent0 = 0, src0 = 0;
     if (live) {
+        ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+#pragma unroll
+        for (int i = 0; i < K; ++i) off[i] = offsets[g * K + i];
+        sent0 = seq[2 * g];
+        src0 = seq[2 * g + 1];
         const uint64_t flat0 = (uint64_t)gl * lpg;
         for (uint64_t row = (flat0 >> 4) + (uint64_t)q; row <= (flat0 + lpg - 1) >> 4; row += 4) {
             const uint32_t* rec = part + (row0 + row) * 2 * P + ((row << 4) >= flat0 ? 0 : P);
@@ -632,6 +622,26 @@ __global__ void __launch_bounds__(256) k_pack_line0(WireArgs a, const uint8_t* _
             }
         }
     }
+    // chunk q: datagram bytes [16q, 16q + 16), payload offset p = 16q - 17
+    const int p = 16 * q - HDR - HEAD;
+    uint4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
+    if (ok && q > 0) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + off[i] + min(max(p, 0), size[i]));
+#pragma unroll
+        for (int i = 0; i < K; ++i) {  // chunk 1: payload byte 0 sits at chunk byte 1
+            const uint4 sh = window(make_uint4(0, 0, 0, 0), x[i], 15);
+            x[i] = mask16(pick16(q == 1, sh, x[i]), q == 1 ? 1 : 0, size[i] - p);
+        }
+    }
+    uint4 acc[M];
+    encode_cols<K, M>(x, acc, tab);
+    // row sums: own chunk (payload / check bytes; shard bytes 0-3 are still zero here) plus the
+    // body's 16-lane records of this group, spread over the quad's lanes
+#pragma unroll
+    for (int r = 0; r < N; ++r) tot[r] += sum16(r < K ? x[r] : acc[r - K], 0);
 #pragma unroll
     for (int r = 0; r < N; ++r) tot[r] = quad_sum(tot[r]);
     if (!live) return;
@@ -640,7 +650,6 @@ __global__ void __launch_bounds__(256) k_pack_line0(WireArgs a, const uint8_t* _
             for (int r = 0; r < N; ++r) wire_len[g * N + r] = -1;
         return;
     }
-    const uint32_t sent0 = seq[2 * g], src0 = seq[2 * g + 1];
     uint32_t d[K];  // shard bytes 0-3 of the data rows: [size lo][size hi][cksum lo][cksum hi]
 #pragma unroll
     for (int i = 0; i < K; ++i) d[i] = ((uint32_t)size[i] & 0xFFFFu) | ((tot[i] & 0xFFFFu) << 16);
