@@ -130,6 +130,7 @@ struct Tuning {
     int wire_rx_tail = 1;   // fused receive: 1 = tail dwords ride on the last 16-B pass (0: own pass)
     int wire_store_nt = 3;  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
     int wire_line = 1;      // fused send writes whole 64-B lines when the wire pitch allows it
+    int wire_send_wave = 1; // fused send, 1088-B wire pitch: one wave per group finishes line 0 itself (k_pack_wave64)
     int wire_chunk = 0;     // fused send: groups per body + head launch pair (0: as many as fit)
     int host_chunk = 0;     // qfec_encode_host: groups per pipelined chunk (0: ~32 MiB of data)
     int recon_full_lines = 1;  // 8-/12-B reconstruct lanes cover the 16-B columns' span (no partial 64-B lines)

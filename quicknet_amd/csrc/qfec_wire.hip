@@ -702,6 +702,123 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// ------------------------------------------------------------------ send: one wave per group
+// HDR 13 with a 1088-B wire pitch (1 KiB payloads): the body's chunks 4..67 are exactly 64
+// lanes, so with groups wave-aligned each wave holds one whole group and can finish its first
+// 64-B line itself (tuning "wire_send_wave"): wave sums of the body's chunks, then lanes 0..15
+// take dword i of line 0 of every row -- header, shard bytes 0-3, payload bytes 0..46 and
+// their check bytes (a dword-wide encode) -- and store each row's line 0 as one instruction.
+// This replaces k_pack_line0's scattered second pass (13 lines 1088 B apart per group).
+template <int K, int M>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
+                                                     const int64_t* __restrict__ offsets,
+                                                     const int32_t* __restrict__ sizes,
+                                                     const uint32_t* __restrict__ seq,
+                                                     const uint32_t* __restrict__ tab, uint64_t groups) {
+    constexpr int N = K + M, HDR = 13, HEAD = 4;
+    const int lane = threadIdx.x & 63;
+    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));  // wave-uniform
+    if (g >= groups) return;  // whole waves
+    const int t = 4 + lane;
+    const int p = 16 * t - HDR - HEAD;  // payload offset of this chunk's first byte (>= 47)
+    int size[K], gmax = 0;
+    const bool ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+    if (!ok) {
+        if (lane < N) a.wire_len[g * N + lane] = -1;
+        return;
+    }
+    int64_t off[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) off[i] = offsets[g * K + i];
+    uint8_t* out_g = a.wire + g * (uint64_t)N * a.wire_pitch;
+    uint4 x[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = ldu16(payload + off[i] + min(p, size[i]));
+#pragma unroll
+    for (int i = 0; i < K; ++i) x[i] = mask16(x[i], 0, size[i] - p);
+    uint32_t ps[N];  // per-lane byte sums of each row's chunk (payload / check bytes)
+#pragma unroll
+    for (int i = 0; i < K; ++i) ps[i] = sum16(x[i], 0);
+    uint4 acc[M];
+    encode_cols<K, M>(x, acc, tab);
+#pragma unroll
+    for (int r = 0; r < M; ++r) pin16(acc[r]);
+    uint8_t* out = out_g + 16 * t;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        const uint4 v = r < K ? x[r] : acc[r - K];
+        stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
+        if (r >= K) ps[r] = sum16(v, 0);
+    }
+    // ---- line 0
+    // line 0's payload dwords (lanes 0..15: datagram bytes 4 lane .. 4 lane + 3; payload byte
+    // 4 lane - 17 at its first byte)
+    const int q = 4 * lane - HDR - HEAD;
+    uint32_t pay[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        pay[i] = 0;
+        if (lane >= 4 && lane < 16) __builtin_memcpy(&pay[i], payload + off[i] + min(max(q, 0), size[i]), 4);
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        // byte j of the dword holds payload byte q + j (dword 4: loaded from payload byte 0 and
+        // shifted up one byte); keep the bytes below the payload's size
+        const uint32_t v = lane == 4 ? pay[i] << 8 : pay[i];
+        const int nb = min(max(size[i] - q, 0), 4);
+        pay[i] = nb >= 4 ? v : v & ((1u << (8 * nb)) - 1u);
+    }
+    uint32_t tot[N];  // payload sums of the data rows, check-byte sums of the check rows
+#pragma unroll
+    for (int i = 0; i < K; ++i) tot[i] = wave_total(ps[i] + __builtin_amdgcn_sad_u8(pay[i], 0u, 0u));
+    // shard view of line 0's dwords: data row i = [size][cksum] at shard bytes 0-3, then payload
+    uint32_t sh[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const uint32_t w = ((uint32_t)size[i] & 0xFFFFu) | ((tot[i] & 0xFFFFu) << 16);  // shard bytes 0-3
+        sh[i] = lane == 3 ? w << 8 : lane == 4 ? (w >> 24) | pay[i] : pay[i];
+    }
+    uint32_t par[M];  // check rows' shard view: a dword-wide encode of the data rows'
+#pragma unroll
+    for (int j = 0; j < M; ++j) par[j] = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const Sel sl = gf_sel(sh[i]);
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const uint32_t* e = tab + (j * K + i) * QFEC_TAB_STRIDE;
+            par[j] ^= gf_mul4(sl, e[0], e[1], e[2], e[3], e[4]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M; ++j) tot[K + j] = wave_total(ps[K + j] + (lane < 16 ? __builtin_amdgcn_sad_u8(par[j], 0u, 0u) : 0u));
+    const uint32_t sent0 = seq[2 * g], src0 = seq[2 * g + 1];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+        uint32_t dsum;
+        const uint32_t v = r < K ? sh[r] : par[r - K];
+        if (r < K) {
+            const uint32_t w = ((uint32_t)size[r] & 0xFFFFu) | ((tot[r] & 0xFFFFu) << 16);
+            dsum = tot[r] + (w & 0xFF) + ((w >> 8) & 0xFF) + ((w >> 16) & 0xFF) + (w >> 24);
+        } else {
+            dsum = tot[r];  // check shard bytes 0-3 are in par's dwords 3-4, summed above
+        }
+        const uint32_t sent = sent0 + (uint32_t)r, src = src0 + (uint32_t)(r < K ? r : K - 1);
+        const uint32_t ikn = ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu;
+        uint32_t d = v;
+        if (lane == 0) d = 0xEDu | (sent << 8);
+        else if (lane == 1) d = (sent >> 24) | (src << 8);
+        else if (lane == 2) d = (src >> 24) | (ikn << 8) | ((dsum & 0xFFu) << 24);
+        else if (lane == 3) d = ((dsum >> 8) & 0xFFu) | v;
+        if (lane < 16) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(out_g + (uint64_t)r * a.wire_pitch + 4 * lane);
+            if (a.store_nt & 2) __builtin_nontemporal_store(d, dst);
+            else *dst = d;
+        }
+    }
+    if (lane < N) a.wire_len[g * N + lane] = HDR + (lane < K ? size[lane] + HEAD : gmax);
+}
+
 // A lane's slice of a shard row in one pass: NV16 = 4 -> one 16-B chunk at pos16, then NVT
 // tail dwords at tail + 4 * (lane + 64 t) (coalesced per instruction).  Dword d sits at
 // byte pos(d) of the row.
@@ -1610,6 +1727,18 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
     // memory a read-modify-write: tools/wrskel.hip, profiles/r02zn_wrskel.txt)
     const bool line = tuning().wire_line && a.wire_pitch % 64 == 0 &&
                       a.wire_pitch == (HDR + a.pitch + 63) / 64 * 64 && a.wire_pitch / 16 >= (HDR == 13 ? 20u : 16u);
+    // one wave per group when the body's chunks 4..67 are exactly one wave (k_pack_wave64)
+    if (HDR == 13 && line && a.wire_pitch == 1088 && tuning().wire_send_wave) {
+        for (uint64_t g0 = 0; g0 < a.groups; g0 += ((uint64_t)1 << 28)) {
+            const uint64_t gn = std::min((uint64_t)1 << 28, a.groups - g0);
+            WireArgs b = a;
+            b.wire = a.wire + g0 * (uint64_t)(K + M) * a.wire_pitch;
+            b.wire_len = a.wire_len + g0 * (K + M);
+            hipLaunchKernelGGL((k_pack_wave64<K, M>), dim3((unsigned)((gn + 3) / 4)), dim3(256), 0, s, b, a.payload,
+                               a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn);
+        }
+        return hipGetLastError();
+    }
     const uint32_t TS = HDR == 13 ? (line ? 4 : 1) : 0;
     const uint32_t tn = line ? (uint32_t)(a.wire_pitch / 16) : (uint32_t)((HDR + a.pitch + 15) / 16);
     const uint32_t lpg = std::max(16u, tn - TS);

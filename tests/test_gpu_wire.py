@@ -236,3 +236,49 @@ def test_unpack_row_tails(k, n, checksum, pitch):
             assert np.array_equal(sh[g, i, head:head + sz], payload[offs[g * k + i]:offs[g * k + i] + sz]), (g, i)
     ok_rows = (status[:, :] == head).sum()
     assert ok_rows > G * k // 2
+
+
+@pytest.mark.parametrize("k,n", [(10, 13), (4, 6), (8, 12), (5, 8)])
+def test_pack_wave64_matches_line0(oracle, k, n):
+    """1 KiB-class payloads with a 1088-B wire pitch: the one-wave-per-group send
+    (k_pack_wave64, wire_send_wave 1) writes the same datagrams and lengths as the body +
+    k_pack_line0 pair (0), and both equal the oracle's on sampled groups.  Sizes 0..1036
+    (half exactly 1024), one oversize group."""
+    rng = np.random.default_rng(n * 7 + k)
+    G, m = 500, n - k
+    sizes = rng.integers(0, 1037, size=G * k).astype(np.int32)
+    sizes[rng.random(G * k) < 0.5] = 1024
+    sizes[:3] = [0, 1, 46]  # payloads ending inside line 0
+    sizes[7 * k + 1] = 1040  # 1040 + 4 > the 1040-B shard pitch: group 7 is void
+    payload = rng.integers(0, 256, size=int(np.maximum(sizes, 0).sum()) + 1, dtype=np.uint8)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    seq = np.stack([np.arange(G, dtype=np.uint32) * n + 5, np.arange(G, dtype=np.uint32) * k + 2], 1)
+    code = qa.Code.vandermonde(k, m)
+    full = np.concatenate([np.eye(k, dtype=np.uint8), code.rows])
+    res = []
+    for wave in (1, 0):
+        qa.tune("wire_send_wave", wave)
+        try:
+            _, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq), True,
+                                                shard_pitch=1040, wire_pitch=1088)
+            torch.cuda.synchronize()
+        finally:
+            qa.tune("wire_send_wave", 1)
+        res.append((wire.cpu().numpy(), wlen.cpu().numpy()))
+    (w1, l1), (w0, l0) = res
+    assert np.array_equal(l1, l0)
+    assert (l1[7] == -1).all()
+    for g in range(G):
+        if g == 7:
+            continue
+        for j in range(n):
+            assert np.array_equal(w1[g, j, :l1[g, j]], w0[g, j, :l0[g, j]]), (g, j)
+            assert not w1[g, j, l1[g, j]:].any(), (g, j)  # zeros up to the pitch (whole lines)
+    for g in list(rng.choice(G, 20, replace=False)) + [0]:
+        if g == 7:
+            continue
+        out, ln, _ = oracle.pack_group(k, n, full, payload, offs[g * k:(g + 1) * k], sizes[g * k:(g + 1) * k],
+                                       int(seq[g, 0]), int(seq[g, 1]), 1, pitch=1088)
+        assert np.array_equal(ln, l1[g])
+        for j in range(n):
+            assert np.array_equal(out[j, :ln[j]], w1[g, j, :ln[j]]), (g, j)
