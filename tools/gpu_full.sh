@@ -22,6 +22,13 @@ echo "== rocprofv3 kernel trace" && (cd /tmp && timeout -k 10 600 rocprofv3 --ke
   -d $R/$OUT/prof -o trace -- python3 $R/bench.py --no-cpu --no-host --no-side > $R/$OUT/bench_prof.json 2> $R/$OUT/prof.err) || { tail -20 $OUT/prof.err; exit 5; }
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 cut -d, -f1-4 $OUT/kernel_stats.csv | head -6
+echo "== rocprofv3 kernel trace, datagram kernels (bench's wire leg shapes: RS(10,13) 100k x 1 KiB, wire pitch 1088)" && \
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof_wire -o wire -- \
+   python3 $R/tools/wire_ab.py --wire-align 64 --variants base --rounds 3 > $R/$OUT/wire_ab_prof.txt 2> $R/$OUT/prof_wire.err && \
+   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof_wire_rx -o wire -- \
+   python3 $R/tools/wire_ab.py --unpack --wire-align 64 --variants base --rounds 3 >> $R/$OUT/wire_ab_prof.txt 2>> $R/$OUT/prof_wire.err) \
+  || { tail -20 $OUT/prof_wire.err; exit 8; }
+grep -h -E "k_pack|k_unpack" $(find $OUT/prof_wire $OUT/prof_wire_rx -name "*kernel_stats.csv") | cut -d, -f1-4 | cut -c1-120
 echo "== bench --gpus 2 (gloo rehearsal: the launcher's own ranks share the one GPU)" && QFEC_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 --no-cpu > $OUT/bench_g2.json 2> $OUT/bench_g2.err || { tail -20 $OUT/bench_g2.err; exit 7; }
 cut -c1-400 $OUT/bench_g2.json
 echo done
