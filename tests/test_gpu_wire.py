@@ -238,14 +238,14 @@ def test_unpack_row_tails(k, n, checksum, pitch):
     assert ok_rows > G * k // 2
 
 
-@pytest.mark.parametrize("k,n", [(10, 13), (4, 6), (8, 12), (5, 8)])
-def test_pack_wave64_matches_line0(oracle, k, n):
+@pytest.mark.parametrize("k,n,G", [(10, 13, 500), (4, 6, 500), (8, 12, 500), (5, 8, 500), (10, 13, 13)])
+def test_pack_wave64_matches_line0(oracle, k, n, G):
     """1 KiB-class payloads with a 1088-B wire pitch: the one-wave-per-group send
     (k_pack_wave64, wire_send_wave 1) writes the same datagrams and lengths as the body +
     k_pack_line0 pair (0), and both equal the oracle's on sampled groups.  Sizes 0..1036
     (half exactly 1024), one oversize group."""
-    rng = np.random.default_rng(n * 7 + k)
-    G, m = 500, n - k
+    rng = np.random.default_rng(n * 7 + k + G)
+    m = n - k  # G = 13: the last block holds one live wave of four
     sizes = rng.integers(0, 1037, size=G * k).astype(np.int32)
     sizes[rng.random(G * k) < 0.5] = 1024
     sizes[:3] = [0, 1, 46]  # payloads ending inside line 0
@@ -274,7 +274,7 @@ def test_pack_wave64_matches_line0(oracle, k, n):
         for j in range(n):
             assert np.array_equal(w1[g, j, :l1[g, j]], w0[g, j, :l0[g, j]]), (g, j)
             assert not w1[g, j, l1[g, j]:].any(), (g, j)  # zeros up to the pitch (whole lines)
-    for g in list(rng.choice(G, 20, replace=False)) + [0]:
+    for g in list(rng.choice(G, min(G, 20), replace=False)) + [0, G - 1]:
         if g == 7:
             continue
         out, ln, _ = oracle.pack_group(k, n, full, payload, offs[g * k:(g + 1) * k], sizes[g * k:(g + 1) * k],
