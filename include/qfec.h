@@ -200,6 +200,11 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "wire_rx_split"    1 k_unpack_v2, lanes by pitch | 2 16-B | 3 8-B | 0 the round-1 k_unpack_fused
  *   "wire_store_nt"    0-3 non-temporal datagram stores (bit 0 body, bit 1 head)
  *   "wire_chunk"       groups per fused send launch pair (0: as many as fit)
+ *   "wire_line"        1 the fused send writes whole 64-B lines when the wire pitch is the 64-B
+ *                      multiple above 13 + shard pitch (body + k_pack_line0) | 0 body + k_pack_head
+ *   "wire_send_wave"   1 at a 1088-B wire pitch, one wave per group writes its rows' first lines
+ *                      itself (k_pack_wave64) | 0 body + k_pack_line0
+ *   "wire_rx_tail"     1 (k_unpack_fused) tail dwords ride on the last 16-B pass | 0 their own pass
  *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged
  *   "percall_spin"     1 a per-call launch of one block is waited for by spinning on the completion
  *                      word the kernel stores in coherent pinned memory | 0 hipStreamSynchronize */
