@@ -1366,8 +1366,13 @@ __device__ __forceinline__ uint32_t head_bytes_sum(uint32_t w0, int head) {
     return __builtin_amdgcn_sad_u8(head == 4 ? w0 : (w0 & 0xFFFFu), 0u, 0u);
 }
 
-template <int K, int M, int NVA>
-__global__ void __launch_bounds__(256) k_unpack_v2(WireArgs a, const uint8_t* __restrict__ wire,
+// LDSW (tuning "wire_rx_lds"; one wave per block, K * pitch bytes of LDS): the passes write the
+// group's K data rows into LDS, and the wave then stores them as one flat byte range, 1 KiB per
+// instruction, so no 64-B line is written in two parts where a row ends mid-line (pitch 1040)
+extern __shared__ uint4 rx_stage[];
+
+template <int K, int M, int NVA, bool LDSW = false>
+__global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const uint8_t* __restrict__ wire,
                                                    const int32_t* __restrict__ wire_len,
                                                    const int32_t* __restrict__ lut,
                                                    const uint32_t* __restrict__ records, uint32_t rec_hdr,
@@ -1375,12 +1380,13 @@ __global__ void __launch_bounds__(256) k_unpack_v2(WireArgs a, const uint8_t* __
     constexpr int N = K + M;
     constexpr int A = 256 * NVA;  // row bytes per full pass
     const int lane = threadIdx.x & 63;
-    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint64_t g = __builtin_amdgcn_readfirstlane(LDSW ? blockIdx.x : blockIdx.x * 4u + (threadIdx.x >> 6));
     if (g >= a.groups) return;
     const int pitch = (int)a.pitch;
     const uint64_t wp = a.wire_pitch;
     const uint8_t* wire_g = wire + g * (uint64_t)N * wp;
-    uint8_t* out_g = shards + g * a.group_stride;
+    uint8_t* const out_hbm = shards + g * a.group_stride;
+    uint8_t* out_g = LDSW ? reinterpret_cast<uint8_t*>(rx_stage) : out_hbm;
     // ---- headers (unpack_fec_head's checks, FecCodecBuf.cpp:334-411)
     int len = 0, hdr = 11, size = 0;
     uint32_t stated = 0;
@@ -1510,6 +1516,10 @@ __global__ void __launch_bounds__(256) k_unpack_v2(WireArgs a, const uint8_t* __
             break;
         }
         bad |= newbad;
+    }
+    if constexpr (LDSW) {  // the K data rows, staged whole, as one flat range
+        const int total = K * pitch;
+        for (int o = 16 * lane; o < total; o += 1024) st16(out_hbm + o, rx_stage[o >> 4]);
     }
     // ---- per-row results (k_unpack_fused's)
     const uint32_t okrows = good & ~bad;
@@ -1813,6 +1823,22 @@ template <int K, int M>
 hipError_t unpack_v2_shape(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
                            hipStream_t s, int nva) {
     const dim3 grid((unsigned)((a.groups + 3) / 4)), block(256);
+    // the K rows staged in LDS and stored flat (tuning "wire_rx_lds"): 1 where the staging leaves
+    // at least 3/4 of the waves per CU the registers allow (16 on 16-B lanes, 24 on 8-B lanes;
+    // 160 KiB of LDS per CU), 2 whenever the rows fit 16 KiB (A/B).  RS(10,13), 100k groups:
+    // 1 KiB 520 -> 465 us, 512 B 339 -> 291 us; 1400 B on 8-B lanes (11 waves) 691 -> 769 us
+    const size_t stage = (size_t)K * a.pitch;
+    const int lds = tuning().wire_rx_lds;
+    const size_t lds_waves = stage ? (size_t)(160 * 1024) / stage : 0, reg_waves = nva == 4 ? 16 : 24;
+    if (stage <= 16384 && (lds == 2 || (lds == 1 && 4 * lds_waves >= 3 * reg_waves))) {
+        if (nva == 4)
+            hipLaunchKernelGGL((k_unpack_v2<K, M, 4, true>), dim3((unsigned)a.groups), dim3(64), stage, s, a,
+                               (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+        else
+            hipLaunchKernelGGL((k_unpack_v2<K, M, 2, true>), dim3((unsigned)a.groups), dim3(64), stage, s, a,
+                               (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+        return hipGetLastError();
+    }
     if (nva == 4)
         hipLaunchKernelGGL((k_unpack_v2<K, M, 4>), grid, block, 0, s, a, (const uint8_t*)a.wire,
                            (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);

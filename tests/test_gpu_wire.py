@@ -187,8 +187,8 @@ def test_pack_oversize_group(wire_fused):
 def test_unpack_row_tails(k, n, checksum, pitch):
     """Shard pitches whose last pass leaves a short row tail (1040 = 1024 + 16, 1056, 1088, 528,
     544, 1280; k_unpack_v2 runs it as tail dwords on the last pass): every data packet of a
-    recoverable group comes back exactly, on 16-B and 8-B lanes alike (both give the same
-    shard rows, verdicts and sizes).  Losses up to m + 1 per group, some datagrams corrupted
+    recoverable group comes back exactly, on 16-B lanes with and without the LDS-staged flat row
+    stores (wire_rx_lds) and on 8-B lanes (all give the same shard rows, verdicts and sizes).  Losses up to m + 1 per group, some datagrams corrupted
     inside the row tail, half the rows full to the pitch's limit."""
     rng = np.random.default_rng(pitch * 31 + k)
     G, m = 300, n - k
@@ -214,17 +214,20 @@ def test_unpack_row_tails(k, n, checksum, pitch):
                 w[g, j, wl[g, j] - 1] ^= 0x10  # a byte inside the row tail
     rx_len = np.where(drop, 0, wl).astype(np.int32)
     outs = []
-    for split in (2, 3):  # 16-B lanes, 8-B lanes
+    for split, lds in ((2, 1), (2, 0), (3, 1)):  # 16-B lanes with / without LDS-staged rows, 8-B lanes
         qa.tune("wire_rx_split", split)
+        qa.tune("wire_rx_lds", lds)
         try:
             sh, status, psize, rx = code.unpack_datagrams(dev(w), dev(rx_len), checksum=bool(checksum), shard_pitch=pitch)
             torch.cuda.synchronize()
         finally:
             qa.tune("wire_rx_split", 1)
+            qa.tune("wire_rx_lds", 1)
         outs.append([t.cpu().numpy() for t in (sh, status, psize, rx)])
-    (sh, status, psize, rx), (sh0, status0, psize0, rx0) = outs
-    assert np.array_equal(sh[:, :k], sh0[:, :k])
-    assert np.array_equal(status, status0) and np.array_equal(psize, psize0) and np.array_equal(rx, rx0)
+    sh, status, psize, rx = outs[0]
+    for sh0, status0, psize0, rx0 in outs[1:]:
+        assert np.array_equal(sh[:, :k], sh0[:, :k])
+        assert np.array_equal(status, status0) and np.array_equal(psize, psize0) and np.array_equal(rx, rx0)
     for g in range(G):
         if (rx[g] >= 0).sum() < k:
             continue
