@@ -202,8 +202,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "wire_chunk"       groups per fused send launch pair (0: as many as fit)
  *   "wire_line"        1 the fused send writes whole 64-B lines when the wire pitch is the 64-B
  *                      multiple above 13 + shard pitch (body + k_pack_line0) | 0 body + k_pack_head
- *   "wire_send_wave"   1 at a 1088-B wire pitch, one wave per group writes its rows' first lines
- *                      itself (k_pack_wave64) | 0 body + k_pack_line0
+ *   "wire_send_wave"   1 at a 1088-B (576-B) wire pitch one wave holds one (two) groups and writes
+ *                      their rows' first lines itself (k_pack_wave64) | 0 body + k_pack_line0
  *   "wire_rx_tail"     1 (k_unpack_fused) tail dwords ride on the last 16-B pass | 0 their own pass
  *   "wire_rx_lds"      1 k_unpack_v2 stages the K data rows in LDS and stores them flat where that
  *                      keeps 3/4 of the waves | 2 whenever they fit 16 KiB | 0 row by row

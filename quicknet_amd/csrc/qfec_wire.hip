@@ -709,33 +709,54 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
 // take dword i of line 0 of every row -- header, shard bytes 0-3, payload bytes 0..46 and
 // their check bytes (a dword-wide encode) -- and store each row's line 0 as one instruction.
 // This replaces k_pack_line0's scattered second pass (13 lines 1088 B apart per group).
-template <int K, int M>
+// sum over the lanes of each group of 64 / GPW lanes, in every lane of the group
+template <int GPW>
+__device__ __forceinline__ uint32_t group_total(uint32_t v) {
+    if constexpr (GPW == 1) {
+        return wave_total(v);
+    } else {  // GPW 2: 16-lane rows, then the row pair of each 32-lane half
+        v = row16_sum(v);
+        return v + (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);  // lane ^ 16
+    }
+}
+
+template <int K, int M, int GPW>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
                                                      const int64_t* __restrict__ offsets,
                                                      const int32_t* __restrict__ sizes,
                                                      const uint32_t* __restrict__ seq,
                                                      const uint32_t* __restrict__ tab, uint64_t groups) {
-    constexpr int N = K + M, HDR = 13, HEAD = 4;
+    constexpr int N = K + M, HDR = 13, HEAD = 4, LPG = 64 / GPW;  // lanes per group
     const int lane = threadIdx.x & 63;
-    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));  // wave-uniform
-    if (g >= groups) return;  // whole waves
-    const int t = 4 + lane;
+    const int ln = GPW == 1 ? lane : lane % LPG;  // lane within its group: chunk 4 + ln
+    const uint64_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));  // wave-uniform
+    if (w * GPW >= groups) return;  // whole waves
+    // GPW 1: g is wave-uniform (scalar loads of sizes / offsets); GPW 2: two groups per wave,
+    // a dead second group still joins the cross-lane sums
+    const uint64_t g = GPW == 1 ? w : w * GPW + (uint64_t)(lane / LPG);
+    const bool live = GPW == 1 || g < groups;
+    const int t = 4 + ln;
     const int p = 16 * t - HDR - HEAD;  // payload offset of this chunk's first byte (>= 47)
     int size[K], gmax = 0;
-    const bool ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
-    if (!ok) {
+    bool ok = false;
+    if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
+    if (GPW == 1 && !ok) {
         if (lane < N) a.wire_len[g * N + lane] = -1;
         return;
     }
     int64_t off[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) off[i] = offsets[g * K + i];
+    for (int i = 0; i < K; ++i) off[i] = ok ? offsets[g * K + i] : 0;
     uint8_t* out_g = a.wire + g * (uint64_t)N * a.wire_pitch;
     uint4 x[K];
 #pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = ldu16(payload + off[i] + min(p, size[i]));
+    for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
+    if (ok) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = mask16(x[i], 0, size[i] - p);
+        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + off[i] + min(p, size[i]));
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = mask16(x[i], 0, size[i] - p);
+    }
     uint32_t ps[N];  // per-lane byte sums of each row's chunk (payload / check bytes)
 #pragma unroll
     for (int i = 0; i < K; ++i) ps[i] = sum16(x[i], 0);
@@ -747,36 +768,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
     for (int r = 0; r < N; ++r) {
         const uint4 v = r < K ? x[r] : acc[r - K];
-        stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
+        if (ok) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
         if (r >= K) ps[r] = sum16(v, 0);
     }
     // ---- line 0
-    // line 0's payload dwords (lanes 0..15: datagram bytes 4 lane .. 4 lane + 3; payload byte
-    // 4 lane - 17 at its first byte)
-    const int q = 4 * lane - HDR - HEAD;
+    // line 0's payload dwords (lanes ln 0..15: datagram bytes 4 ln .. 4 ln + 3; payload byte
+    // 4 ln - 17 at its first byte)
+    const int q = 4 * ln - HDR - HEAD;
     uint32_t pay[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         pay[i] = 0;
-        if (lane >= 4 && lane < 16) __builtin_memcpy(&pay[i], payload + off[i] + min(max(q, 0), size[i]), 4);
+        if (ok && ln >= 4 && ln < 16) __builtin_memcpy(&pay[i], payload + off[i] + min(max(q, 0), size[i]), 4);
     }
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         // byte j of the dword holds payload byte q + j (dword 4: loaded from payload byte 0 and
         // shifted up one byte); keep the bytes below the payload's size
-        const uint32_t v = lane == 4 ? pay[i] << 8 : pay[i];
+        const uint32_t v = ln == 4 ? pay[i] << 8 : pay[i];
         const int nb = min(max(size[i] - q, 0), 4);
         pay[i] = nb >= 4 ? v : v & ((1u << (8 * nb)) - 1u);
     }
     uint32_t tot[N];  // payload sums of the data rows, check-byte sums of the check rows
 #pragma unroll
-    for (int i = 0; i < K; ++i) tot[i] = wave_total(ps[i] + __builtin_amdgcn_sad_u8(pay[i], 0u, 0u));
+    for (int i = 0; i < K; ++i) tot[i] = group_total<GPW>(ps[i] + __builtin_amdgcn_sad_u8(pay[i], 0u, 0u));
     // shard view of line 0's dwords: data row i = [size][cksum] at shard bytes 0-3, then payload
     uint32_t sh[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
-        const uint32_t w = ((uint32_t)size[i] & 0xFFFFu) | ((tot[i] & 0xFFFFu) << 16);  // shard bytes 0-3
-        sh[i] = lane == 3 ? w << 8 : lane == 4 ? (w >> 24) | pay[i] : pay[i];
+        const uint32_t wd = ((uint32_t)size[i] & 0xFFFFu) | ((tot[i] & 0xFFFFu) << 16);  // shard bytes 0-3
+        sh[i] = !ok ? 0u : ln == 3 ? wd << 8 : ln == 4 ? (wd >> 24) | pay[i] : pay[i];
     }
     uint32_t par[M];  // check rows' shard view: a dword-wide encode of the data rows'
 #pragma unroll
@@ -791,32 +812,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         }
     }
 #pragma unroll
-    for (int j = 0; j < M; ++j) tot[K + j] = wave_total(ps[K + j] + (lane < 16 ? __builtin_amdgcn_sad_u8(par[j], 0u, 0u) : 0u));
+    for (int j = 0; j < M; ++j)
+        tot[K + j] = group_total<GPW>(ps[K + j] + (ln < 16 ? __builtin_amdgcn_sad_u8(par[j], 0u, 0u) : 0u));
+    if (!ok) {  // (GPW 2) a void or dead group: no datagram bytes, lengths -1
+        if (live && ln < N) a.wire_len[g * N + ln] = -1;
+        return;
+    }
     const uint32_t sent0 = seq[2 * g], src0 = seq[2 * g + 1];
 #pragma unroll
     for (int r = 0; r < N; ++r) {
         uint32_t dsum;
         const uint32_t v = r < K ? sh[r] : par[r - K];
         if (r < K) {
-            const uint32_t w = ((uint32_t)size[r] & 0xFFFFu) | ((tot[r] & 0xFFFFu) << 16);
-            dsum = tot[r] + (w & 0xFF) + ((w >> 8) & 0xFF) + ((w >> 16) & 0xFF) + (w >> 24);
+            const uint32_t wd = ((uint32_t)size[r] & 0xFFFFu) | ((tot[r] & 0xFFFFu) << 16);
+            dsum = tot[r] + (wd & 0xFF) + ((wd >> 8) & 0xFF) + ((wd >> 16) & 0xFF) + (wd >> 24);
         } else {
             dsum = tot[r];  // check shard bytes 0-3 are in par's dwords 3-4, summed above
         }
         const uint32_t sent = sent0 + (uint32_t)r, src = src0 + (uint32_t)(r < K ? r : K - 1);
         const uint32_t ikn = ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu;
         uint32_t d = v;
-        if (lane == 0) d = 0xEDu | (sent << 8);
-        else if (lane == 1) d = (sent >> 24) | (src << 8);
-        else if (lane == 2) d = (src >> 24) | (ikn << 8) | ((dsum & 0xFFu) << 24);
-        else if (lane == 3) d = ((dsum >> 8) & 0xFFu) | v;
-        if (lane < 16) {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(out_g + (uint64_t)r * a.wire_pitch + 4 * lane);
+        if (ln == 0) d = 0xEDu | (sent << 8);
+        else if (ln == 1) d = (sent >> 24) | (src << 8);
+        else if (ln == 2) d = (src >> 24) | (ikn << 8) | ((dsum & 0xFFu) << 24);
+        else if (ln == 3) d = ((dsum >> 8) & 0xFFu) | v;
+        if (ln < 16) {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(out_g + (uint64_t)r * a.wire_pitch + 4 * ln);
             if (a.store_nt & 2) __builtin_nontemporal_store(d, dst);
             else *dst = d;
         }
     }
-    if (lane < N) a.wire_len[g * N + lane] = HDR + (lane < K ? size[lane] + HEAD : gmax);
+    if (ln < N) a.wire_len[g * N + ln] = HDR + (ln < K ? size[ln] + HEAD : gmax);
 }
 
 // A lane's slice of a shard row in one pass: NV16 = 4 -> one 16-B chunk at pos16, then NVT
@@ -1737,15 +1763,22 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
     // memory a read-modify-write: tools/wrskel.hip, profiles/r02zn_wrskel.txt)
     const bool line = tuning().wire_line && a.wire_pitch % 64 == 0 &&
                       a.wire_pitch == (HDR + a.pitch + 63) / 64 * 64 && a.wire_pitch / 16 >= (HDR == 13 ? 20u : 16u);
-    // one wave per group when the body's chunks 4..67 are exactly one wave (k_pack_wave64)
-    if (HDR == 13 && line && a.wire_pitch == 1088 && tuning().wire_send_wave) {
+    // groups that fill a wave exactly (k_pack_wave64): the body's chunks 4.. are 64 lanes at a
+    // 1088-B wire pitch (one group per wave) and 32 at 576 B (two)
+    const int gpw = a.wire_pitch == 1088 ? 1 : a.wire_pitch == 576 ? 2 : 0;
+    if (HDR == 13 && line && gpw && tuning().wire_send_wave) {
         for (uint64_t g0 = 0; g0 < a.groups; g0 += ((uint64_t)1 << 28)) {
             const uint64_t gn = std::min((uint64_t)1 << 28, a.groups - g0);
             WireArgs b = a;
             b.wire = a.wire + g0 * (uint64_t)(K + M) * a.wire_pitch;
             b.wire_len = a.wire_len + g0 * (K + M);
-            hipLaunchKernelGGL((k_pack_wave64<K, M>), dim3((unsigned)((gn + 3) / 4)), dim3(256), 0, s, b, a.payload,
-                               a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn);
+            const dim3 grid((unsigned)((gn + 4 * gpw - 1) / (4 * gpw)));
+            if (gpw == 1)
+                hipLaunchKernelGGL((k_pack_wave64<K, M, 1>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
+                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn);
+            else
+                hipLaunchKernelGGL((k_pack_wave64<K, M, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
+                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn);
         }
         return hipGetLastError();
     }

@@ -241,18 +241,21 @@ def test_unpack_row_tails(k, n, checksum, pitch):
     assert ok_rows > G * k // 2
 
 
-@pytest.mark.parametrize("k,n,G", [(10, 13, 500), (4, 6, 500), (8, 12, 500), (5, 8, 500), (10, 13, 13)])
-def test_pack_wave64_matches_line0(oracle, k, n, G):
-    """1 KiB-class payloads with a 1088-B wire pitch: the one-wave-per-group send
-    (k_pack_wave64, wire_send_wave 1) writes the same datagrams and lengths as the body +
-    k_pack_line0 pair (0), and both equal the oracle's on sampled groups.  Sizes 0..1036
-    (half exactly 1024), one oversize group."""
-    rng = np.random.default_rng(n * 7 + k + G)
-    m = n - k  # G = 13: the last block holds one live wave of four
-    sizes = rng.integers(0, 1037, size=G * k).astype(np.int32)
-    sizes[rng.random(G * k) < 0.5] = 1024
+@pytest.mark.parametrize("k,n,G,sp,wp", [(10, 13, 500, 1040, 1088), (4, 6, 500, 1040, 1088), (8, 12, 500, 1040, 1088),
+                                         (5, 8, 500, 1040, 1088), (10, 13, 13, 1040, 1088), (10, 13, 500, 528, 576),
+                                         (4, 6, 501, 528, 576), (10, 13, 13, 528, 576)])
+def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp):
+    """Payloads with a 1088-B (1 KiB class, one group per wave) or 576-B (512-B class, two
+    groups per wave) wire pitch: the send that finishes line 0 inside the wave (k_pack_wave64,
+    wire_send_wave 1) writes the same datagrams and lengths as the body + k_pack_line0 pair
+    (0), and both equal the oracle's on sampled groups.  Sizes 0 .. sp - 4 (half exactly
+    sp - 16), one oversize group, G = 13 / 501 leave the last block partly (or a wave half) dead."""
+    rng = np.random.default_rng(n * 7 + k + G + sp)
+    m = n - k
+    sizes = rng.integers(0, sp - 3, size=G * k).astype(np.int32)
+    sizes[rng.random(G * k) < 0.5] = sp - 16
     sizes[:3] = [0, 1, 46]  # payloads ending inside line 0
-    sizes[7 * k + 1] = 1040  # 1040 + 4 > the 1040-B shard pitch: group 7 is void
+    sizes[7 * k + 1] = sp  # sp + 4 > the shard pitch: group 7 is void
     payload = rng.integers(0, 256, size=int(np.maximum(sizes, 0).sum()) + 1, dtype=np.uint8)
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     seq = np.stack([np.arange(G, dtype=np.uint32) * n + 5, np.arange(G, dtype=np.uint32) * k + 2], 1)
@@ -263,7 +266,7 @@ def test_pack_wave64_matches_line0(oracle, k, n, G):
         qa.tune("wire_send_wave", wave)
         try:
             _, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq), True,
-                                                shard_pitch=1040, wire_pitch=1088)
+                                                shard_pitch=sp, wire_pitch=wp)
             torch.cuda.synchronize()
         finally:
             qa.tune("wire_send_wave", 1)
@@ -281,7 +284,7 @@ def test_pack_wave64_matches_line0(oracle, k, n, G):
         if g == 7:
             continue
         out, ln, _ = oracle.pack_group(k, n, full, payload, offs[g * k:(g + 1) * k], sizes[g * k:(g + 1) * k],
-                                       int(seq[g, 0]), int(seq[g, 1]), 1, pitch=1088)
+                                       int(seq[g, 0]), int(seq[g, 1]), 1, pitch=wp)
         assert np.array_equal(ln, l1[g])
         for j in range(n):
             assert np.array_equal(out[j, :ln[j]], w1[g, j, :ln[j]]), (g, j)
