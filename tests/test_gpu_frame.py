@@ -21,8 +21,10 @@ def dev(a):
 
 
 @pytest.mark.parametrize("session", [False, True])
-@pytest.mark.parametrize("pitch", [64, 1056, 2080])
-def test_frame_vs_oracle(oracle, session, pitch):
+@pytest.mark.parametrize("pitch", [64, 1056, 1088, 2080])
+@pytest.mark.parametrize("op64", [False, True])
+def test_frame_vs_oracle(oracle, session, pitch, op64):
+    """With the default 16-B output pitch and a 64-B multiple one."""
     rng = np.random.default_rng(pitch + session)
     R = 300
     lens = rng.integers(0, pitch + 1, size=R).astype(np.int32)
@@ -31,8 +33,10 @@ def test_frame_vs_oracle(oracle, session, pitch):
     masks = rng.integers(0, 256, size=R, dtype=np.uint8)
     ch = rng.integers(0, 2**32, size=(R, 2), dtype=np.uint64).astype(np.uint32) if session else None
     gmask = 0x3C
+    P = 12 if session else 4
     out, out_len = qa.frame_udp(dev(rows), dev(lens), dev(masks), gmask=gmask,
-                                conv_hid=dev(ch.view(np.int32)) if session else None)
+                                conv_hid=dev(ch.view(np.int32)) if session else None,
+                                out_pitch=(pitch + P + 63) // 64 * 64 if op64 else None)
     torch.cuda.synchronize()
     out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
     P = 12 if session else 4
