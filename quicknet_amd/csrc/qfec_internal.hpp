@@ -137,6 +137,7 @@ struct Tuning {
     int recon_compact = 1;
     int host_zero_copy = 1; // pinned host batches: kernels read/write them directly (0: staged copies)  // LUT reconstruct reads coefficient tables via the record's offsets + t256
     int wire_rx_lds = 1;    // fused receive: K rows staged in LDS, stored flat (one wave per block)
+    int frame_rows = 2;     // ProtocolUdp framing: rows per wave, loads issued first (2 or 4; 1: one row per wave)
     int wire_rx_split = 1;  // fused receive: k_unpack_v2 (1 auto lanes, 2 16-B, 3 8-B); 0 k_unpack_fused
 };
 Tuning& tuning();

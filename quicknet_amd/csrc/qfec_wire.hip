@@ -1677,6 +1677,88 @@ __global__ void __launch_bounds__(256) k_frame_udp(FrameArgs a) {
     }
 }
 
+// k_frame_udp over ROWS rows per wave with every load issued before any use (tuning
+// "frame_rows"): one row per wave keeps ~1 KB in flight per wave, too little to cover the
+// memory latency at this kernel's occupancy; ROWS rows put ROWS times as many bytes in flight.
+// Rows of at most 2 048 B (one pass of two 16-B chunks per lane); the host checks.
+template <int ROWS>
+__global__ void __launch_bounds__(256) k_frame_udp_rows(FrameArgs a) {
+    const uint64_t row0 = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * ROWS;
+    if (row0 >= a.rows) return;
+    const int lane = threadIdx.x & 63;
+    const int P = a.session ? 12 : 4;
+    const int in_chunks = (int)(a.in_pitch / 16);
+    int len[ROWS], total[ROWS];
+    bool good[ROWS];
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) {
+        len[i] = row0 + i < a.rows ? a.in_len[row0 + i] : -1;
+        total[i] = P + len[i];
+        good[i] = row0 + i < a.rows && len[i] >= 0 && total[i] <= (int)a.out_pitch && len[i] <= (int)a.in_pitch;
+    }
+    uint4 lo[ROWS][2], hi[ROWS][2];
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) {
+        const uint8_t* in = a.in + (row0 + i) * a.in_pitch;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = 2 * lane + h;
+            lo[i][h] = hi[i][h] = make_uint4(0, 0, 0, 0);
+            if (good[i] && 16 * q < total[i]) {
+                if (q >= 1) lo[i][h] = *reinterpret_cast<const uint4*>(in + 16 * (q - 1));
+                if (q < in_chunks) hi[i][h] = *reinterpret_cast<const uint4*>(in + 16 * q);
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) {
+        const uint64_t row = row0 + i;
+        if (row >= a.rows) break;
+        if (!good[i]) {
+            if (lane == 0) a.out_len[row] = -1;
+            continue;
+        }
+        uint8_t* out = a.out + row * a.out_pitch;
+        const uint32_t m = a.mask[row];
+        const uint32_t x = (m ^ a.gmask ^ 0x5Au) & 0xFFu;
+        const uint32_t mm = x * 0x01010101u;
+        uint32_t sum = 0;
+        uint4 first = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = 2 * lane + h;
+            if (16 * q >= total[i]) continue;
+            // frame bytes [16q, 16q + 16) = data bytes [16q - P, 16q + 16 - P)
+            uint4 v = mask16(window(lo[i][h], hi[i][h], 16 - P), q == 0 ? P : 0, total[i] - 16 * q);
+            sum = sum16(v, sum);
+            if (q == 0) first = v;
+            else st16a(out + 16 * q, xor16(v, mm));
+        }
+        sum = wave_sum(sum);
+        if (lane == 0) {
+            const uint32_t cmd = (a.cmd & 0x1Fu) | 0xA0u, proto = a.protocol & 0xFFu;
+            put_byte(first, 2, cmd);
+            put_byte(first, 3, proto);
+            uint32_t s2 = sum + cmd + proto;
+            if (a.session) {
+                const uint32_t conv = a.conv_hid[2 * row], hid = a.conv_hid[2 * row + 1];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    put_byte(first, 4 + b, conv >> (8 * b));
+                    put_byte(first, 8 + b, hid >> (8 * b));
+                    s2 += ((conv >> (8 * b)) & 0xFFu) + ((hid >> (8 * b)) & 0xFFu);
+                }
+            }
+            const uint32_t c = ~((s2 >> 16) + (s2 & 0xFFFFu)) & 0xFFu;
+            put_byte(first, 1, c);
+            first = xor16(first, mm);
+            put_byte(first, 0, m);
+            st16a(out, first);
+            a.out_len[row] = total[i];
+        }
+    }
+}
+
 // Reverse (ProtocolUdp::RecvPacket, ProtocolBasic.cpp:152-210): status 0 ok, 1 shorter than 4
 // bytes (or than the 12 with the Session prefix), 2 checksum, 3 cmd (& 0xe0 != 0xA0), 4 does
 // not fit the output pitch.  The data (frame bytes [P, len), un-XORed) is written for every
@@ -1739,6 +1821,89 @@ __global__ void __launch_bounds__(256) k_unframe_udp(FrameArgs a) {
             }
             a.conv_hid[2 * row] = conv;
             a.conv_hid[2 * row + 1] = hid;
+        }
+    }
+}
+
+// k_unframe_udp over ROWS rows per wave, every load issued before any use (tuning "frame_rows",
+// as k_frame_udp_rows); rows of at most 2 048 B
+template <int ROWS>
+__global__ void __launch_bounds__(256) k_unframe_udp_rows(FrameArgs a) {
+    const uint64_t row0 = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * ROWS;
+    if (row0 >= a.rows) return;
+    const int lane = threadIdx.x & 63;
+    const int P = a.session ? 12 : 4;
+    const int in_chunks = (int)(a.in_pitch / 16);
+    int len[ROWS];
+    bool good[ROWS];
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) {
+        len[i] = row0 + i < a.rows ? a.in_len[row0 + i] : 0;
+        good[i] = row0 + i < a.rows && len[i] >= P && len[i] <= (int)a.in_pitch && len[i] - P <= (int)a.out_pitch;
+    }
+    uint4 f[ROWS][2], nx[ROWS][2], h0[ROWS];
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) {
+        const uint8_t* in = a.in + (row0 + i) * a.in_pitch;
+        h0[i] = good[i] ? *reinterpret_cast<const uint4*>(in) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = 2 * lane + h;
+            f[i][h] = nx[i][h] = make_uint4(0, 0, 0, 0);
+            if (good[i] && 16 * q < len[i]) {
+                f[i][h] = *reinterpret_cast<const uint4*>(in + 16 * q);
+                if (16 * q < len[i] - P && q + 1 < in_chunks) nx[i][h] = *reinterpret_cast<const uint4*>(in + 16 * (q + 1));
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < ROWS; ++i) {
+        const uint64_t row = row0 + i;
+        if (row >= a.rows) break;
+        if (!good[i]) {
+            if (lane == 0) {
+                a.status[row] = len[i] < P ? 1 : 4;
+                a.out_len[row] = -1;
+            }
+            continue;
+        }
+        uint8_t* out = a.out + row * a.out_pitch;
+        const uint32_t x = (get_byte(h0[i], 0) ^ a.gmask ^ 0x5Au) & 0xFFu;
+        const uint32_t mm = x * 0x01010101u;
+        const int dlen = len[i] - P;
+        uint32_t sum = 0;  // frame bytes [2, len), un-XORed
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = 2 * lane + h;
+            if (16 * q >= len[i]) continue;
+            const uint4 fv = xor16(f[i][h], mm);
+            sum = sum16(mask16(fv, 2 - 16 * q, len[i] - 16 * q), sum);
+            // data chunk q = frame bytes [16q + P, 16q + P + 16)
+            if (16 * q < dlen) st16a(out + 16 * q, mask16(window(fv, xor16(nx[i][h], mm), P), 0, dlen - 16 * q));
+        }
+        sum = wave_sum(sum);
+        if (lane == 0) {
+            const uint4 f0 = xor16(h0[i], mm);
+            const uint32_t check = get_byte(f0, 1), cmd = get_byte(f0, 2);
+            const uint32_t c = ~((sum >> 16) + (sum & 0xFFFFu)) & 0xFFu;
+            a.status[row] = c != check ? 2 : (cmd & 0xE0u) != 0xA0u ? 3 : 0;
+            a.out_len[row] = dlen;
+            if (a.info) {
+                a.info[4 * row + 0] = (uint8_t)x;
+                a.info[4 * row + 1] = (uint8_t)check;
+                a.info[4 * row + 2] = (uint8_t)(cmd & 0x1Fu);
+                a.info[4 * row + 3] = (uint8_t)get_byte(f0, 3);
+            }
+            if (a.session && a.conv_hid) {
+                uint32_t conv = 0, hid = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    conv |= get_byte(f0, 4 + b) << (8 * b);
+                    hid |= get_byte(f0, 8 + b) << (8 * b);
+                }
+                a.conv_hid[2 * row] = conv;
+                a.conv_hid[2 * row + 1] = hid;
+            }
         }
     }
 }
@@ -1908,12 +2073,28 @@ hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint
 
 hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s) {
     if (!a.rows) return hipSuccess;
+    const int fr = tuning().frame_rows;
+    if (fr > 1 && a.in_pitch <= 2048 && a.out_pitch <= 2048) {
+        if (fr == 2)
+            hipLaunchKernelGGL(k_frame_udp_rows<2>, dim3(waves_grid((a.rows + 1) / 2)), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_frame_udp_rows<4>, dim3(waves_grid((a.rows + 3) / 4)), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_frame_udp, dim3(waves_grid(a.rows)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_unframe_udp(const FrameArgs& a, hipStream_t s) {
     if (!a.rows) return hipSuccess;
+    const int fr = tuning().frame_rows;
+    if (fr > 1 && a.in_pitch <= 2048 && a.out_pitch <= 2048) {
+        if (fr == 2)
+            hipLaunchKernelGGL(k_unframe_udp_rows<2>, dim3(waves_grid((a.rows + 1) / 2)), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_unframe_udp_rows<4>, dim3(waves_grid((a.rows + 3) / 4)), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_unframe_udp, dim3(waves_grid(a.rows)), dim3(256), 0, s, a);
     return hipGetLastError();
 }

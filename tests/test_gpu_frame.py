@@ -23,10 +23,13 @@ def dev(a):
 @pytest.mark.parametrize("session", [False, True])
 @pytest.mark.parametrize("pitch", [64, 1056, 1088, 2080])
 @pytest.mark.parametrize("op64", [False, True])
-def test_frame_vs_oracle(oracle, session, pitch, op64):
-    """With the default 16-B output pitch and a 64-B multiple one."""
+@pytest.mark.parametrize("rows_per_wave", [1, 2, 4])
+def test_frame_vs_oracle(oracle, session, pitch, op64, rows_per_wave):
+    """With the default 16-B output pitch and a 64-B multiple one; one, two or four rows per
+    wave (frame_rows, default 2; rows longer than 2 KiB always take one row per wave).  301 rows: the
+    last wave is partly empty."""
     rng = np.random.default_rng(pitch + session)
-    R = 300
+    R = 301
     lens = rng.integers(0, pitch + 1, size=R).astype(np.int32)
     lens[:4] = [0, 1, 15, pitch]
     rows = rng.integers(0, 256, size=(R, pitch), dtype=np.uint8)
@@ -34,10 +37,14 @@ def test_frame_vs_oracle(oracle, session, pitch, op64):
     ch = rng.integers(0, 2**32, size=(R, 2), dtype=np.uint64).astype(np.uint32) if session else None
     gmask = 0x3C
     P = 12 if session else 4
-    out, out_len = qa.frame_udp(dev(rows), dev(lens), dev(masks), gmask=gmask,
-                                conv_hid=dev(ch.view(np.int32)) if session else None,
-                                out_pitch=(pitch + P + 63) // 64 * 64 if op64 else None)
-    torch.cuda.synchronize()
+    qa.tune("frame_rows", rows_per_wave)
+    try:
+        out, out_len = qa.frame_udp(dev(rows), dev(lens), dev(masks), gmask=gmask,
+                                    conv_hid=dev(ch.view(np.int32)) if session else None,
+                                    out_pitch=(pitch + P + 63) // 64 * 64 if op64 else None)
+        torch.cuda.synchronize()
+    finally:
+        qa.tune("frame_rows", 2)
     out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
     P = 12 if session else 4
     for r in range(R):
@@ -49,10 +56,18 @@ def test_frame_vs_oracle(oracle, session, pitch, op64):
         assert np.array_equal(out[r, :len(ref)], ref), r
 
 
+@pytest.fixture(params=[2, 1, 4], ids=["rows2", "rows1", "rows4"])
+def frame_rows(request):
+    """Rows per wave of the framing kernels (frame_rows; 2 is the default)."""
+    qa.tune("frame_rows", request.param)
+    yield request.param
+    qa.tune("frame_rows", 2)
+
+
 @pytest.mark.parametrize("session", [False, True])
-def test_unframe_roundtrip_and_errors(oracle, session):
+def test_unframe_roundtrip_and_errors(oracle, session, frame_rows):
     rng = np.random.default_rng(7 + session)
-    R, pitch = 400, 1072
+    R, pitch = 403, 1072  # odd: the last wave of two or four rows is partly empty
     P = 12 if session else 4
     lens = rng.integers(0, pitch - P + 1, size=R).astype(np.int32)
     rows = rng.integers(0, 256, size=(R, pitch), dtype=np.uint8)
