@@ -205,7 +205,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "wire_send_wave"   1 at a 1088-B (576-B) wire pitch one wave holds one (two) groups and writes
  *                      their rows' first lines itself (k_pack_wave64) | 0 body + k_pack_line0
  *   "wire_rx_tail"     1 (k_unpack_fused) tail dwords ride on the last 16-B pass | 0 their own pass
- *   "frame_rows"       2 framing kernels run two rows per wave, loads first (rows <= 2 KiB) | 1 | 4
+ *   "frame_rows"       2 framing kernels run two rows per wave, loads first, frames built in LDS and
+ *                      stored flat (rows <= 2 KiB) | 3 the same, stored directly | 1 | 4
  *   "wire_rx_lds"      1 k_unpack_v2 stages the K data rows in LDS and stores them flat where that
  *                      keeps 3/4 of the waves | 2 whenever they fit 16 KiB | 0 row by row
  *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged

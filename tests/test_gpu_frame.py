@@ -23,10 +23,11 @@ def dev(a):
 @pytest.mark.parametrize("session", [False, True])
 @pytest.mark.parametrize("pitch", [64, 1056, 1088, 2080])
 @pytest.mark.parametrize("op64", [False, True])
-@pytest.mark.parametrize("rows_per_wave", [1, 2, 4])
+@pytest.mark.parametrize("rows_per_wave", [1, 2, 3, 4])
 def test_frame_vs_oracle(oracle, session, pitch, op64, rows_per_wave):
-    """With the default 16-B output pitch and a 64-B multiple one; one, two or four rows per
-    wave (frame_rows, default 2; rows longer than 2 KiB always take one row per wave).  301 rows: the
+    """With the default 16-B output pitch and a 64-B multiple one; one, two (staged in LDS:
+    frame_rows 2, the default; stored directly: 3) or four rows per wave (rows longer than
+    2 KiB always take one row per wave).  301 rows: the
     last wave is partly empty."""
     rng = np.random.default_rng(pitch + session)
     R = 301
