@@ -34,12 +34,27 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-import quicknet_amd as qa  # noqa: E402  (libqfec.so is loaded lazily, at the first codec call)
+from quicknet_amd import topology  # noqa: E402  (sysfs only: no torch, no HIP)
 from quicknet_amd.sharding import rank_seed, shard_range  # noqa: E402
-from quicknet_amd.synth import SEED_DECODE, SEED_ENCODE, SEED_RS16, erasure_marks, marks_to_rs_layout  # noqa: E402
+
+# numpy / torch / the codec are imported by _load(), after the launcher decision: the parent of
+# `bench.py --gpus N` starts its ranks without ever importing torch
+np = torch = qa = None
+SEED_DECODE = SEED_ENCODE = SEED_RS16 = erasure_marks = marks_to_rs_layout = None
+
+
+def _load():
+    global np, torch, qa, SEED_DECODE, SEED_ENCODE, SEED_RS16, erasure_marks, marks_to_rs_layout
+    if torch is not None:
+        return
+    import numpy
+    import torch as _torch
+
+    import quicknet_amd  # libqfec.so is loaded lazily, at the first codec call
+    from quicknet_amd import synth
+    np, torch, qa = numpy, _torch, quicknet_amd
+    SEED_DECODE, SEED_ENCODE, SEED_RS16 = synth.SEED_DECODE, synth.SEED_ENCODE, synth.SEED_RS16
+    erasure_marks, marks_to_rs_layout = synth.erasure_marks, synth.marks_to_rs_layout
 
 METRIC = "RS(k,m) FEC encode+decode GiB/s (device-resident) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -65,14 +80,26 @@ def parse(argv=None):
     p.add_argument("--variant", type=int, default=0, help="0 perm tables (default), 1 LDS log/exp")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (rank 0, N=1)")
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=16,
-                   help="threads for the all-cores CPU baseline (the GPU box's CPU share is 16; 0 skips it)")
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="threads for the all-cores CPU baseline (default: the CPUs this process may use -- "
+                        "affinity mask and cgroup quota, quicknet_amd.topology.cpu_share; 0 skips it)")
     p.add_argument("--no-side", action="store_true", help="skip the rank-0 side configurations")
     p.add_argument("--no-config4", action="store_true", help="skip the sharded RS(16,4) config 4 leg")
     p.add_argument("--config4-groups", type=int, default=250_000, help="config 4 job size (tests shrink it)")
     p.add_argument("--no-host", action="store_true", help="skip the host-to-host legs (config 5)")
     p.add_argument("--protocol-check", action="store_true",
                    help="no GPU work: run the rank launch + barrier/max/sum protocol only (CPU tests)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="launcher only: print the pre-spawn state (device count, NUMA plan, open GPU fds) and exit")
+    p.add_argument("--deadline-s", type=float, default=1500.0,
+                   help="launcher: ranks still running after this many seconds are killed (exit 124)")
+    p.add_argument("--fail-grace-s", type=float, default=15.0,
+                   help="launcher: after one rank fails, the others are ended this many seconds later")
+    p.add_argument("--fail-rank", type=int, default=-1, help="--protocol-check only: this rank exits 3 (tests)")
+    p.add_argument("--hang-rank", type=int, default=-1, help="--protocol-check only: this rank hangs (tests)")
+    p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
+    p.add_argument("--force-dist", action="store_true",
+                   help="init the process group even at one rank (exercises the RCCL path on a one-GPU box)")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py), if present")
     return p.parse_args(argv)
@@ -87,44 +114,93 @@ def _free_port():
     return port
 
 
+def _kill_group(p, sig):
+    try:
+        os.killpg(p.pid, sig)
+    except (ProcessLookupError, PermissionError):
+        pass
+
+
 def launch_ranks(args, argv):
-    """--gpus N > 1 with no WORLD_SIZE in the environment: start N fresh rank processes (this
-    process never touches the GPU: torch.cuda.device_count() does not initialise it on this
-    image) and return the worst of their exit codes.  A rank that fails ends the others."""
+    """--gpus N > 1 with no WORLD_SIZE in the environment: start N fresh rank processes and
+    return the worst of their exit codes.
+
+    This process never imports torch and makes no HIP call: it counts devices from the KFD
+    topology in sysfs (quicknet_amd.topology), and when sysfs does not say, each rank checks
+    its own index (dist_setup).  Every rank runs in its own session, so ending it ends the
+    processes it started too.  A rank that fails ends the others after --fail-grace-s (they
+    would wait on a barrier forever); ranks still running at --deadline-s are killed and the
+    launcher exits 124."""
+    import signal
     n = args.gpus
     backend = os.environ.get("QFEC_BENCH_BACKEND", "nccl")
+    count, source = (None, "not checked")
     if not args.protocol_check and backend == "nccl":
-        have = torch.cuda.device_count()
-        if have < n:
-            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+        count, source = topology.gpu_count()
+        if count is not None and count < n:
+            print(f"bench.py: --gpus {n} but only {count} GPU(s) visible ({source})", file=sys.stderr)
             return 2
+    if args.launch_check:  # the pre-spawn state, for tests: no torch, no GPU file open
+        print(json.dumps({"launch_check": True, "gpus_arg": n, "gpu_count": count, "gpu_count_source": source,
+                          "torch_imported": "torch" in sys.modules, "gpu_fds": topology.open_gpu_fds(),
+                          "plan": [topology.gpu_numa(r) and {kk: (len(v) if kk == "cpus" else v)
+                                                              for kk, v in topology.gpu_numa(r).items()}
+                                   for r in range(n)]}), flush=True)
+        return 0
     port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      start_new_session=True))
     rcs = [None] * n
-    failed_at = None
-    while any(rc is None for rc in rcs):
-        for i, p in enumerate(procs):
-            if rcs[i] is None:
-                rcs[i] = p.poll()
-                if rcs[i] not in (None, 0) and failed_at is None:
-                    failed_at = time.time()
-        if failed_at is not None and time.time() - failed_at > 30:
-            for i, p in enumerate(procs):  # the survivors would wait on a barrier forever
+    t_start = time.time()
+    failed_at = first_bad = None
+    timed_out = False
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
                 if rcs[i] is None:
-                    p.kill()
-                    rcs[i] = p.wait()
-        time.sleep(0.05)
-    bad = [rc for rc in rcs if rc != 0]
-    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+                    rcs[i] = p.poll()
+                    if rcs[i] not in (None, 0) and failed_at is None:
+                        failed_at, first_bad = time.time(), rcs[i]
+                        print(f"bench.py: rank {i} exited {rcs[i]}; ending the others in {args.fail_grace_s:g} s",
+                              file=sys.stderr)
+            now = time.time()
+            over = now - t_start > args.deadline_s
+            if over and not timed_out and any(rc is None for rc in rcs):
+                timed_out = True
+                print(f"bench.py: launch deadline {args.deadline_s:g} s passed; killing the ranks still running",
+                      file=sys.stderr)
+            if over or (failed_at is not None and now - failed_at > args.fail_grace_s):
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        _kill_group(p, signal.SIGTERM)
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        try:
+                            rcs[i] = p.wait(timeout=10)
+                        except subprocess.TimeoutExpired:
+                            _kill_group(p, signal.SIGKILL)
+                            rcs[i] = p.wait()
+            time.sleep(0.05)
+    finally:
+        for p in procs:  # never leave a rank behind (e.g. the launcher itself interrupted)
+            if p.poll() is None:
+                _kill_group(p, signal.SIGKILL)
+                p.wait()
+    if timed_out:
+        return 124
+    if failed_at is None:
+        return 0
+    return first_bad if first_bad > 0 else 1  # the rank that failed first, not the ones ended after it
 
 
 def dist_setup(args):
     """One rank per GPU over RCCL.  QFEC_BENCH_BACKEND=gloo (rehearsal only) runs the same
-    rank protocol over gloo, with ranks sharing the visible GPUs round-robin."""
+    rank protocol over gloo, with ranks sharing the visible GPUs round-robin.  Before anything
+    imports torch, the rank binds itself to its GPU's NUMA node (quicknet_amd.topology)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -133,21 +209,44 @@ def dist_setup(args):
     backend = os.environ.get("QFEC_BENCH_BACKEND", "nccl")
     if args.protocol_check:
         backend = "gloo"
-    elif backend != "nccl":
-        local %= max(1, torch.cuda.device_count())
+    numa = None
     if not args.protocol_check:
+        dev_index = local
+        if backend != "nccl":
+            cnt, _ = topology.gpu_count()
+            dev_index = local % cnt if cnt else 0
+        numa = topology.bind_rank(dev_index) if not args.no_numa_bind else {"bound": False, "reason": "--no-numa-bind"}
+    if args.protocol_check and args.fail_rank == rank:
+        raise SystemExit(3)  # injected failure (tests/test_launch.py)
+    if args.protocol_check and args.hang_rank == rank:
+        time.sleep(3600)
+    _load()
+    if not args.protocol_check:
+        have = torch.cuda.device_count()
+        if backend != "nccl":
+            local %= max(1, have)
+        if local >= have:  # this rank's own check (the launcher may not have been able to count)
+            print(f"bench.py: rank {rank} wants device {local} but {have} GPU(s) are visible", file=sys.stderr)
+            raise SystemExit(2)
         torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    return rank, world, local
+    return rank, world, local, numa
+
+
+def _dist_on():
+    if torch is None:
+        return False
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
 
 
 def barrier(world):
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.barrier()
 
@@ -155,7 +254,8 @@ def barrier(world):
 def _all_reduce(x, world, op):
     """One float over all ranks.  The tensor lives where the backend wants it: on the GPU for
     RCCL, on the host for gloo (tests/test_multiproc.py drives these helpers over gloo)."""
-    if world == 1:
+    _load()
+    if not _dist_on():
         return x
     import torch.distributed as dist
     dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
@@ -176,7 +276,8 @@ def all_sum(x, world):
 
 def all_gather_float(x, world, rank):
     """Every rank's value of x, in rank order (a one-hot sum: one all-reduce of `world` floats)."""
-    if world == 1:
+    _load()
+    if not _dist_on():
         return [x]
     import torch.distributed as dist
     dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
@@ -315,6 +416,41 @@ def cpu_baseline_threads(args, budget_s, threads):
     return {"value": round(gib / el, 4), "unit": "GiB/s", "cores": len(slices), "kind": "reference",
             "sample": f"{sum(done)} slice passes over {sample} groups split {len(slices)} ways (encode + reconstruct with "
                       f"{args.erasures} random erasures/group), RS({k},{m}) B={B}, {el:.1f} s, {len(slices)} threads"}
+
+
+def cpu_check_host_sample(samples):
+    """The cpu_baseline leg's checker for config 5 (host_to_host_mixed): sampled groups of every
+    pipe batch run through the reference's own module/rs.c (oracle/_ref) -- encode must give the
+    parity the pipe wrote, and reconstruct of the same damaged groups must give the rows the pipe
+    restored.  Without oracle/_ref, the C restatement (oracle/liboracle.so) is the checker."""
+    from oracle.oracle import Oracle, RefCodec
+    use_ref = RefCodec.available()
+    ref = RefCodec() if use_ref else None
+    orc = None if use_ref else Oracle()
+    groups = bad = 0
+    for s in samples:
+        k, m, B = s["k"], s["m"], s["B"]
+        G = len(s["idx"])
+        data = np.ascontiguousarray(s["data"])
+        par = np.zeros((G, m, B), np.uint8)
+        dmg = data.copy()
+        dmg[s["marks_data"].astype(bool)] = 0x5A
+        marks = np.concatenate([s["marks_data"].reshape(-1), s["marks_parity"].reshape(-1)]).astype(np.uint8)
+        if use_ref:
+            h = ref.rs.reed_solomon_new(k, m)
+            ref.rs_encode(h, ref.shard_ptrs(data, par), G * (k + m), B)
+            rpar = par.copy()
+            ref.rs_reconstruct(h, ref.shard_ptrs(dmg, rpar), marks, G * (k + m), B)
+            ref.rs.reed_solomon_release(h)
+        else:
+            rows = orc.cauchy(k, m)
+            orc.rs_encode(rows, data, par, B)
+            orc.rs_reconstruct(rows, dmg, par.copy(), marks, B)
+        good = (par == s["parity"]).all(axis=(1, 2)) & (dmg == s["restored"]).all(axis=(1, 2))
+        groups += G
+        bad += int((~good).sum())
+    return {"match": bad == 0, "groups_checked": groups, "mismatched_groups": bad,
+            "checker": "reference module/rs.c (oracle/_ref)" if use_ref else "oracle/liboracle.so (C restatement)"}
 
 
 def cpu_config0(budget_s):
@@ -663,12 +799,12 @@ def kernel_sources_hash():
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.launch_check) and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args, argv)
-    rank, world, local = dist_setup(args)
+    rank, world, local, numa = dist_setup(args)
     if args.protocol_check:
         rc = protocol_check(args, rank, world)
-        if world > 1:
+        if _dist_on():
             import torch.distributed as dist
             dist.destroy_process_group()
         return rc
@@ -794,10 +930,12 @@ def main(argv=None):
 
     # BASELINE configs[4] (host -> device -> host) on every rank, and the single-shape
     # host-inclusive encode on rank 0; both verified byte for byte
-    host_mixed = host_line = None
+    host_mixed = host_line = host_sample = None
     if not args.no_host:
         from quicknet_amd.hoststream import host_encode_leg, host_mixed_leg
-        host_mixed = host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather_float)
+        host_mixed = host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather_float,
+                                    sample_groups=64 if rank == 0 and world == 1 and not args.no_cpu else 0)
+        host_sample = host_mixed.pop("_sample", None)
         ok = ok and bool(host_mixed.get("verified"))
         # the same stream through the staged copies, for comparison (not the field's value)
         staged = host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather_float, passes=2, zero_copy=False)
@@ -831,9 +969,10 @@ def main(argv=None):
             cpu = cpu_baseline(args, args.cpu_seconds)
         except Exception as exc:  # report, never fake
             cpu = {"value": None, "error": repr(exc)}
-        if args.cpu_threads > 0:
+        threads = topology.cpu_share()["usable"] if args.cpu_threads is None else args.cpu_threads
+        if threads > 0:
             try:
-                cpu_mt = cpu_baseline_threads(args, args.cpu_seconds / 2, args.cpu_threads)
+                cpu_mt = cpu_baseline_threads(args, args.cpu_seconds / 2, threads)
             except Exception as exc:
                 cpu_mt = {"value": None, "error": repr(exc)}
         try:
@@ -850,6 +989,12 @@ def main(argv=None):
                     per_call["batch_beats_reference_encode_at_groups"] = beat[0] if beat else None
         except Exception as exc:
             cpu["per_call"] = {"error": repr(exc)}
+        if host_sample is not None:  # the checker role: config 5's output against the reference rs.c
+            try:
+                host_mixed["reference_check"] = cpu_check_host_sample(host_sample)
+                ok = ok and bool(host_mixed["reference_check"].get("match"))
+            except Exception as exc:
+                host_mixed["reference_check"] = {"error": repr(exc)}
         # the reference's datagram pipeline (FecCodecBuf.cpp + system/fec.c, oracle/_ref),
         # RS(10,13) 1 KiB payloads, send + receive, 1 thread: the CPU side of DESIGN 3.5
         ref_wire = os.path.join(ROOT, "oracle", "_ref", "ref_wire_bench")
@@ -861,6 +1006,9 @@ def main(argv=None):
             except Exception as exc:
                 cpu["wire"] = {"error": repr(exc)}
 
+    host_cpus = topology.cpu_share()
+    nn = numa.get("numa_node") if isinstance(numa, dict) else None
+    per_rank_numa = [int(x) for x in all_gather_float(float(-1 if nn is None else nn), world, rank)]
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -897,11 +1045,15 @@ def main(argv=None):
             "verified": ok,
             "cpu_baseline": cpu,
             "cpu_baseline_threads": cpu_mt,
+            "host_cpus": host_cpus,
+            "per_rank_numa": per_rank_numa,
+            "numa_binding_rank0": numa,
+            "process_group": torch.distributed.get_backend() if _dist_on() else None,
             "side_configs": side,
             "wire": wire,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         barrier(world)  # the other ranks wait for rank 0's side configurations, then all tear down
         dist.destroy_process_group()

@@ -107,7 +107,8 @@ def mixed_units(batches, zero_copy=True):
     return data, h2d, d2h
 
 
-def host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather, passes=3, streams=3, zero_copy=True):
+def host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather, passes=3, streams=3, zero_copy=True,
+                   sample_groups=0):
     dev = torch.device("cuda", torch.cuda.current_device())
     tune("host_zero_copy", int(zero_copy))
     try:
@@ -133,6 +134,8 @@ def host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather, passes=3,
     total = all_sum(float(data * passes), world)
     per_rank = all_gather((t1 - t0) * 1e3 / passes, world, rank)
     out = {"value": round(total / el / GIB, 2) if el > 0 else None, "unit": "GiB/s", "verified": ok,
+           "verified_against": "the pipe's own device-resident encode (parity) and the undamaged data (restored rows); "
+                               "bench.py's cpu_baseline leg re-checks a sample against the reference rs.c at N=1",
            "what": "BASELINE configs[4]: (4,2), (10,3) 1 KiB and (16,4) 1400 B batches of ~64 MiB data, interleaved, "
                    "encode + reconstruct (m random erasures of n per group), pinned host buffers per batch, "
                    f"qfec_pipe with {streams} HIP streams per GPU, "
@@ -149,8 +152,30 @@ def host_mixed_leg(rank, world, barrier, all_max, all_sum, all_gather, passes=3,
         out["error"] = err
     if err is None:
         pipe.close()
+        if sample_groups:
+            out["_sample"] = sample_batches(batches, sample_groups, rank)
     tune("host_zero_copy", 1)
     del batches
+    return out
+
+
+def sample_batches(batches, per_batch, rank):
+    """Copies of `per_batch` seeded random groups of every batch after the timed passes, as
+    numpy arrays, for an independent CPU check: the tx data and the parity the pipe wrote,
+    and the rx marks (rs.c layout) with the rows the pipe restored."""
+    import numpy as np
+    rng = np.random.default_rng(0x5A3F1E + rank)
+    out = []
+    for b in batches:
+        k, m, B, G = b["k"], b["m"], b["B"], b["G"]
+        idx = np.sort(rng.choice(G, size=min(per_batch, G), replace=False))
+        ti = torch.from_numpy(idx)
+        gm = b["rx_marks"].numpy()
+        dm, pm = gm[:G * k].reshape(G, k), gm[G * k:].reshape(G, m)
+        out.append({"k": k, "m": m, "B": B, "idx": idx,
+                    "data": b["tx_data"][ti, :, :B].numpy().copy(), "parity": b["tx_par"][ti, :, :B].numpy().copy(),
+                    "marks_data": dm[idx].copy(), "marks_parity": pm[idx].copy(),
+                    "restored": b["rx_data"][ti, :, :B].numpy().copy()})
     return out
 
 
