@@ -229,6 +229,13 @@ def dist_setup(args):
             print(f"bench.py: rank {rank} wants device {local} but {have} GPU(s) are visible", file=sys.stderr)
             raise SystemExit(2)
         torch.cuda.set_device(local)
+        if isinstance(numa, dict) and not args.no_numa_bind:
+            # the device HIP actually gave this rank: if sysfs ordering guessed another one,
+            # move to the right node now (before any pinned host allocation)
+            actual = topology.bdf_of_torch_device(torch.cuda.get_device_properties(local))
+            numa["bdf_hip"] = actual
+            if actual and numa.get("bdf") and actual != numa["bdf"]:
+                numa["rebound"] = topology.bind_bdf(actual)
     if world > 1 or args.force_dist:
         import torch.distributed as dist
         if backend == "nccl":

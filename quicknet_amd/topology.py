@@ -27,6 +27,7 @@ KFD_NODES = "sys/class/kfd/kfd/topology/nodes"
 # the sysfs root the functions read by default; tests point it at a fake tree
 SYSFS = os.environ.get("QFEC_SYSFS_ROOT", "/")
 PCI_DEVICES = "sys/bus/pci/devices"
+_UNREADABLE = 0  # KFD nodes the last kfd_gpus() call could not read
 
 
 def _read(path):
@@ -76,9 +77,14 @@ def kfd_gpus(sysfs=None):
     except OSError:
         return None
     gpus = []
+    global _UNREADABLE
+    _UNREADABLE = 0
     for i in ids:
         p = _props(os.path.join(root, str(i), "properties"))
-        if not p or not p.get("gfx_target_version"):
+        if p is None:  # a sandbox may hide other jobs' GPUs (EPERM); ROCr skips them too
+            _UNREADABLE += 1
+            continue
+        if not p.get("gfx_target_version"):
             continue
         loc, dom = p.get("location_id", 0), p.get("domain", 0)
         bdf = "%04x:%02x:%02x.%x" % (dom, (loc >> 8) & 0xFF, (loc >> 3) & 0x1F, loc & 0x7)
@@ -127,12 +133,41 @@ def visible_gpus(env=None, sysfs=None):
 
 
 def gpu_count(env=None, sysfs=None):
-    """(count, source) without any HIP call; count is None when sysfs does not say."""
+    """(count, source) without any HIP call.  count is None when sysfs does not say for sure:
+    the topology is unreadable, or some of its nodes are (then the count is only a lower
+    bound, and the launcher leaves the check to the ranks)."""
     sysfs = SYSFS if sysfs is None else sysfs
     devs = visible_gpus(env, sysfs)
     if devs is None:
         return None, "kfd topology unreadable"
-    return len(devs), "kfd topology (%s)" % os.path.join(sysfs, KFD_NODES)
+    src = "kfd topology (%s)" % os.path.join(sysfs, KFD_NODES)
+    if _UNREADABLE:
+        return None, "%s: %d readable GPU node(s), %d node(s) unreadable" % (src, len(devs), _UNREADABLE)
+    return len(devs), src
+
+
+def bdf_of_torch_device(props):
+    """The PCI function of a torch device-properties object (pci_domain_id/bus_id/device_id), or None."""
+    try:
+        return "%04x:%02x:%02x.0" % (props.pci_domain_id, props.pci_bus_id, props.pci_device_id)
+    except (AttributeError, TypeError):
+        return None
+
+
+def bind_bdf(bdf, sysfs=None, apply=True):
+    """Bind to the NUMA node of the PCI function `bdf` (the rank's post-init check)."""
+    sysfs = SYSFS if sysfs is None else sysfs
+    base = os.path.join(sysfs, PCI_DEVICES, bdf)
+    node_txt = _read(os.path.join(base, "numa_node"))
+    node = int(node_txt) if node_txt and node_txt.strip().lstrip("-").isdigit() else -1
+    cpus = parse_cpulist(_read(os.path.join(base, "local_cpulist")))
+    rec = {"bdf": bdf, "numa_node": node, "bound": False}
+    mine = os.sched_getaffinity(0)
+    target = cpus & mine
+    if target and apply:
+        os.sched_setaffinity(0, target)
+        rec.update(bound=True, cpus=len(target))
+    return rec
 
 
 def gpu_numa(local, env=None, sysfs=None):

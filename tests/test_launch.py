@@ -97,6 +97,12 @@ def test_topology_counts_and_places(tmp_path):
     assert T.gpu_numa(3, {}, root) is None
     assert T.parse_cpulist("0-2,5,7-8") == {0, 1, 2, 5, 7, 8}
     assert T.gpu_count({}, str(tmp_path / "none"))[0] is None
+    # a node the sandbox will not let us read (another job's GPU): the count is only a lower
+    # bound, so the launcher does not refuse on it; placement still follows the readable nodes
+    os.makedirs(os.path.join(root, "sys/class/kfd/kfd/topology/nodes", "9"))
+    n, why = T.gpu_count({}, root)
+    assert n is None and "unreadable" in why
+    assert T.gpu_numa(2, {}, root)["bdf"] == "0000:85:00.0"
 
 
 def test_bind_rank_dry_run(tmp_path):

@@ -23,11 +23,11 @@ grep -E "PASS|FAIL|launch-check|numa:" $OUT/pytest_launch.log
 echo "== bench (N=1)"
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 3; }
 python -c "
-import json; d=json.load(open('$OUT/bench.json'))
+import json; d=[json.loads(l) for l in open('$OUT/bench.json') if l.startswith('{')][-1]
 print({k: d[k] for k in ('value','verified','host_cpus','per_rank_numa','numa_binding_rank0','process_group')})
 print('cpu_mt', d['cpu_baseline_threads']); print('ref check', d['host_to_host_mixed'].get('reference_check'))"
 echo "== bench --gpus 2 (gloo rehearsal)"
 QFEC_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 20 --no-cpu > $OUT/bench_g2.json 2> $OUT/bench_g2.err || { tail -30 $OUT/bench_g2.err; exit 4; }
 python -c "
-import json; d=json.load(open('$OUT/bench_g2.json'))
+import json; d=[json.loads(l) for l in open('$OUT/bench_g2.json') if l.startswith('{')][-1]
 print({k: d[k] for k in ('value','verified','n_gpus','per_rank_numa','numa_binding_rank0','process_group')})"
