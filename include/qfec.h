@@ -166,7 +166,8 @@ int qfec_unpack_datagrams(qfec_code *code, const unsigned char *d_wire, long lon
  * with bytes 1.. XORed by mask ^ gmask ^ 0x5a, mask = d_mask[r] (the session's _mask++),
  * c = CheckSum(bytes 2..) & 0xff, CheckSum(x) = ~(fold16(byte sum)) (ProtocolBasic.cpp:56-87).
  * The 8-byte Session prefix is present iff d_conv_hid ([rows][2] conv, hid) is non-NULL.
- * d_out_len[r] = framed length, or -1 when it does not fit out_pitch.
+ * d_out_len[r] = framed length, or -1 when it does not fit out_pitch.  Bytes of a row past its
+ * frame, up to out_pitch, are zero, and a row with d_out_len -1 is all zero (every path).
  * qfec_unframe_udp reverses it (ProtocolUdp::RecvPacket, ProtocolBasic.cpp:152-210):
  * d_status[r] = 0 ok, 1 short, 2 bad checksum, 3 bad cmd, 4 too long; d_out row = the data,
  * d_out_len = len - 4 (- 8 with session = 1); d_info [rows][4] = xor mask, c, cmd & 0x1f,
@@ -178,6 +179,34 @@ int qfec_frame_udp(const unsigned char *d_in, long long in_pitch, const int *d_l
 int qfec_unframe_udp(const unsigned char *d_in, long long in_pitch, const int *d_len, long long rows, int gmask,
                      int session, unsigned char *d_out, long long out_pitch, int *d_out_len, int *d_status,
                      unsigned char *d_info, unsigned int *d_conv_hid, void *stream);
+
+/* ---- FEC datagrams straight to / from ProtocolUdp frames (SURVEY 8(f) ranks 2-4 fused) ----
+ * qfec_pack_frames = qfec_pack_datagrams followed by qfec_frame_udp on every datagram, with
+ * cmd / protocol as Session::TransmissionOutput sets them for FEC data (QUICKNET_CMD_DATA,
+ * QUICKNET_PROTOCOL_FEC, network/SessionDesc.cpp:513-519): frame row (g, j) of d_frames =
+ * [mask][c][(cmd & 0x1f) | 0xA0][protocol]([conv][hid])[datagram (g, j)], bytes 1.. XORed with
+ * d_mask[g*n+j] ^ gmask ^ 0x5a; d_frame_len[g*n+j] = framed length (-1 for a void group).
+ * The Session prefix is present iff d_conv_hid ([G*n][2]) is non-NULL.  Bytes of a row past its
+ * frame, up to frame_pitch, are zero.  One pass (no datagram buffer in HBM) with checksums on, a
+ * templated (k, m) and frame_pitch = 1088 or 576 equal to the 64-B multiple above prefix + 13 +
+ * shard_pitch (1 KiB / 512-B payloads); other cases run the two calls over stream-ordered scratch.
+ * d_shards is scratch as in qfec_pack_datagrams.
+ * qfec_unpack_frames = qfec_unframe_udp (ProtocolUdp::RecvPacket, ProtocolBasic.cpp:155-199) of
+ * every row, rows RecvPacket rejects counting as not received, then qfec_unpack_datagrams over
+ * the datagrams inside: the same d_marks / d_rx_size / d_status / d_psize / d_shards as that
+ * call.  d_frame_status [G*n] (nullable) = RecvPacket's verdict per row (0 ok, 1 short,
+ * 2 checksum, 3 cmd, 4 too long, as qfec_unframe_udp); d_conv_hid receives the Session prefix
+ * of rows with status 0 when session = 1 (nullable).  One pass for the templated (k, m). */
+int qfec_pack_frames(qfec_code *code, const unsigned char *d_payload, const long long *d_offsets,
+                     const int *d_sizes, const unsigned int *d_seq, long long groups, int checksum,
+                     unsigned char *d_shards, long long shard_pitch, const unsigned char *d_mask,
+                     const unsigned int *d_conv_hid, int gmask, int cmd, int protocol, unsigned char *d_frames,
+                     long long frame_pitch, int *d_frame_len, void *stream);
+int qfec_unpack_frames(qfec_code *code, const unsigned char *d_frames, long long frame_pitch,
+                       const int *d_frame_len, long long groups, int gmask, int session, int checksum,
+                       int dec_pkt_size, unsigned char *d_shards, long long shard_pitch, unsigned char *d_marks,
+                       int *d_rx_size, int *d_status, int *d_psize, int *d_frame_status,
+                       unsigned int *d_conv_hid, void *stream);
 
 /* Fill nbytes of device memory with the synthetic stream of quicknet_amd/synth.py. */
 int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long seed, void *stream);

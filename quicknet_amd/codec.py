@@ -226,7 +226,10 @@ class Code:
                        stream=None):
         """payload: uint8 device tensor (16 readable bytes past the last packet); offsets int64
         [G*k]; sizes int32 [G*k]; seq uint32/int32 [G, 2] (sent, src index of each group's first
-        packet).  Returns (shards [G, n, pitch], wire [G, n, wire_pitch], wire_len int32 [G, n])."""
+        packet).  Returns (shards [G, n, pitch], wire [G, n, wire_pitch], wire_len int32 [G, n]).
+        wire_pitch defaults to the 64-B multiple above 13 + shard_pitch (1088 for 1 KiB payloads;
+        round 1 used the 16-B multiple, 1056): the fused send then writes whole 64-B lines.  Pass
+        wire_pitch explicitly where a consumer needs another row layout."""
         import torch
         G = sizes.numel() // self.k
         n = self.k + self.m
@@ -264,6 +267,60 @@ class Code:
                                           _dev_ptr(status, _I32), _dev_ptr(psize, _I32), _stream_handle(stream)),
               "qfec_unpack_datagrams")
         return shards, status, psize, rx
+
+    # -- the same batches straight to / from ProtocolUdp frames (qfec_pack_frames / qfec_unpack_frames)
+    def pack_frames(self, payload, offsets, sizes, seq, masks, gmask=0, cmd=0x11, protocol=0xFF, conv_hid=None,
+                    checksum=True, shard_pitch=None, frame_pitch=None, stream=None):
+        """pack_datagrams + frame_udp in one call: masks uint8 [G*n] (one per datagram), conv_hid
+        int32/uint32 [G*n, 2] or None (no Session prefix).  frame_pitch defaults to the 64-B
+        multiple above prefix + 13 + shard_pitch (the one-pass kernel's pitch for 1 KiB and
+        512-B payloads).  Returns (frames [G, n, frame_pitch], frame_len int32 [G, n])."""
+        import torch
+        G = sizes.numel() // self.k
+        n = self.k + self.m
+        head = 4 if checksum else 2
+        P = 12 if conv_hid is not None else 4
+        if shard_pitch is None:
+            shard_pitch = (int(sizes.max().item()) + head + 15) // 16 * 16 if G else 16
+        if frame_pitch is None:
+            frame_pitch = (shard_pitch + 13 + P + 63) // 64 * 64
+        dev = payload.device
+        shards = torch.empty((G, n, shard_pitch), dtype=torch.uint8, device=dev)
+        frames = torch.empty((G, n, frame_pitch), dtype=torch.uint8, device=dev)
+        flen = torch.empty((G, n), dtype=torch.int32, device=dev)
+        check(lib().qfec_pack_frames(self._h, _dev_ptr(payload, what="payload"), _dev_ptr(offsets, _I64, "offsets"),
+                                     _dev_ptr(sizes, _I32, "sizes"), _dev_ptr(seq, _I32, "seq"), G, int(bool(checksum)),
+                                     _dev_ptr(shards), shard_pitch, _dev_ptr(masks, what="masks"),
+                                     _dev_ptr(conv_hid, _I32, "conv_hid") if conv_hid is not None else None,
+                                     int(gmask), int(cmd), int(protocol), _dev_ptr(frames), frame_pitch,
+                                     _dev_ptr(flen, _I32), _stream_handle(stream)), "qfec_pack_frames")
+        return frames, flen
+
+    def unpack_frames(self, frames, frame_len, gmask=0, session=False, checksum=True, dec_pkt_size=2068,
+                      shard_pitch=None, stream=None):
+        """unframe_udp + unpack_datagrams in one call.  frames [G, n, frame_pitch], frame_len int32
+        [G, n] (0 = not received).  Returns (shards, status, psize, rx_size, frame_status [G, n],
+        conv_hid [G, n, 2] int32 or None)."""
+        import torch
+        G, n, fpitch = frames.shape
+        P = 12 if session else 4
+        if shard_pitch is None:
+            shard_pitch = (fpitch - 13 - P) // 16 * 16
+        dev = frames.device
+        shards = torch.empty((G, n, shard_pitch), dtype=torch.uint8, device=dev)
+        marks = torch.empty(G * n, dtype=torch.uint8, device=dev)
+        rx = torch.empty((G, n), dtype=torch.int32, device=dev)
+        status = torch.empty((G, self.k), dtype=torch.int32, device=dev)
+        psize = torch.empty((G, self.k), dtype=torch.int32, device=dev)
+        fst = torch.empty((G, n), dtype=torch.int32, device=dev)
+        ch = torch.zeros((G, n, 2), dtype=torch.int32, device=dev) if session else None
+        check(lib().qfec_unpack_frames(self._h, _dev_ptr(frames, what="frames"), fpitch,
+                                       _dev_ptr(frame_len, _I32, "frame_len"), G, int(gmask), int(bool(session)),
+                                       int(bool(checksum)), dec_pkt_size, _dev_ptr(shards), shard_pitch, _dev_ptr(marks),
+                                       _dev_ptr(rx, _I32), _dev_ptr(status, _I32), _dev_ptr(psize, _I32),
+                                       _dev_ptr(fst, _I32), _dev_ptr(ch, _I32) if ch is not None else None,
+                                       _stream_handle(stream)), "qfec_unpack_frames")
+        return shards, status, psize, rx, fst, ch
 
     def decode_rows(self, marks_n):
         """Host-side decode matrix for one group-order mark vector: (e, rows[e,k], survivors[k], erased[e])."""

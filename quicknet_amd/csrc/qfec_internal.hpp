@@ -113,6 +113,22 @@ struct FrameArgs {
     int session;              // 1: the 8-byte conv/hid prefix is part of the frame
 };
 hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s);
+// ProtocolUdp framing inside the datagram kernels (qfec_pack_frames / qfec_unpack_frames)
+struct FrameSend {
+    const uint8_t* mask;       // [G*n] raw mask bytes (Session::PacketOutput's _mask++)
+    const uint32_t* conv_hid;  // [G*n][2] Session prefix, or NULL (4-byte prefix)
+    uint32_t gmask, cmd, protocol;
+};
+struct FrameRecv {
+    uint32_t gmask;
+    int32_t* status;           // [G*n] RecvPacket verdict (0 ok, 1 short, 2 checksum, 3 cmd, 4 too long); nullable
+    uint32_t* conv_hid;        // [G*n][2] Session prefix out (session frames only); nullable
+};
+hipError_t launch_pack_frames(const WireArgs& a, const FrameSend& fs, int fp, const uint32_t* tab, hipStream_t s,
+                              bool* launched);
+hipError_t launch_unpack_frames(const WireArgs& a, const FrameRecv& fr, int fp, const int32_t* lut,
+                                const uint32_t* records, uint32_t rec_hdr, hipStream_t s, bool* launched);
+hipError_t launch_len_by_status(int32_t* len, const int32_t* status, uint64_t rows, hipStream_t s);
 // fused receive for templated (k, m); *launched = false when the shape has no instance
 hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
                                hipStream_t s, bool* launched);

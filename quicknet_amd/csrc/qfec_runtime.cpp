@@ -1314,6 +1314,18 @@ int wire_check(const qfec_code* c, long long groups, int checksum, long long pit
     return QFEC_OK;
 }
 
+// frame rows: a 16-B multiple pitch that holds prefix + 13 + shard pitch
+int frame_check(const qfec_code* c, long long groups, int checksum, long long pitch, long long frame_pitch, int fp,
+                const void* shards, const void* frames) {
+    const int rc = wire_check(c, groups, checksum, pitch, (long long)round_up((size_t)pitch + 13, 16), shards, frames);
+    if (rc) return rc;
+    if (frame_pitch % 16 || frame_pitch < pitch + 13 + fp) {
+        set_error("frames: frame pitch must be a multiple of 16 and >= prefix (%d) + 13 + shard pitch", fp);
+        return QFEC_EINVAL;
+    }
+    return QFEC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1423,6 +1435,131 @@ int qfec_unpack_datagrams(qfec_code* code, const unsigned char* d_wire, long lon
     return e == hipSuccess ? QFEC_OK : hip_fail(e, "check_payloads launch");
 }
 
+
+// ---- datagrams straight to / from ProtocolUdp frames (one pass where a kernel instance exists)
+int qfec_pack_frames(qfec_code* code, const unsigned char* d_payload, const long long* d_offsets, const int* d_sizes,
+                     const unsigned int* d_seq, long long groups, int checksum, unsigned char* d_shards,
+                     long long shard_pitch, const unsigned char* d_mask, const unsigned int* d_conv_hid, int gmask,
+                     int cmd, int protocol, unsigned char* d_frames, long long frame_pitch, int* d_frame_len,
+                     void* stream) {
+    const int fp = d_conv_hid ? 12 : 4;
+    int rc = frame_check(code, groups, checksum, shard_pitch, frame_pitch, fp, d_shards, d_frames);
+    if (rc) return rc;
+    if (!d_mask || !d_frame_len) return QFEC_EINVAL;
+    if (groups == 0) return QFEC_OK;
+    DevCtx* ctx = nullptr;
+    if ((rc = current_ctx(&ctx))) return rc;
+    uint32_t* tab = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_enc(code, ctx->device, &tab);
+    }
+    if (rc) return rc;
+    const int k = code->k, m = code->m, n = k + m;
+    hipStream_t s = (hipStream_t)stream;
+    if (tuning().wire_fused) {
+        WireArgs a{};
+        a.payload = d_payload;
+        a.offsets = (const int64_t*)d_offsets;
+        a.sizes = d_sizes;
+        a.seq = d_seq;
+        a.pitch = (uint64_t)shard_pitch;
+        a.group_stride = (uint64_t)n * shard_pitch;
+        a.wire = d_frames;
+        a.wire_pitch = (uint64_t)frame_pitch;
+        a.wire_len = d_frame_len;
+        a.groups = (uint64_t)groups;
+        a.k = k;
+        a.m = m;
+        a.checksum = checksum;
+        a.store_nt = tuning().wire_store_nt;
+        FrameSend fs{d_mask, d_conv_hid, (uint32_t)gmask & 0xFFu, (uint32_t)cmd, (uint32_t)protocol};
+        bool launched = false;
+        const hipError_t e = launch_pack_frames(a, fs, fp, tab, s, &launched);
+        if (e != hipSuccess) return hip_fail(e, "pack_frames launch");
+        if (launched) return QFEC_OK;
+    }
+    // two passes: datagrams into stream-ordered scratch, then qfec_frame_udp over them
+    const long long wp = (long long)round_up((size_t)shard_pitch + 13, 16);
+    const size_t rows = (size_t)groups * n, wbytes = rows * (size_t)wp;
+    uint8_t* scratch = nullptr;
+    if (hipMallocAsync((void**)&scratch, wbytes + rows * 4, s) != hipSuccess)
+        return hip_fail(hipGetLastError(), "pack_frames scratch");
+    int* wlen = reinterpret_cast<int*>(scratch + wbytes);
+    rc = qfec_pack_datagrams(code, d_payload, d_offsets, d_sizes, d_seq, groups, checksum, d_shards, shard_pitch,
+                             scratch, wp, wlen, stream);
+    if (!rc)
+        rc = qfec_frame_udp(scratch, wp, wlen, (long long)rows, d_mask, d_conv_hid, gmask, cmd, protocol, d_frames,
+                            frame_pitch, d_frame_len, stream);
+    (void)hipFreeAsync(scratch, s);
+    return rc;
+}
+
+int qfec_unpack_frames(qfec_code* code, const unsigned char* d_frames, long long frame_pitch, const int* d_frame_len,
+                       long long groups, int gmask, int session, int checksum, int dec_pkt_size,
+                       unsigned char* d_shards, long long shard_pitch, unsigned char* d_marks, int* d_rx_size,
+                       int* d_status, int* d_psize, int* d_frame_status, unsigned int* d_conv_hid, void* stream) {
+    if (session != 0 && session != 1) return QFEC_EINVAL;
+    const int fp = session ? 12 : 4;
+    int rc = frame_check(code, groups, checksum, shard_pitch, frame_pitch, fp, d_shards, d_frames);
+    if (rc) return rc;
+    if (groups == 0) return QFEC_OK;
+    if (!d_marks || !d_status || !d_psize || !d_frame_len) return QFEC_EINVAL;
+    DevCtx* ctx = nullptr;
+    if ((rc = current_ctx(&ctx))) return rc;
+    DevTables* d = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(code->mu);
+        rc = ensure_lut(code, ctx->device, &d);
+    }
+    if (rc) return rc;
+    const int k = code->k, m = code->m, n = k + m;
+    hipStream_t s = (hipStream_t)stream;
+    if (tuning().wire_fused_rx && d->d_lut) {
+        WireArgs a{};
+        a.shards = d_shards;
+        a.pitch = (uint64_t)shard_pitch;
+        a.group_stride = (uint64_t)n * shard_pitch;
+        a.wire = const_cast<uint8_t*>(d_frames);
+        a.wire_pitch = (uint64_t)frame_pitch;
+        a.wire_len = const_cast<int32_t*>(d_frame_len);
+        a.marks = d_marks;
+        a.rx_size = d_rx_size;
+        a.status = d_status;
+        a.psize = d_psize;
+        a.groups = (uint64_t)groups;
+        a.k = k;
+        a.m = m;
+        a.checksum = checksum;
+        a.dec_pkt_size = dec_pkt_size;
+        FrameRecv fr{(uint32_t)gmask & 0xFFu, d_frame_status, session ? d_conv_hid : nullptr};
+        bool launched = false;
+        const hipError_t e = launch_unpack_frames(a, fr, fp, d->d_lut, d->d_rec, (uint32_t)record_layout(k, m).hdr, s,
+                                                  &launched);
+        if (e != hipSuccess) return hip_fail(e, "unpack_frames launch");
+        if (launched) return QFEC_OK;
+    }
+    // two passes: qfec_unframe_udp into stream-ordered scratch (rows RecvPacket rejects count as
+    // not received), then qfec_unpack_datagrams
+    const long long wp = (long long)round_up((size_t)frame_pitch, 16);
+    const size_t rows = (size_t)groups * n, wbytes = rows * (size_t)wp;
+    uint8_t* scratch = nullptr;
+    if (hipMallocAsync((void**)&scratch, wbytes + rows * 8, s) != hipSuccess)
+        return hip_fail(hipGetLastError(), "unpack_frames scratch");
+    int* wlen = reinterpret_cast<int*>(scratch + wbytes);
+    int* fst = d_frame_status ? d_frame_status : wlen + rows;
+    rc = qfec_unframe_udp(d_frames, frame_pitch, d_frame_len, (long long)rows, gmask, session, scratch, wp, wlen, fst,
+                          nullptr, session ? d_conv_hid : nullptr, stream);
+    if (!rc) {
+        const hipError_t e = launch_len_by_status(wlen, fst, rows, s);
+        if (e != hipSuccess) rc = hip_fail(e, "len_by_status launch");
+    }
+    if (!rc)
+        rc = qfec_unpack_datagrams(code, scratch, wp, wlen, groups, checksum, dec_pkt_size, d_shards, shard_pitch,
+                                   d_marks, d_rx_size, d_status, d_psize, stream);
+    (void)hipFreeAsync(scratch, s);
+    return rc;
+}
 
 int qfec_frame_udp(const unsigned char* d_in, long long in_pitch, const int* d_len, long long rows,
                    const unsigned char* d_mask, const unsigned int* d_conv_hid, int gmask, int cmd, int protocol,

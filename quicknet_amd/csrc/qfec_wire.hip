@@ -81,6 +81,18 @@ __device__ __forceinline__ uint32_t get_byte(const uint4& v, int pos) {
     return (w >> (8 * (pos & 3))) & 0xFFu;
 }
 
+// lanes of one wave hand data to each other through LDS: make the order explicit (a release /
+// acquire pair at wavefront scope around a wave barrier; no workgroup barrier is needed)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint4 xor16(uint4 v, uint32_t mm) {
+    return make_uint4(v.x ^ mm, v.y ^ mm, v.z ^ mm, v.w ^ mm);
+}
+
 // datagram store: non-temporal or write-back (tuning "wire_store_nt"), wave-uniform flag
 __device__ __forceinline__ void stw(uint8_t* p, const uint4& v, int nt) {
     if (nt) st16(p, v);
@@ -720,13 +732,23 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
     }
 }
 
-template <int K, int M, int GPW>
+// FP (frame prefix 4 or 12, qfec_pack_frames): the same pass emits ProtocolUdp frames
+// instead of bare datagrams -- frame = [mask][c][cmd][proto]([conv][hid])[datagram], bytes 1..
+// XORed with mask ^ gmask ^ 0x5a (network/ProtocolBasic.cpp:111-150, SessionDesc.cpp:69-77).
+// Lane ln then owns frame chunk 4 + ln, i.e. datagram bytes shifted down by FP (the payload
+// loads are unaligned anyway); line 0's dword ln is datagram dword ln - FP/4, the prefix below
+// it.  The frame checksum is the datagram's byte sum (header + the shard sum the wave already
+// has) plus the prefix bytes, so no byte is read twice.  Bytes of a row past its frame are 0.
+template <int K, int M, int GPW, int FP = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
                                                      const int64_t* __restrict__ offsets,
                                                      const int32_t* __restrict__ sizes,
                                                      const uint32_t* __restrict__ seq,
-                                                     const uint32_t* __restrict__ tab, uint64_t groups) {
+                                                     const uint32_t* __restrict__ tab, uint64_t groups,
+                                                     FrameSend fs) {
     constexpr int N = K + M, HDR = 13, HEAD = 4, LPG = 64 / GPW;  // lanes per group
+    constexpr int FD = FP / 4;                                      // prefix dwords of line 0
+    static_assert(FP == 0 || FP == 4 || FP == 12, "frame prefix");
     const int lane = threadIdx.x & 63;
     const int ln = GPW == 1 ? lane : lane % LPG;  // lane within its group: chunk 4 + ln
     const uint64_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));  // wave-uniform
@@ -736,7 +758,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     const uint64_t g = GPW == 1 ? w : w * GPW + (uint64_t)(lane / LPG);
     const bool live = GPW == 1 || g < groups;
     const int t = 4 + ln;
-    const int p = 16 * t - HDR - HEAD;  // payload offset of this chunk's first byte (>= 47)
+    const int p = 16 * t - FP - HDR - HEAD;  // payload offset of this chunk's first byte (>= 35)
     int size[K], gmax = 0;
     bool ok = false;
     if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
@@ -747,6 +769,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     int64_t off[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) off[i] = ok ? offsets[g * K + i] : 0;
+    uint32_t mm[FP ? N : 1];  // per-row XOR word (frame bytes 1..)
+    if constexpr (FP != 0) {
+#pragma unroll
+        for (int r = 0; r < N; ++r)
+            mm[r] = ok ? ((fs.mask[g * N + r] ^ fs.gmask ^ 0x5Au) & 0xFFu) * 0x01010101u : 0u;
+    }
     uint8_t* out_g = a.wire + g * (uint64_t)N * a.wire_pitch;
     uint4 x[K];
 #pragma unroll
@@ -767,25 +795,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     uint8_t* out = out_g + 16 * t;
 #pragma unroll
     for (int r = 0; r < N; ++r) {
-        const uint4 v = r < K ? x[r] : acc[r - K];
-        if (ok) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
+        uint4 v = r < K ? x[r] : acc[r - K];
         if (r >= K) ps[r] = sum16(v, 0);
+        if constexpr (FP != 0) {  // XOR the frame's bytes only: padding past it stays 0
+            const int total = FP + HDR + (r < K ? size[r] + HEAD : gmax);
+            v = make_uint4(v.x ^ (mm[r] & byte_mask(0, total - 16 * t, 0)), v.y ^ (mm[r] & byte_mask(0, total - 16 * t, 1)),
+                           v.z ^ (mm[r] & byte_mask(0, total - 16 * t, 2)), v.w ^ (mm[r] & byte_mask(0, total - 16 * t, 3)));
+        }
+        if (ok) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
     }
     // ---- line 0
-    // line 0's payload dwords (lanes ln 0..15: datagram bytes 4 ln .. 4 ln + 3; payload byte
-    // 4 ln - 17 at its first byte)
-    const int q = 4 * ln - HDR - HEAD;
+    // line 0's payload dwords (lanes ln 0..15: frame bytes 4 ln .. 4 ln + 3 = datagram dword
+    // dl = ln - FD; payload byte 4 dl - 17 at its first byte)
+    const int dl = ln - FD;
+    const int q = 4 * dl - HDR - HEAD;
     uint32_t pay[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         pay[i] = 0;
-        if (ok && ln >= 4 && ln < 16) __builtin_memcpy(&pay[i], payload + off[i] + min(max(q, 0), size[i]), 4);
+        if (ok && dl >= 4 && ln < 16) __builtin_memcpy(&pay[i], payload + off[i] + min(max(q, 0), size[i]), 4);
     }
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         // byte j of the dword holds payload byte q + j (dword 4: loaded from payload byte 0 and
         // shifted up one byte); keep the bytes below the payload's size
-        const uint32_t v = ln == 4 ? pay[i] << 8 : pay[i];
+        const uint32_t v = dl == 4 ? pay[i] << 8 : pay[i];
         const int nb = min(max(size[i] - q, 0), 4);
         pay[i] = nb >= 4 ? v : v & ((1u << (8 * nb)) - 1u);
     }
@@ -797,7 +831,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
     for (int i = 0; i < K; ++i) {
         const uint32_t wd = ((uint32_t)size[i] & 0xFFFFu) | ((tot[i] & 0xFFFFu) << 16);  // shard bytes 0-3
-        sh[i] = !ok ? 0u : ln == 3 ? wd << 8 : ln == 4 ? (wd >> 24) | pay[i] : pay[i];
+        sh[i] = !ok || dl < 3 ? 0u : dl == 3 ? wd << 8 : dl == 4 ? (wd >> 24) | pay[i] : pay[i];
     }
     uint32_t par[M];  // check rows' shard view: a dword-wide encode of the data rows'
 #pragma unroll
@@ -819,6 +853,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         return;
     }
     const uint32_t sent0 = seq[2 * g], src0 = seq[2 * g + 1];
+    uint32_t fcmd = 0, fproto = 0;
+    if constexpr (FP != 0) {
+        fcmd = (fs.cmd & 0x1Fu) | 0xA0u;
+        fproto = fs.protocol & 0xFFu;
+    }
 #pragma unroll
     for (int r = 0; r < N; ++r) {
         uint32_t dsum;
@@ -832,17 +871,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         const uint32_t sent = sent0 + (uint32_t)r, src = src0 + (uint32_t)(r < K ? r : K - 1);
         const uint32_t ikn = ((uint32_t)N | ((uint32_t)K << 4) | ((uint32_t)r << 8)) & 0xFFFFu;
         uint32_t d = v;
-        if (ln == 0) d = 0xEDu | (sent << 8);
-        else if (ln == 1) d = (sent >> 24) | (src << 8);
-        else if (ln == 2) d = (src >> 24) | (ikn << 8) | ((dsum & 0xFFu) << 24);
-        else if (ln == 3) d = ((dsum >> 8) & 0xFFu) | v;
+        if (dl == 0) d = 0xEDu | (sent << 8);
+        else if (dl == 1) d = (sent >> 24) | (src << 8);
+        else if (dl == 2) d = (src >> 24) | (ikn << 8) | ((dsum & 0xFFu) << 24);
+        else if (dl == 3) d = ((dsum >> 8) & 0xFFu) | v;
+        if constexpr (FP != 0) {
+            const int total = FP + HDR + (r < K ? size[r] + HEAD : gmax);
+            uint32_t conv = 0, hid = 0;
+            if (FP == 12) {
+                conv = fs.conv_hid[2 * (g * N + r)];
+                hid = fs.conv_hid[2 * (g * N + r) + 1];
+            }
+            // CheckSum over frame bytes 2.. (ProtocolBasic.cpp:80-87): cmd, protocol, the Session
+            // prefix and every datagram byte -- the header's bytes plus the shard sum dsum
+            const uint32_t hsum = 0xEDu + __builtin_amdgcn_sad_u8(sent, 0u, 0u) + __builtin_amdgcn_sad_u8(src, 0u, 0u) +
+                                  (ikn & 0xFFu) + (ikn >> 8) + (dsum & 0xFFu) + ((dsum >> 8) & 0xFFu);
+            const uint32_t fsum = fcmd + fproto + __builtin_amdgcn_sad_u8(conv, 0u, 0u) +
+                                  __builtin_amdgcn_sad_u8(hid, 0u, 0u) + hsum + dsum;
+            const uint32_t c = ~((fsum >> 16) + (fsum & 0xFFFFu)) & 0xFFu;
+            if (ln == 0) d = (c | (fcmd << 8) | (fproto << 16)) << 8;
+            else if (FP == 12 && ln == 1) d = conv;
+            else if (FP == 12 && ln == 2) d = hid;
+            d ^= mm[r] & byte_mask(ln == 0 ? 1 : 0, total - 4 * ln, 0);
+            if (ln == 0) d |= fs.mask[g * N + r];
+        }
         if (ln < 16) {
             uint32_t* dst = reinterpret_cast<uint32_t*>(out_g + (uint64_t)r * a.wire_pitch + 4 * ln);
             if (a.store_nt & 2) __builtin_nontemporal_store(d, dst);
             else *dst = d;
         }
     }
-    if (ln < N) a.wire_len[g * N + ln] = HDR + (ln < K ? size[ln] + HEAD : gmax);
+    if (ln < N) a.wire_len[g * N + ln] = FP + HDR + (ln < K ? size[ln] + HEAD : gmax);
 }
 
 // A lane's slice of a shard row in one pass: NV16 = 4 -> one 16-B chunk at pos16, then NVT
@@ -1274,6 +1333,11 @@ struct RxSl {
             for (int d = NVA; d < NV; ++d) v[d] = keep_dw(v[d], n - pos(d));
         }
     }
+    // un-XOR the dwords this lane loaded (ProtocolUdp frames); the others stay 0
+    __device__ __forceinline__ void xor_act(uint32_t (&v)[NV], uint32_t mm) const {
+#pragma unroll
+        for (int d = 0; d < NV; ++d) v[d] ^= act(d) ? mm : 0u;
+    }
     __device__ __forceinline__ static uint32_t keep_dw(uint32_t x, int nb) {  // the low nb bytes of x
         const int c = min(max(nb, 0), 4);
         return c >= 4 ? x : x & ((1u << (8 * c)) - 1u);
@@ -1288,6 +1352,7 @@ struct RxSl {
 template <int K, int M>
 struct RxP {
     uint32_t v_off, v_rs;
+    uint32_t v_mm;  // frames: lane c survivor c's XOR word, lane K + r checksum-only row r's
     int ns, e, nx;
     bool dec, recoverable;
     uint32_t zero_rows, svmask, lost_data;
@@ -1295,7 +1360,7 @@ struct RxP {
     const uint32_t* tab;
 };
 
-template <int K, int M, int NVA, int NVT>
+template <int K, int M, int NVA, int NVT, int FP = 0>
 __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restrict__ wire_g, uint8_t* __restrict__ out_g,
                                          uint64_t pitch, const RxSl<NVA, NVT>& sl, bool first, int head, int end_a,
                                          int end_t,
@@ -1303,12 +1368,18 @@ __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restric
     constexpr int NV = NVA + NVT;
     // opaque per pass: the v_readlane results below are not carried across passes in SGPRs
     asm volatile("" : "+v"(pl.v_off), "+v"(pl.v_rs), "+v"(v_w0));
+    if constexpr (FP != 0) asm volatile("" : "+v"(pl.v_mm));
     uint32_t x[K][NV];
 #pragma unroll
     for (int c = 0; c < K; ++c) {
 #pragma unroll
         for (int d = 0; d < NV; ++d) x[c][d] = 0;
         if (c < pl.ns) sl.load(x[c], wire_g + lane_of(pl.v_off, c));
+    }
+    if constexpr (FP != 0) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+            if (c < pl.ns) sl.xor_act(x[c], lane_of(pl.v_mm, c));
     }
     // some survivor's datagram ends inside this pass: keep [0, size) (end_a / end_t: where the
     // pass's NVA part and tail dwords end)
@@ -1381,6 +1452,7 @@ __device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restric
 #pragma unroll
             for (int d = 0; d < NV; ++d) y[d] = 0;
             sl.load(y, wire_g + lane_of(pl.v_off, K + r));
+            if constexpr (FP != 0) sl.xor_act(y, lane_of(pl.v_mm, K + r));
             const int xs = (int)(lane_of(pl.v_rs, K + r) >> 16);
             sl.keep_below(y, xs, end_a > xs, end_t > xs);
             xsum[r] += sum_vec<NV>(y);
@@ -1397,12 +1469,22 @@ __device__ __forceinline__ uint32_t head_bytes_sum(uint32_t w0, int head) {
 // instruction, so no 64-B line is written in two parts where a row ends mid-line (pitch 1040)
 extern __shared__ uint4 rx_stage[];
 
-template <int K, int M, int NVA, bool LDSW = false>
+// FP (frame prefix 4 or 12, qfec_unpack_frames): the rows are ProtocolUdp frames of the
+// datagrams.  Lanes j < n read frame j's mask byte and un-XOR its first 32 bytes: RecvPacket's
+// length and cmd tests (network/ProtocolBasic.cpp:155-199) join the FEC header tests, every
+// survivor / checksum-only load is un-XORed with its row's word, and a row whose frame checksum
+// (prefix bytes + datagram header + the shard sum the passes produce) fails is dropped like a
+// datagram with a bad shard checksum -- RecvPacket returns it before the FEC layer sees it.  In
+// frame mode every good non-survivor row is read and checked (the frame checksum covers rows
+// the datagram checksum does not), and rows whose FEC header is rejected get their checksum
+// from a last per-row pass, so fr.status is RecvPacket's verdict for every row: 0 ok, 1 short,
+// 2 checksum, 3 cmd, 4 too long (as qfec_unframe_udp).
+template <int K, int M, int NVA, bool LDSW = false, int FP = 0>
 __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const uint8_t* __restrict__ wire,
                                                    const int32_t* __restrict__ wire_len,
                                                    const int32_t* __restrict__ lut,
                                                    const uint32_t* __restrict__ records, uint32_t rec_hdr,
-                                                   uint8_t* __restrict__ shards) {
+                                                   uint8_t* __restrict__ shards, FrameRecv fr) {
     constexpr int N = K + M;
     constexpr int A = 256 * NVA;  // row bytes per full pass
     const int lane = threadIdx.x & 63;
@@ -1417,17 +1499,43 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
     int len = 0, hdr = 11, size = 0;
     uint32_t stated = 0;
     bool okh = false;
+    uint32_t v_fx = 0, v_fs = 0;  // frames, lane r: row r's XOR byte; its prefix + header byte sum | check << 24
+    int fst = 0;                  // frames, lane r: RecvPacket's verdict before the checksum
     if (lane < N) {
         len = wire_len[g * N + lane];
-        const uint4 h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
+        int dlen = len;
+        uint4 h;
+        if constexpr (FP != 0) {
+            const uint8_t* frow = wire_g + (uint64_t)lane * wp;
+            const uint4 f0 = *reinterpret_cast<const uint4*>(frow), f1 = *reinterpret_cast<const uint4*>(frow + 16);
+            v_fx = (get_byte(f0, 0) ^ fr.gmask ^ 0x5Au) & 0xFFu;
+            const uint32_t mmx = v_fx * 0x01010101u;
+            const uint4 u0 = xor16(f0, mmx), u1 = xor16(f1, mmx);
+            h = window(u0, u1, FP);
+            dlen = len - FP;
+            const uint32_t cmd = get_byte(u0, 2);
+            fst = len < FP ? 1 : len > (int)wp ? 4 : (cmd & 0xE0u) != 0xA0u ? 3 : 0;
+            uint32_t pre = cmd + get_byte(u0, 3);  // frame bytes 2 .. FP - 1
+            if (FP == 12) {
+                pre = __builtin_amdgcn_sad_u8(u0.y, 0u, __builtin_amdgcn_sad_u8(u0.z, 0u, pre));
+                if (fr.conv_hid && fst == 0) {
+                    fr.conv_hid[2 * (g * N + lane)] = u0.y;
+                    fr.conv_hid[2 * (g * N + lane) + 1] = u0.z;
+                }
+            }
+            v_fs = pre | (get_byte(u0, 1) << 24);
+        } else {
+            h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
+        }
         const uint32_t tag = get_byte(h, 0);
         hdr = tag == 0xED ? 13 : 11;
         const uint32_t ikn = get_byte(h, 9) | (get_byte(h, 10) << 8);
-        okh = len >= 11 && len <= (int)wp && (tag == 0xEC || tag == 0xED) && len >= hdr &&
+        okh = fst == 0 && dlen >= 11 && dlen <= (int)wp && (tag == 0xEC || tag == 0xED) && dlen >= hdr &&
               (int)(ikn & 0xF) == N && (int)((ikn >> 4) & 0xF) == K && (int)((ikn >> 8) & 0xF) == lane &&
-              len - hdr <= pitch;
-        size = okh ? len - hdr : 0;
+              dlen - hdr <= pitch;
+        size = okh ? dlen - hdr : 0;
         stated = get_byte(h, 11) | (get_byte(h, 12) << 8);
+        if constexpr (FP != 0) v_fs += sum16(mask16(h, 0, hdr), 0);  // the datagram header's bytes
     }
     const uint32_t rowmask = (1u << N) - 1u, kmask = (1u << K) - 1u;
     const uint32_t good = (uint32_t)__ballot(okh) & rowmask;
@@ -1442,8 +1550,9 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
     const int P = pitch / A, rem = pitch % A;
     const bool fuse_tail = P > 0 && rem > 0 && rem <= 256;
     const int passes = P + ((rem > 0 && !fuse_tail) ? 1 : 0);
-    uint32_t bad = 0, verified = 0;
+    uint32_t bad = 0, verified = 0, fbad = 0;
     RxP<K, M> pl;
+    pl.v_mm = 0;
     uint32_t v_w0 = 0, v_dt = 0;  // lane c: survivor c's dword 0 / datagram total; K + j: decoded row j's
     for (int round = 0; round <= N; ++round) {
         // ---- plan: survivors = the lowest K good rows (or the good data rows if too few)
@@ -1462,8 +1571,9 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
                 const int r = __builtin_ctz(take);
                 take &= take - 1;
                 const int sz = __builtin_amdgcn_readlane((int)v_ss, r) & 0xFFFF;
-                pl.v_off = set_lane(pl.v_off, c, (uint32_t)((uint64_t)r * wp + (((summed >> r) & 1u) ? 13u : 11u)));
+                pl.v_off = set_lane(pl.v_off, c, (uint32_t)((uint64_t)r * wp + FP + (((summed >> r) & 1u) ? 13u : 11u)));
                 pl.v_rs = set_lane(pl.v_rs, c, (uint32_t)(r | (sz << 16)));
+                if constexpr (FP != 0) pl.v_mm = set_lane(pl.v_mm, c, lane_of(v_fx, r) * 0x01010101u);
                 pl.min_size = min(pl.min_size, sz);
                 pl.ns = c + 1;
                 pl.svmask |= 1u << r;
@@ -1480,7 +1590,8 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
             for (int j = 0; j < M; ++j)
                 if (j < pl.e) pl.v_rs = set_lane(pl.v_rs, K + M + j, records[rec + 4 + K + j]);
         }
-        uint32_t extra = good & summed & ~pl.svmask & ~verified & ~bad;  // rows only checksummed
+        // rows only checksummed (frames: every good row, for its frame checksum)
+        uint32_t extra = good & (FP ? rowmask : summed) & ~pl.svmask & ~verified & ~bad;
         pl.nx = 0;
         pl.min_xsize = pitch;
 #pragma unroll
@@ -1489,8 +1600,9 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
                 const int rr = __builtin_ctz(extra);
                 extra &= extra - 1;
                 const int sz = __builtin_amdgcn_readlane((int)v_ss, rr) & 0xFFFF;
-                pl.v_off = set_lane(pl.v_off, K + r, (uint32_t)((uint64_t)rr * wp + 13u));
+                pl.v_off = set_lane(pl.v_off, K + r, (uint32_t)((uint64_t)rr * wp + FP + (((summed >> rr) & 1u) ? 13u : 11u)));
                 pl.v_rs = set_lane(pl.v_rs, K + r, (uint32_t)(rr | (sz << 16)));
+                if constexpr (FP != 0) pl.v_mm = set_lane(pl.v_mm, K + r, lane_of(v_fx, rr) * 0x01010101u);
                 pl.min_xsize = min(pl.min_xsize, sz);
                 pl.nx = r + 1;
             }
@@ -1505,11 +1617,11 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
             const int base = A * q;
             if (fuse_tail && q == passes - 1) {
                 RxSl<NVA, 1> sl{base + 4 * NVA * lane, base + A, lane, true, pitch};
-                rx2_pass<K, M, NVA, 1>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, base + A, pitch, v_w0,
+                rx2_pass<K, M, NVA, 1, FP>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, base + A, pitch, v_w0,
                                               dsum, xsum, psl);
             } else {
                 RxSl<NVA, 0> sl{base + 4 * NVA * lane, 0, lane, base + 4 * NVA * lane < pitch, pitch};
-                rx2_pass<K, M, NVA, 0>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, min(pitch, base + A), 0,
+                rx2_pass<K, M, NVA, 0, FP>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, min(pitch, base + A), 0,
                                               v_w0, dsum, xsum, psl);
             }
         }
@@ -1521,10 +1633,22 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
             v_dt = set_lane(v_dt, c, t);
             if (c < pl.ns) {
                 const int r = (int)(lane_of(pl.v_rs, c) & 0xFFFF);
+                bool rb = false, rv = false;
                 if ((summed >> r) & 1u) {
-                    if ((t & 0xFFFFu) != (lane_of(v_ss, r) >> 16)) newbad |= 1u << r;
-                    else verified |= 1u << r;
+                    if ((t & 0xFFFFu) != (lane_of(v_ss, r) >> 16)) rb = true;
+                    else rv = true;
                 }
+                if constexpr (FP != 0) {  // ProtocolUdp::CheckSum over frame bytes 2.. (ProtocolBasic.cpp:80-87)
+                    const uint32_t fs = lane_of(v_fs, r), s = (fs & 0xFFFFFFu) + t;
+                    if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (fs >> 24)) {
+                        rb = true;
+                        fbad |= 1u << r;
+                    } else {
+                        rv = true;
+                    }
+                }
+                if (rb) newbad |= 1u << r;
+                else if (rv) verified |= 1u << r;
             }
         }
 #pragma unroll
@@ -1532,7 +1656,15 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
             const uint32_t t = wave_total(xsum[j]);
             if (j < pl.nx) {
                 const int r = (int)(lane_of(pl.v_rs, K + j) & 0xFFFF);
-                if ((t & 0xFFFFu) != (lane_of(v_ss, r) >> 16)) bad |= 1u << r;
+                bool rb = ((summed >> r) & 1u) && (t & 0xFFFFu) != (lane_of(v_ss, r) >> 16);
+                if constexpr (FP != 0) {
+                    const uint32_t fs = lane_of(v_fs, r), s = (fs & 0xFFFFFFu) + t;
+                    if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (fs >> 24)) {
+                        rb = true;
+                        fbad |= 1u << r;
+                    }
+                }
+                if (rb) bad |= 1u << r;
                 else verified |= 1u << r;
             }
         }
@@ -1544,6 +1676,7 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
         bad |= newbad;
     }
     if constexpr (LDSW) {  // the K data rows, staged whole, as one flat range
+        wave_lds_sync();
         const int total = K * pitch;
         for (int o = 16 * lane; o < total; o += 1024) st16(out_hbm + o, rx_stage[o >> 4]);
     }
@@ -1571,6 +1704,7 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
                     const int pos = p0 + 16 * lane;
                     if (pos < sz) {
                         uint4 v = ldu16(row + pos);
+                        if constexpr (FP != 0) v = xor16(v, lane_of(v_fx, r) * 0x01010101u);
                         v = mask16(v, head - pos, min(sz, head + p) - pos);
                         s = sum16(v, s);
                     }
@@ -1598,6 +1732,24 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
         st = -2;
         psz = 0;
     }
+    if constexpr (FP != 0) {
+        // frames the FEC header rejected were not read by the passes: their RecvPacket checksum,
+        // one row at a time over the wave (only malformed rows come here)
+        uint32_t chk = (uint32_t)__ballot(lane < N && fst == 0 && !okh) & rowmask;
+        while (chk) {
+            const int r = __builtin_ctz(chk);
+            chk &= chk - 1;
+            const int flen = __builtin_amdgcn_readlane(len, r);
+            const uint32_t mmr = lane_of(v_fx, r) * 0x01010101u;
+            const uint8_t* row = wire_g + (uint64_t)r * wp;
+            uint32_t s = 0;
+            for (int pos = 16 * lane; pos < flen; pos += 1024)
+                s = sum16(mask16(xor16(*reinterpret_cast<const uint4*>(row + pos), mmr), 2 - pos, flen - pos), s);
+            s = wave_total(s);
+            if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (lane_of(v_fs, r) >> 24)) fbad |= 1u << r;
+        }
+        if (fr.status && lane < N) fr.status[g * N + lane] = fst ? fst : ((fbad >> lane) & 1u) ? 2 : 0;
+    }
     if (lane < K) {
         a.status[g * K + lane] = st;
         a.psize[g * K + lane] = psz;
@@ -1613,9 +1765,6 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
 // so frame = [mask][c][cmd][proto]([conv LE][hid LE])[data], bytes 1.. XORed, with
 // CheckSum(x) = ~((s >> 16) + (s & 0xffff)), s = byte sum (ProtocolBasic.cpp:56-87).
 // One wave per row, 32 bytes per lane per pass; chunk 0 (which holds c) is written last.
-__device__ __forceinline__ uint4 xor16(uint4 v, uint32_t mm) {
-    return make_uint4(v.x ^ mm, v.y ^ mm, v.z ^ mm, v.w ^ mm);
-}
 
 __global__ void __launch_bounds__(256) k_frame_udp(FrameArgs a) {
     const uint64_t row = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -1627,9 +1776,12 @@ __global__ void __launch_bounds__(256) k_frame_udp(FrameArgs a) {
     const uint8_t* in = a.in + row * a.in_pitch;
     uint8_t* out = a.out + row * a.out_pitch;
     if (len < 0 || total > (int)a.out_pitch || len > (int)a.in_pitch) {
+        for (int o = 16 * lane; o < (int)a.out_pitch; o += 1024) st16a(out + o, make_uint4(0, 0, 0, 0));
         if (lane == 0) a.out_len[row] = -1;
         return;
     }
+    for (int o = 16 * ((total + 15) / 16) + 16 * lane; o < (int)a.out_pitch; o += 1024)  // zero padding
+        st16a(out + o, make_uint4(0, 0, 0, 0));
     const uint32_t m = a.mask[row];
     const uint32_t x = (m ^ a.gmask ^ 0x5Au) & 0xFFu;
     const uint32_t mm = x * 0x01010101u;
@@ -1702,6 +1854,7 @@ __global__ void __launch_bounds__(256) k_frame_udp_rows(FrameArgs a) {
     uint4* const region = STAGE ? rx_stage + (threadIdx.x >> 6) * (ROWS * a.out_pitch / 16) : nullptr;
     if constexpr (STAGE) {
         for (int o = lane; o < (int)(ROWS * a.out_pitch / 16); o += 64) region[o] = make_uint4(0, 0, 0, 0);
+        wave_lds_sync();
     }
     uint4 lo[ROWS][2], hi[ROWS][2];
 #pragma unroll
@@ -1721,11 +1874,16 @@ __global__ void __launch_bounds__(256) k_frame_udp_rows(FrameArgs a) {
     for (int i = 0; i < ROWS; ++i) {
         const uint64_t row = row0 + i;
         if (row >= a.rows) break;
-        if (!good[i]) {
+        uint8_t* out = STAGE ? reinterpret_cast<uint8_t*>(region) + i * a.out_pitch : a.out + row * a.out_pitch;
+        if (!good[i]) {  // a rejected row reads back zeros (staged: the zeroed region)
+            if (!STAGE) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (16 * (2 * lane + h) < (int)a.out_pitch) st16a(out + 16 * (2 * lane + h), make_uint4(0, 0, 0, 0));
+            }
             if (lane == 0) a.out_len[row] = -1;
             continue;
         }
-        uint8_t* out = STAGE ? reinterpret_cast<uint8_t*>(region) + i * a.out_pitch : a.out + row * a.out_pitch;
         const uint32_t m = a.mask[row];
         const uint32_t x = (m ^ a.gmask ^ 0x5Au) & 0xFFu;
         const uint32_t mm = x * 0x01010101u;
@@ -1734,7 +1892,10 @@ __global__ void __launch_bounds__(256) k_frame_udp_rows(FrameArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int q = 2 * lane + h;
-            if (16 * q >= total[i]) continue;
+            if (16 * q >= total[i]) {  // padding up to the pitch is zero (staged: already)
+                if (!STAGE && 16 * q < (int)a.out_pitch) st16a(out + 16 * q, make_uint4(0, 0, 0, 0));
+                continue;
+            }
             // frame bytes [16q, 16q + 16) = data bytes [16q - P, 16q + 16 - P)
             uint4 v = mask16(window(lo[i][h], hi[i][h], 16 - P), q == 0 ? P : 0, total[i] - 16 * q);
             sum = sum16(v, sum);
@@ -1765,6 +1926,7 @@ __global__ void __launch_bounds__(256) k_frame_udp_rows(FrameArgs a) {
         }
     }
     if constexpr (STAGE) {
+        wave_lds_sync();
         const uint64_t nrows = min((uint64_t)ROWS, a.rows - row0);
         uint8_t* dst = a.out + row0 * a.out_pitch;
         for (int o = 16 * lane; o < (int)(nrows * a.out_pitch); o += 1024) st16(dst + o, region[o >> 4]);
@@ -1952,10 +2114,10 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
             const dim3 grid((unsigned)((gn + 4 * gpw - 1) / (4 * gpw)));
             if (gpw == 1)
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 1>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
-                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn);
+                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
             else
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
-                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn);
+                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
         }
         return hipGetLastError();
     }
@@ -2014,6 +2176,57 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
 }
 #undef QFEC_PACK_CASE
 
+// qfec_pack_frames: datagrams and their ProtocolUdp frames in one pass (k_pack_wave64 with a
+// frame prefix) where the frame pitch is the 64-B multiple just above prefix + 13 + shard pitch
+// and a group fills a wave (1088 B) or half of one (576 B); *launched = false otherwise
+template <int K, int M>
+hipError_t pack_frames_shape(const WireArgs& a, const FrameSend& fs, int fp, const uint32_t* tab, hipStream_t s,
+                             bool* launched) {
+    const uint64_t fpitch = a.wire_pitch;
+    const int gpw = fpitch == 1088 ? 1 : fpitch == 576 ? 2 : 0;
+    if (!a.checksum || !gpw || !tuning().wire_send_wave || fpitch != (fp + 13 + a.pitch + 63) / 64 * 64) return hipSuccess;
+    *launched = true;
+    for (uint64_t g0 = 0; g0 < a.groups; g0 += ((uint64_t)1 << 28)) {
+        const uint64_t gn = std::min((uint64_t)1 << 28, a.groups - g0);
+        WireArgs b = a;
+        b.wire = a.wire + g0 * (uint64_t)(K + M) * fpitch;
+        b.wire_len = a.wire_len + g0 * (K + M);
+        FrameSend f = fs;
+        f.mask = fs.mask + g0 * (K + M);
+        if (fs.conv_hid) f.conv_hid = fs.conv_hid + 2 * g0 * (K + M);
+        const dim3 grid((unsigned)((gn + 4 * gpw - 1) / (4 * gpw)));
+#define QFEC_PF(GPW, FP)                                                                                          \
+    hipLaunchKernelGGL((k_pack_wave64<K, M, GPW, FP>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K, \
+                       a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, f)
+        if (gpw == 1 && fp == 4) QFEC_PF(1, 4);
+        else if (gpw == 1) QFEC_PF(1, 12);
+        else if (fp == 4) QFEC_PF(2, 4);
+        else QFEC_PF(2, 12);
+#undef QFEC_PF
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_frames(const WireArgs& a, const FrameSend& fs, int fp, const uint32_t* tab, hipStream_t s,
+                              bool* launched) {
+    *launched = false;
+    if (!a.groups) return hipSuccess;
+#define QFEC_PFC(KK, MM) \
+    if (a.k == KK && a.m == MM) return pack_frames_shape<KK, MM>(a, fs, fp, tab, s, launched);
+    QFEC_PFC(10, 3)
+    QFEC_PFC(4, 1)
+    QFEC_PFC(4, 2)
+    QFEC_PFC(2, 2)
+    QFEC_PFC(3, 1)
+    QFEC_PFC(3, 2)
+    QFEC_PFC(5, 1)
+    QFEC_PFC(5, 3)
+    QFEC_PFC(7, 1)
+    QFEC_PFC(8, 4)
+#undef QFEC_PFC
+    return hipSuccess;
+}
+
 #define QFEC_UNPACK_CASE(KK, MM)                                                                        \
     if (a.k == KK && a.m == MM) {                                                                       \
         *launched = true;                                                                               \
@@ -2028,10 +2241,11 @@ hipError_t launch_pack_fused(const WireArgs& a, const uint32_t* tab, uint32_t* p
         return hipGetLastError();                                                                       \
     }
 
-// the lean single-wave receive for one (K, M): 16-B lanes (NVA 4) or 8-B lanes (NVA 2)
-template <int K, int M>
-hipError_t unpack_v2_shape(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
-                           hipStream_t s, int nva) {
+// the lean single-wave receive for one (K, M): 16-B lanes (NVA 4) or 8-B lanes (NVA 2); fp 4 / 12
+// reads ProtocolUdp frames (qfec_unpack_frames)
+template <int K, int M, int FP>
+hipError_t unpack_v2_launch(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
+                            hipStream_t s, int nva, const FrameRecv& fr) {
     const dim3 grid((unsigned)((a.groups + 3) / 4)), block(256);
     // the K rows staged in LDS and stored flat (tuning "wire_rx_lds"): 1 where the staging leaves
     // at least 3/4 of the waves per CU the registers allow (16 on 16-B lanes, 24 on 8-B lanes;
@@ -2040,22 +2254,32 @@ hipError_t unpack_v2_shape(const WireArgs& a, const int32_t* lut, const uint32_t
     const size_t stage = (size_t)K * a.pitch;
     const int lds = tuning().wire_rx_lds;
     const size_t lds_waves = stage ? (size_t)(160 * 1024) / stage : 0, reg_waves = nva == 4 ? 16 : 24;
+    const uint8_t* w = a.wire;
+    const int32_t* wl = a.wire_len;
     if (stage <= 16384 && (lds == 2 || (lds == 1 && 4 * lds_waves >= 3 * reg_waves))) {
         if (nva == 4)
-            hipLaunchKernelGGL((k_unpack_v2<K, M, 4, true>), dim3((unsigned)a.groups), dim3(64), stage, s, a,
-                               (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+            hipLaunchKernelGGL((k_unpack_v2<K, M, 4, true, FP>), dim3((unsigned)a.groups), dim3(64), stage, s, a, w, wl,
+                               lut, records, rec_hdr, a.shards, fr);
         else
-            hipLaunchKernelGGL((k_unpack_v2<K, M, 2, true>), dim3((unsigned)a.groups), dim3(64), stage, s, a,
-                               (const uint8_t*)a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+            hipLaunchKernelGGL((k_unpack_v2<K, M, 2, true, FP>), dim3((unsigned)a.groups), dim3(64), stage, s, a, w, wl,
+                               lut, records, rec_hdr, a.shards, fr);
         return hipGetLastError();
     }
     if (nva == 4)
-        hipLaunchKernelGGL((k_unpack_v2<K, M, 4>), grid, block, 0, s, a, (const uint8_t*)a.wire,
-                           (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+        hipLaunchKernelGGL((k_unpack_v2<K, M, 4, false, FP>), grid, block, 0, s, a, w, wl, lut, records, rec_hdr,
+                           a.shards, fr);
     else
-        hipLaunchKernelGGL((k_unpack_v2<K, M, 2>), grid, block, 0, s, a, (const uint8_t*)a.wire,
-                           (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);
+        hipLaunchKernelGGL((k_unpack_v2<K, M, 2, false, FP>), grid, block, 0, s, a, w, wl, lut, records, rec_hdr,
+                           a.shards, fr);
     return hipGetLastError();
+}
+
+template <int K, int M>
+hipError_t unpack_v2_shape(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
+                           hipStream_t s, int nva, int fp = 0, const FrameRecv& fr = FrameRecv{}) {
+    if (fp == 4) return unpack_v2_launch<K, M, 4>(a, lut, records, rec_hdr, s, nva, fr);
+    if (fp == 12) return unpack_v2_launch<K, M, 12>(a, lut, records, rec_hdr, s, nva, fr);
+    return unpack_v2_launch<K, M, 0>(a, lut, records, rec_hdr, s, nva, fr);
 }
 
 hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
@@ -2082,6 +2306,46 @@ hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint
     return hipSuccess;
 }
 #undef QFEC_UNPACK_CASE
+
+// qfec_unpack_frames: unframe + unpack in one pass (k_unpack_v2 with a frame prefix) for the
+// templated shapes; *launched = false otherwise
+hipError_t launch_unpack_frames(const WireArgs& a, const FrameRecv& fr, int fp, const int32_t* lut,
+                                const uint32_t* records, uint32_t rec_hdr, hipStream_t s, bool* launched) {
+    *launched = false;
+    if (!a.groups) return hipSuccess;
+    const int rx = tuning().wire_rx_split;
+    const int nva = rx == 2 ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
+#define QFEC_UFC(KK, MM)                                                               \
+    if (a.k == KK && a.m == MM) {                                                      \
+        *launched = true;                                                              \
+        return unpack_v2_shape<KK, MM>(a, lut, records, rec_hdr, s, nva, fp, fr);     \
+    }
+    QFEC_UFC(10, 3)
+    QFEC_UFC(4, 1)
+    QFEC_UFC(4, 2)
+    QFEC_UFC(2, 2)
+    QFEC_UFC(3, 1)
+    QFEC_UFC(3, 2)
+    QFEC_UFC(5, 1)
+    QFEC_UFC(5, 3)
+    QFEC_UFC(7, 1)
+    QFEC_UFC(8, 4)
+#undef QFEC_UFC
+    return hipSuccess;
+}
+
+// rows whose RecvPacket verdict is not 0 are not received (the fallback of qfec_unpack_frames)
+__global__ void __launch_bounds__(256) k_len_by_status(int32_t* __restrict__ len, const int32_t* __restrict__ status,
+                                                       uint64_t rows) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i < rows && status[i] != 0) len[i] = 0;
+}
+
+hipError_t launch_len_by_status(int32_t* len, const int32_t* status, uint64_t rows, hipStream_t s) {
+    if (!rows) return hipSuccess;
+    hipLaunchKernelGGL(k_len_by_status, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, len, status, rows);
+    return hipGetLastError();
+}
 
 hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s) {
     if (!a.rows) return hipSuccess;

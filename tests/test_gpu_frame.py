@@ -52,9 +52,11 @@ def test_frame_vs_oracle(oracle, session, pitch, op64, rows_per_wave):
         ref = oracle.frame_udp(rows[r, :lens[r]], masks[r], gmask=gmask, conv_hid=ch[r] if session else None)
         if P + lens[r] > out.shape[1]:
             assert out_len[r] == -1
+            assert not out[r].any(), r  # a rejected row is all zero (include/qfec.h)
             continue
         assert out_len[r] == len(ref), r
         assert np.array_equal(out[r, :len(ref)], ref), r
+        assert not out[r, len(ref):].any(), r  # zero up to the pitch
 
 
 @pytest.fixture(params=[2, 1, 4], ids=["rows2", "rows1", "rows4"])
