@@ -93,6 +93,12 @@ __device__ __forceinline__ uint4 xor16(uint4 v, uint32_t mm) {
     return make_uint4(v.x ^ mm, v.y ^ mm, v.z ^ mm, v.w ^ mm);
 }
 
+// XOR with mm only the chunk's bytes below n: a frame's padding stays zero
+__device__ __forceinline__ uint4 xor16n(uint4 v, uint32_t mm, int n) {
+    return make_uint4(v.x ^ (mm & byte_mask(0, n, 0)), v.y ^ (mm & byte_mask(0, n, 1)), v.z ^ (mm & byte_mask(0, n, 2)),
+                      v.w ^ (mm & byte_mask(0, n, 3)));
+}
+
 // datagram store: non-temporal or write-back (tuning "wire_store_nt"), wave-uniform flag
 __device__ __forceinline__ void stw(uint8_t* p, const uint4& v, int nt) {
     if (nt) st16(p, v);
@@ -1801,7 +1807,7 @@ __global__ void __launch_bounds__(256) k_frame_udp(FrameArgs a) {
             if (q == 0) {
                 first = v;
             } else {
-                st16a(out + 16 * q, xor16(v, mm));
+                st16a(out + 16 * q, xor16n(v, mm, total - 16 * q));
             }
         }
     }
@@ -1822,7 +1828,7 @@ __global__ void __launch_bounds__(256) k_frame_udp(FrameArgs a) {
         }
         const uint32_t c = ~((s2 >> 16) + (s2 & 0xFFFFu)) & 0xFFu;
         put_byte(first, 1, c);
-        first = xor16(first, mm);
+        first = xor16n(first, mm, total);
         put_byte(first, 0, m);
         st16a(out, first);
         a.out_len[row] = total;
@@ -1900,7 +1906,7 @@ __global__ void __launch_bounds__(256) k_frame_udp_rows(FrameArgs a) {
             uint4 v = mask16(window(lo[i][h], hi[i][h], 16 - P), q == 0 ? P : 0, total[i] - 16 * q);
             sum = sum16(v, sum);
             if (q == 0) first = v;
-            else st16a(out + 16 * q, xor16(v, mm));
+            else st16a(out + 16 * q, xor16n(v, mm, total[i] - 16 * q));
         }
         sum = wave_sum(sum);
         if (lane == 0) {
@@ -1919,7 +1925,7 @@ __global__ void __launch_bounds__(256) k_frame_udp_rows(FrameArgs a) {
             }
             const uint32_t c = ~((s2 >> 16) + (s2 & 0xFFFFu)) & 0xFFu;
             put_byte(first, 1, c);
-            first = xor16(first, mm);
+            first = xor16n(first, mm, total[i]);
             put_byte(first, 0, m);
             st16a(out, first);
             a.out_len[row] = total[i];
