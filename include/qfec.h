@@ -208,6 +208,17 @@ int qfec_unpack_frames(qfec_code *code, const unsigned char *d_frames, long long
                        int *d_rx_size, int *d_status, int *d_psize, int *d_frame_status,
                        unsigned int *d_conv_hid, void *stream);
 
+/* Gather scattered rows (e.g. datagrams where a receive ring put them) into the pitched batch the
+ * calls above take: row r of d_out = the d_len[r] bytes at d_base + d_off[r], zero-padded to
+ * out_pitch, d_out_len[r] = d_len[r]; rows with d_len <= 0 get 0 and are not written, rows that
+ * do not fit get -1.  wrap_n > 0: the rows are bare shards (row r = shard ik = r % wrap_n of a
+ * group) and each gets the 11-byte header a 0xEC datagram of it carries ([0xEC][sent 0][src 0]
+ * [wrap_n | wrap_k << 4 | ik << 8]), so qfec_unpack_datagrams decodes groups of chosen shards
+ * (fec_decode_pkts, network/FecCodecBuf.cpp:181-232).  Sources stay readable 16 bytes past
+ * their last byte. */
+int qfec_gather_rows(const unsigned char *d_base, const unsigned long long *d_off, const int *d_len, long long rows,
+                     int wrap_n, int wrap_k, unsigned char *d_out, long long out_pitch, int *d_out_len, void *stream);
+
 /* Fill nbytes of device memory with the synthetic stream of quicknet_amd/synth.py. */
 int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long seed, void *stream);
 

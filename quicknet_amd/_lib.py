@@ -19,7 +19,7 @@ EXPORTS = {
                "qfec_encode", "qfec_encode_host", "qfec_reconstruct", "qfec_reconstruct_host", "qfec_prepare_reconstruct", "qfec_decode_rows",
                "qfec_pipe_new", "qfec_pipe_free", "qfec_pipe_encode", "qfec_pipe_reconstruct", "qfec_pipe_wait", "qfec_pipe_slots",
                "qfec_fec_code", "qfec_rs_code", "qfec_fec_matrix", "qfec_pack_datagrams", "qfec_unpack_datagrams",
-               "qfec_frame_udp", "qfec_unframe_udp", "qfec_pack_frames", "qfec_unpack_frames", "qfec_synth_fill", "qfec_probe_stream",
+               "qfec_frame_udp", "qfec_unframe_udp", "qfec_pack_frames", "qfec_unpack_frames", "qfec_gather_rows", "qfec_synth_fill", "qfec_probe_stream",
                "qfec_tune", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
                "qfec_last_error", "qfec_version"],
     "qfec_net.h": ["qfec_net_new", "qfec_net_free", "qfec_net_session", "qfec_net_enable", "qfec_net_pack_input", "qfec_net_flush_pack",
@@ -86,6 +86,7 @@ def lib():
         "qfec_frame_udp": (i, [vp, ll, vp, ll, vp, vp, i, i, i, vp, ll, vp, vp]),
         "qfec_pack_frames": (i, [vp, vp, vp, vp, vp, ll, i, vp, ll, vp, vp, i, i, i, vp, ll, vp, vp]),
         "qfec_unpack_frames": (i, [vp, vp, ll, vp, ll, i, i, i, i, vp, ll, vp, vp, vp, vp, vp, vp, vp]),
+        "qfec_gather_rows": (i, [vp, vp, vp, ll, i, i, vp, ll, vp, vp]),
         "qfec_net_new": (vp, [i, i, i, i]),
         "qfec_net_free": (None, [vp]),
         "qfec_net_session": (i, [vp, vp]),

@@ -129,6 +129,8 @@ hipError_t launch_pack_frames(const WireArgs& a, const FrameSend& fs, int fp, co
 hipError_t launch_unpack_frames(const WireArgs& a, const FrameRecv& fr, int fp, const int32_t* lut,
                                 const uint32_t* records, uint32_t rec_hdr, hipStream_t s, bool* launched);
 hipError_t launch_len_by_status(int32_t* len, const int32_t* status, uint64_t rows, hipStream_t s);
+hipError_t launch_gather_rows(const uint8_t* base, const uint64_t* off, const int32_t* len, uint64_t rows, int wrap_n,
+                              int wrap_k, uint8_t* out, uint64_t out_pitch, int32_t* out_len, hipStream_t s);
 // fused receive for templated (k, m); *launched = false when the shape has no instance
 hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
                                hipStream_t s, bool* launched);

@@ -1561,6 +1561,22 @@ int qfec_unpack_frames(qfec_code* code, const unsigned char* d_frames, long long
     return rc;
 }
 
+int qfec_gather_rows(const unsigned char* d_base, const unsigned long long* d_off, const int* d_len, long long rows,
+                     int wrap_n, int wrap_k, unsigned char* d_out, long long out_pitch, int* d_out_len, void* stream) {
+    if (rows < 0 || (rows && (!d_base || !d_off || !d_len || !d_out || !d_out_len)) || out_pitch < 16 || out_pitch % 16 ||
+        (uintptr_t)d_out % 16 || wrap_n < 0 || wrap_n > 15 || (wrap_n && (wrap_k < 1 || wrap_k >= wrap_n))) {
+        set_error("gather_rows: out_pitch a multiple of 16, 16-B aligned output, 0 < wrap_k < wrap_n <= 15");
+        return QFEC_EINVAL;
+    }
+    if (rows == 0) return QFEC_OK;
+    DevCtx* ctx = nullptr;
+    const int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    const hipError_t e = launch_gather_rows(d_base, (const uint64_t*)d_off, d_len, (uint64_t)rows, wrap_n, wrap_k, d_out,
+                                            (uint64_t)out_pitch, d_out_len, (hipStream_t)stream);
+    return e == hipSuccess ? QFEC_OK : hip_fail(e, "gather_rows launch");
+}
+
 int qfec_frame_udp(const unsigned char* d_in, long long in_pitch, const int* d_len, long long rows,
                    const unsigned char* d_mask, const unsigned int* d_conv_hid, int gmask, int cmd, int protocol,
                    unsigned char* d_out, long long out_pitch, int* d_out_len, void* stream) {

@@ -2340,6 +2340,49 @@ hipError_t launch_unpack_frames(const WireArgs& a, const FrameRecv& fr, int fp, 
     return hipSuccess;
 }
 
+// qfec_gather_rows: scattered rows (datagrams in a receive ring, or bare shards with an 11-byte
+// 0xEC header synthesized in front when wrap_n > 0) into the pitched batch the datagram calls
+// take.  One wave per row, 16-B chunks per lane, zero padding to the pitch; rows of len <= 0
+// get out_len 0 and are not written.
+__global__ void __launch_bounds__(256) k_gather_rows(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                     const int32_t* __restrict__ len, uint64_t rows, int wrap_n, int wrap_k,
+                                                     uint8_t* __restrict__ out, uint64_t out_pitch,
+                                                     int32_t* __restrict__ out_len) {
+    const uint64_t row = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const int n = len[row];
+    const int H = wrap_n > 0 ? 11 : 0;
+    if (n <= 0 || H + n > (int)out_pitch) {
+        if (lane == 0) out_len[row] = n <= 0 ? 0 : -1;
+        return;
+    }
+    const uint8_t* src = base + off[row];
+    uint8_t* dst = out + row * out_pitch;
+    for (int q = lane; 16 * q < (int)out_pitch; q += 64) {
+        uint4 v;
+        if (H && q == 0) {  // [0xEC][sent 0][src 0][n | k << 4 | ik << 8] + the shard's first 5 bytes
+            v = window(make_uint4(0, 0, 0, 0), ldu16(src), 16 - H);
+            const uint32_t ikn = (uint32_t)wrap_n | (uint32_t)wrap_k << 4 | (uint32_t)(row % (uint64_t)wrap_n) << 8;
+            v.x = 0xECu;
+            v.y = 0;
+            v.z = (v.z & 0xFF000000u) | ((ikn & 0xFFFFu) << 8);
+        } else {
+            v = 16 * q - H < n ? ldu16(src + 16 * q - H) : make_uint4(0, 0, 0, 0);
+        }
+        st16a(dst + 16 * q, mask16(v, 0, H + n - 16 * q));
+    }
+    if (lane == 0) out_len[row] = H + n;
+}
+
+hipError_t launch_gather_rows(const uint8_t* base, const uint64_t* off, const int32_t* len, uint64_t rows, int wrap_n,
+                              int wrap_k, uint8_t* out, uint64_t out_pitch, int32_t* out_len, hipStream_t s) {
+    if (!rows) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_rows, dim3(waves_grid(rows)), dim3(256), 0, s, base, off, len, rows, wrap_n, wrap_k, out,
+                       out_pitch, out_len);
+    return hipGetLastError();
+}
+
 // rows whose RecvPacket verdict is not 0 are not received (the fallback of qfec_unpack_frames)
 __global__ void __launch_bounds__(256) k_len_by_status(int32_t* __restrict__ len, const int32_t* __restrict__ status,
                                                        uint64_t rows) {

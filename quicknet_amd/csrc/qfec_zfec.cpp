@@ -4,8 +4,9 @@
 // the receive window, expected indices, used flags, codec lists); every byte of work is done
 // by device launches over all sessions' packets of a flush:
 //   send      qfec_pack_datagrams  (shards, payload checksums, headers, datagram checksums,
-//                                   check packets), one launch per (k, n)
-//   receive   qfec_unpack_datagrams, two uses:
+//                                   check packets), one launch per (k, n), the payloads read
+//                                   where the input calls put them
+//   receive   qfec_gather_rows + qfec_unpack_datagrams, two uses:
 //             verdicts  the flush's datagrams placed by ik into pseudo-groups: header and
 //                       shard checksum (unpack_fec_head, FecCodecBuf.cpp:334-411) and, for
 //                       source packets, dec_src_pkt_info (:107-133)
@@ -16,11 +17,14 @@
 // :437), so the receive machine is replayed from the flush's starting state until every decode
 // it calls for has a device result (one replay when no decoded packet fails its checksum).
 //
-// Bytes are never copied on the host beyond what the device needs: datagrams, shards and
-// payloads are views into the queued datagrams (reference-counted, so window slots can hold
-// them across flushes), the device's inputs and outputs go through persistent pinned arenas
-// with one copy each way per launch, and a verdict launch returns only the per-row verdicts
-// (a received source packet's payload is the datagram's own bytes).
+// Memory: every queued payload and datagram is copied once, at its input call, into a pinned
+// arena (one per direction).  A flush mirrors the arenas to the device in one copy each, the
+// kernels read rows where they lie (payload offsets; gathered datagram rows), and every host
+// structure refers to bytes by arena offset (plain values, no per-packet allocation).  At the
+// end of a flush the bytes something still refers to -- the window slots' datagrams, the open
+// send groups' payloads -- move to the other arena of the pair, and the rest is dropped.
+// Sessions' send and receive machines run on several threads; the callbacks run in session
+// order, op order, on the flushing thread.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -48,11 +52,11 @@ inline uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] 
 inline int packed_size(int size) { return size < 0 ? 0 : size + 4 + 12 + 4; }  // getPackedPktSize, FecCodecBuf.cpp:16-25
 inline int cmod(int a, int b) { return a % b; }                                   // C's % (truncating), as in :277
 
-using Buf = std::shared_ptr<const std::vector<uint8_t>>;
-struct View {  // bytes [off, off + len) of a shared buffer
-    Buf b;
+// where a View's bytes live
+enum Src : uint8_t { SRC_NONE = 0, SRC_RX, SRC_TX, SRC_DEC, SRC_OWN };
+struct View {  // bytes [off, off + len) of one of the flush's buffers
+    uint8_t src = SRC_NONE;
     uint32_t off = 0, len = 0;
-    const uint8_t* p() const { return b ? b->data() + off : nullptr; }
 };
 
 // ---- FecCodecList: std::map<float 1 - k/n, FecCodec*> (FecCodec.cpp:18-95)
@@ -101,10 +105,11 @@ struct CodecList {
     }
 };
 
-// ---- one dec_pkts_buf entry (FecPacket.h).  Its FecBuf is the received shard (a view): the
-// decode reads its BufSize bytes, zero-padded (set_fec_dec_buf, FecCodecBuf.cpp:171-172), and
+// ---- one dec_pkts_buf entry (FecPacket.h).  Its FecBuf is the received shard: the decode
+// reads its BufSize bytes, zero-padded (set_fec_dec_buf, FecCodecBuf.cpp:171-172), and
 // flush_avail_pkts delivers the payload dec_src_pkt_info found in it when it was received
-// (only source packets that passed are stored, NetFecCodec.cpp:240-245; dec_pkt_size only grows)
+// (only source packets that passed are stored, NetFecCodec.cpp:240-245; dec_pkt_size only grows).
+// shard and payload lie inside the datagram [dg_off, dg_off + dg_len) of the receive arena.
 struct Slot {
     int64_t iPacket = -1;
     int BufSize = 0;
@@ -114,15 +119,18 @@ struct Slot {
     bool bUsed = false;
     uint64_t uid = 0;  // which received datagram filled it (decode cache key)
     int ik = 0;        // the ik it was received with
+    uint32_t dg_off = 0, dg_len = 0;
     View shard, payload;
-    void set_packet(const View& sh, uint64_t id, int row, const View& pay) {  // SetPacket (FecPacket.h:78-98)
-        shard = sh;
+    void set_packet(const View& sh, uint64_t id, int row, const View& pay, uint32_t doff, uint32_t dlen) {
+        shard = sh;  // SetPacket (FecPacket.h:78-98)
         BufSize = (int)sh.len;
         bValid = true;
         bUsed = false;
         uid = id;
         ik = row;
         payload = pay;
+        dg_off = doff;
+        dg_len = dlen;
     }
     void reset() {  // Reset (:99-122)
         iPacket = -1;
@@ -145,10 +153,10 @@ struct RxState {
     CodecList codecs;                    // the receive side's view of the session's list
 };
 
-enum OpType { OP_PACK, OP_UNPACK, OP_SETKN, OP_ENABLE, OP_SORTED, OP_DYNKN, OP_LOST };
+enum OpType : uint8_t { OP_PACK, OP_UNPACK, OP_SETKN, OP_ENABLE, OP_SORTED, OP_DYNKN, OP_LOST };
 struct Op {
     OpType t;
-    Buf data;  // OP_PACK payload / OP_UNPACK datagram
+    uint32_t off = 0, size = 0;  // OP_PACK payload (send arena) / OP_UNPACK datagram (receive arena)
     int a = 0, b = 0, c = 0;
     float f = 0;
     uint64_t uid = 0;  // OP_UNPACK: the datagram's id (decode cache keys)
@@ -165,7 +173,7 @@ struct TxState {
     // the open group: (k, n) it started with, first indices, payloads so far, rows emitted
     int gk = 0, gn = 0;
     uint32_t g_sent0 = 0, g_src0 = 0;
-    std::vector<Buf> g_pay;
+    std::vector<View> g_pay;  // send-arena views
     int g_emitted = 0;
 };
 
@@ -179,55 +187,87 @@ struct Session {
 
 // an output of one op, filled in after the device work
 struct Emit {
-    int kind = 0;  // 0 datagram of a send batch, 1 owned bytes, 2 delivery (view + src),
-                   // 3 delivery of a decoded row whose result is pending (batch = request, row)
+    uint32_t op = 0;  // the op it belongs to (callbacks run in op order)
+    uint8_t kind = 0;  // 0 datagram of a send batch (batch, group, row), 1 owned bytes (v),
+                       // 2 delivery (v + src), 3 delivery of a decoded row whose result is
+                       // pending (batch = request, row)
     int batch = -1, row = 0;
     long long group = 0;
     View v;
     uint32_t src = 0;
 };
 
-// persistent pinned host + device memory, grow-only, re-made when the current device changes
-struct Arena {
+// pinned host memory, grow-only; offsets stay valid when it grows.  Without a device (FEC-off
+// sessions need none) it is ordinary memory.
+struct HostArena {
     uint8_t* h = nullptr;
+    size_t cap = 0, used = 0;
+    bool pinned = false;
+    void release() {
+        if (h) {
+            if (pinned) (void)hipHostFree(h);
+            else free(h);
+        }
+        h = nullptr;
+        cap = used = 0;
+    }
+    bool reserve(size_t need) {
+        if (need <= cap) return true;
+        size_t ncap = std::max(need + (need >> 1), (size_t)4 << 20);
+        uint8_t* nh = nullptr;
+        bool pin = true;
+        if (hipHostMalloc(reinterpret_cast<void**>(&nh), ncap, hipHostMallocDefault) != hipSuccess || !nh) {
+            (void)hipGetLastError();
+            pin = false;
+            nh = static_cast<uint8_t*>(malloc(ncap));
+            if (!nh) return false;
+        }
+        if (used) memcpy(nh, h, used);
+        const size_t u = used;
+        release();
+        h = nh;
+        cap = ncap;
+        used = u;
+        pinned = pin;
+        return true;
+    }
+    // n bytes at a 16-B aligned offset, 16 readable bytes after them (the kernels' loads)
+    bool append(const void* p, size_t n, uint32_t* off) {
+        const size_t o = round16(used);
+        if (o + n + 16 > (size_t)UINT32_MAX || !reserve(o + n + 16)) return false;
+        if (n) memcpy(h + o, p, n);
+        memset(h + o + n, 0, 16);
+        used = o + n;
+        *off = (uint32_t)o;
+        return true;
+    }
+};
+
+// device memory, grow-only, re-made when the current device changes
+struct DevBuf {
     uint8_t* d = nullptr;
-    size_t hcap = 0, dcap = 0;
+    size_t cap = 0;
     int dev = -1;
     void release() {
-        if (h) (void)hipHostFree(h);
         if (d) (void)hipFree(d);
-        h = d = nullptr;
-        hcap = dcap = 0;
+        d = nullptr;
+        cap = 0;
     }
-    int ensure(size_t hbytes, size_t dbytes) {
+    int ensure(size_t bytes) {
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess) return QFEC_ENODEV;
         if (cur != dev) release();
         dev = cur;
-        if (hbytes > hcap) {
-            if (h) (void)hipHostFree(h);
-            h = nullptr;
-            hcap = 0;
-            const size_t cap = round16(hbytes + (hbytes >> 2) + 4096);
-            if (hipHostMalloc(reinterpret_cast<void**>(&h), cap, hipHostMallocDefault) != hipSuccess) {
-                fprintf(stderr, "[qfec] qfec_zfec_flush: hipHostMalloc(%zu) failed\n", cap);
-                h = nullptr;
-                return QFEC_ENOMEM;
-            }
-            hcap = cap;
-        }
-        if (dbytes > dcap) {
-            if (d) (void)hipFree(d);
+        if (bytes <= cap) return QFEC_OK;
+        release();
+        dev = cur;
+        const size_t ncap = round16(bytes + (bytes >> 2) + 4096);
+        if (hipMalloc(reinterpret_cast<void**>(&d), ncap) != hipSuccess) {
+            fprintf(stderr, "[qfec] qfec_zfec_flush: hipMalloc(%zu) failed\n", ncap);
             d = nullptr;
-            dcap = 0;
-            const size_t cap = round16(dbytes + (dbytes >> 2) + 4096);
-            if (hipMalloc(reinterpret_cast<void**>(&d), cap) != hipSuccess) {
-                fprintf(stderr, "[qfec] qfec_zfec_flush: hipMalloc(%zu) failed\n", cap);
-                d = nullptr;
-                return QFEC_ENOMEM;
-            }
-            dcap = cap;
+            return QFEC_ENOMEM;
         }
+        cap = ncap;
         return QFEC_OK;
     }
 };
@@ -239,7 +279,10 @@ struct qfec_zfec {
     std::vector<Session> sessions;
     std::map<std::pair<int, int>, qfec_code*> codes;  // (k, n) -> fec_new(k, n) matrix on the device
     uint64_t next_uid = 1;
-    Arena pack_arena, rx_arena, dec_arena;
+    HostArena rx[2], tx[2];  // queued datagrams / payloads (+ what the state holds), and their spares
+    int rxc = 0, txc = 0;
+    HostArena io;            // per-flush pinned staging: tables in, results and datagrams out
+    DevBuf d_rx, d_tx, d_io, d_work;
 };
 
 namespace {
@@ -250,102 +293,79 @@ qfec_code* code_for(qfec_zfec* z, int k, int n) {
     return c;
 }
 
+// the flush's byte sources, resolved by View::src
+struct Bufs {
+    const uint8_t* rx = nullptr;
+    const uint8_t* tx = nullptr;
+    const uint8_t* dec = nullptr;
+    const std::vector<std::vector<uint8_t>>* own = nullptr;  // per session
+    const uint8_t* p(const View& v, size_t session) const {
+        switch (v.src) {
+            case SRC_RX: return rx + v.off;
+            case SRC_TX: return tx + v.off;
+            case SRC_DEC: return dec + v.off;
+            case SRC_OWN: return (*own)[session].data() + v.off;
+            default: return nullptr;
+        }
+    }
+};
+
+// run f(i) for i < count on up to `threads` threads
+template <class F>
+void parallel_for(size_t count, unsigned threads, F&& f) {
+    if (threads <= 1 || count <= 1) {
+        for (size_t i = 0; i < count; ++i) f(i);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < threads; ++t)
+        th.emplace_back([&]() {
+            for (size_t i; (i = next.fetch_add(1)) < count;) f(i);
+        });
+    for (auto& x : th) x.join();
+}
+
+// staging bump allocator over the pinned io arena and its device twin (same offsets)
+struct Stage {
+    size_t o = 0;
+    size_t take(size_t n) {
+        const size_t r = o;
+        o = round16(o + n);
+        return r;
+    }
+};
+
 // ---------------------------------------------------------------- device batches
 // send: complete or partial groups of one (k, n); payloads of missing rows are empty
 struct PackGroup {
     uint32_t sent0, src0;
-    std::vector<Buf> pay;  // k entries (null = not yet given)
+    View pay[15];  // k entries (len 0 + SRC_NONE = not yet given)
 };
 struct PackBatch {
     int k, n;
     std::vector<PackGroup> groups;
-    // layout in the pack arena (host and device alike; shards device-only, last)
-    size_t base = 0, total = 0, sp = 0, wp = 0;
-    size_t o_offs = 0, o_sizes = 0, o_seq = 0, o_wlen = 0, o_wire = 0, o_end = 0, o_shards = 0;
-    const uint8_t* wire = nullptr;  // results, in the pinned arena
-    const int* wlen = nullptr;
+    size_t sp = 0, wp = 0;
+    size_t o_offs = 0, o_sizes = 0, o_seq = 0, o_wlen = 0, o_wire = 0, d_shards = 0;  // results: io arena
 };
 
-void pack_layout(PackBatch& b, size_t base) {
-    const size_t G = b.groups.size();
-    size_t maxp = 1, total = 0;
-    for (auto& g : b.groups)
-        for (auto& p : g.pay)
-            if (p) {
-                maxp = std::max(maxp, p->size());
-                total += p->size();
-            }
-    b.total = total;
-    b.sp = round16(maxp + 4);
-    b.wp = (b.sp + 13 + 63) & ~(size_t)63;  // the 64-B multiple: the fused send writes whole lines
-    b.base = base;
-    size_t o = base + round16(total + 16);  // payload (16 readable bytes past the last)
-    b.o_offs = o;
-    o += round16(G * b.k * 8);
-    b.o_sizes = o;
-    o += round16(G * b.k * 4);
-    b.o_seq = o;
-    o += round16(G * 8);
-    b.o_wlen = o;
-    o += round16(G * b.n * 4);
-    b.o_wire = o;
-    o += G * b.n * b.wp;
-    b.o_end = o;
-    b.o_shards = o;  // device only
-}
-
-int run_pack(qfec_zfec* z, PackBatch& b, hipStream_t s) {
-    const size_t G = b.groups.size();
-    Arena& A = z->pack_arena;
-    uint8_t* h = A.h;
-    long long* offs = reinterpret_cast<long long*>(h + b.o_offs);
-    int* sizes = reinterpret_cast<int*>(h + b.o_sizes);
-    uint32_t* seq = reinterpret_cast<uint32_t*>(h + b.o_seq);
-    size_t o = 0;
-    for (size_t g = 0; g < G; ++g) {
-        seq[2 * g] = b.groups[g].sent0;
-        seq[2 * g + 1] = b.groups[g].src0;
-        for (int i = 0; i < b.k; ++i) {
-            const Buf& p = b.groups[g].pay[(size_t)i];
-            offs[g * b.k + i] = (long long)o;
-            sizes[g * b.k + i] = p ? (int)p->size() : 0;
-            if (p && !p->empty()) memcpy(h + b.base + o, p->data(), p->size());
-            o += p ? p->size() : 0;
-        }
-    }
-    memset(h + b.base + o, 0, 16);
-    if (hipMemcpyAsync(A.d + b.base, h + b.base, b.o_wlen - b.base, hipMemcpyHostToDevice, s) != hipSuccess)
-        return QFEC_EHIP;
-    uint8_t* d = A.d;
-    int rc = qfec_pack_datagrams(code_for(z, b.k, b.n), d + b.base, reinterpret_cast<const long long*>(d + b.o_offs),
-                                 reinterpret_cast<const int*>(d + b.o_sizes),
-                                 reinterpret_cast<const unsigned int*>(d + b.o_seq), (long long)G, 1 /* is_send_checksum */,
-                                 d + b.o_shards, (long long)b.sp, d + b.o_wire, (long long)b.wp,
-                                 reinterpret_cast<int*>(d + b.o_wlen), s);
-    if (rc) return rc;
-    if (hipMemcpyAsync(h + b.o_wlen, d + b.o_wlen, b.o_end - b.o_wlen, hipMemcpyDeviceToHost, s) != hipSuccess)
-        return QFEC_EHIP;
-    b.wire = h + b.o_wire;
-    b.wlen = reinterpret_cast<const int*>(h + b.o_wlen);
-    return QFEC_OK;
-}
-
-// receive: pseudo-groups of wire rows (datagrams, or 0xEC-wrapped shards for decodes)
+// receive: pseudo-groups of rows (datagrams, or bare shards for decodes)
 struct UnpackRow {
     int group, ik;
-    View hdr_src;    // bytes written from the row start: the datagram (verdicts) ...
-    int wrap = 0;    // ... or, for decodes, a synthesized 11-byte 0xEC header (wrap = 1) + the shard
+    uint32_t off, len;  // the row's bytes in the receive arena
 };
 struct UnpackBatch {
     int k, n, checksum, dec_pkt_size;
     int groups = 0;
+    int wrap = 0;              // decodes: rows are shards (an 0xEC header synthesized on the device)
     bool want_shards = false;  // decodes: the data rows come back
     size_t need = 0;           // row bytes dec_src_pkt_info may read (head + size field), if known
     std::vector<UnpackRow> rows;
-    // layout in an arena (host and device alike up to o_hend; marks and the device's shard
-    // matrix after it); results in its host side
-    size_t base = 0, sp = 0, wp = 0;
-    size_t o_wlen = 0, o_rx = 0, o_st = 0, o_ps = 0, o_hsh = 0, o_hend = 0, o_marks = 0, o_dsh = 0, o_dend = 0;
+    size_t sp = 0, wp = 0;
+    // staging (io arena, host and device alike): offsets and lengths in, results out
+    size_t o_off = 0, o_len = 0, o_rx = 0, o_st = 0, o_ps = 0, o_hsh = 0;
+    // device work buffer: gathered wire, its lengths, marks, shard matrix
+    size_t w_wire = 0, w_wlen = 0, w_marks = 0, w_sh = 0;
     const int *rx = nullptr, *status = nullptr, *psize = nullptr;
     const uint8_t* shards = nullptr;  // want_shards: the data rows, [G][k][sp]
 };
@@ -354,85 +374,54 @@ struct UnpackBatch {
 // are dec_pkt_size long, zero-filled): `need` (verdicts: the largest head + size field among the
 // rows; decodes: 0 -- a decoded row is zero past its inputs' longest shard, so a genuine packet
 // fits; a row the pitch cuts short is re-decoded at dec_pkt_size + 4, see the decode loop)
-void unpack_layout(UnpackBatch& b, size_t base) {
-    const size_t G = (size_t)b.groups;
+void unpack_layout(UnpackBatch& b, Stage& io, Stage& work) {
+    const size_t G = (size_t)b.groups, R = G * b.n;
     size_t maxd = 16;
-    for (auto& r : b.rows) maxd = std::max(maxd, (size_t)r.hdr_src.len + (r.wrap ? 11u : 0u));
+    for (auto& r : b.rows) maxd = std::max(maxd, (size_t)r.len + (b.wrap ? 11u : 0u));
     b.sp = round16(std::max(maxd, std::min(b.need, (size_t)b.dec_pkt_size + 4)));
     b.wp = round16(b.sp + 13);
-    b.base = base;
-    size_t o = base + G * b.n * b.wp;  // wire
-    b.o_wlen = o;
-    o += round16(G * b.n * 4);
-    b.o_rx = o;
-    o += round16(G * b.n * 4);
-    b.o_st = o;
-    o += round16(G * b.k * 4);
-    b.o_ps = o;
-    o += round16(G * b.k * 4);
-    b.o_hsh = o;
-    if (b.want_shards) o += G * b.k * b.sp;
-    b.o_hend = o;
-    b.o_marks = o;
-    o += round16(G * b.n);
-    b.o_dsh = o;
-    o += G * b.n * b.sp;
-    b.o_dend = o;
+    b.o_off = io.take(R * 8);
+    b.o_len = io.take(R * 4);
+    b.o_rx = io.take(R * 4);
+    b.o_st = io.take(G * b.k * 4);
+    b.o_ps = io.take(G * b.k * 4);
+    b.o_hsh = b.want_shards ? io.take(G * b.k * b.sp) : 0;
+    b.w_wire = work.take(R * b.wp);
+    b.w_wlen = work.take(R * 4);
+    b.w_marks = work.take(R);
+    b.w_sh = work.take(R * b.sp);
 }
 
-// rows copied into the pinned wire on several threads when there are many bytes
-template <class F>
-void parallel_rows(size_t nrows, size_t bytes, F&& f) {
-    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    const unsigned T = bytes > ((size_t)8 << 20) ? hw : 1u;
-    if (T <= 1) {
-        f(0, nrows);
-        return;
+// fill the tables, gather the rows on the device, verdicts / decodes, results back (async)
+int run_unpack(qfec_zfec* z, UnpackBatch& b, const uint8_t* d_rx, hipStream_t s) {
+    const size_t G = (size_t)b.groups, R = G * b.n;
+    uint8_t* h = z->io.h;
+    uint8_t* d = z->d_io.d;
+    uint8_t* w = z->d_work.d;
+    unsigned long long* off = reinterpret_cast<unsigned long long*>(h + b.o_off);
+    int* len = reinterpret_cast<int*>(h + b.o_len);
+    memset(off, 0, R * 8);
+    memset(len, 0, R * 4);
+    for (auto& r : b.rows) {
+        const size_t i = (size_t)r.group * b.n + r.ik;
+        off[i] = r.off;
+        len[i] = (int)r.len;
     }
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < T; ++t) th.emplace_back(f, nrows * t / T, nrows * (t + 1) / T);
-    for (auto& x : th) x.join();
-}
-
-int run_unpack(qfec_zfec* z, Arena& A, UnpackBatch& b, hipStream_t s) {
-    const size_t G = (size_t)b.groups;
-    uint8_t* h = A.h;
-    uint8_t* wire = h + b.base;
-    int* wlen = reinterpret_cast<int*>(h + b.o_wlen);
-    memset(wlen, 0, G * b.n * 4);
-    size_t bytes = 0;
-    for (auto& r : b.rows) bytes += r.hdr_src.len;
-    parallel_rows(b.rows.size(), bytes, [&](size_t r0, size_t r1) {
-        for (size_t i = r0; i < r1; ++i) {
-            const UnpackRow& r = b.rows[i];
-            uint8_t* row = wire + ((size_t)r.group * b.n + r.ik) * b.wp;
-            size_t len = r.hdr_src.len;
-            if (r.wrap) {  // [0xEC][sent 0][src 0][n | k << 4 | ik << 8][shard]
-                memset(row, 0, 11);
-                row[0] = 0xEC;
-                const uint32_t ikn = (uint32_t)b.n | (uint32_t)b.k << 4 | (uint32_t)r.ik << 8;
-                row[9] = (uint8_t)(ikn & 0xFF);
-                row[10] = (uint8_t)(ikn >> 8);
-                if (len) memcpy(row + 11, r.hdr_src.p(), len);
-                len += 11;
-            } else if (len) {
-                memcpy(row, r.hdr_src.p(), len);
-            }
-            wlen[(size_t)r.group * b.n + r.ik] = (int)len;
-        }
-    });
-    uint8_t* d = A.d;
-    if (hipMemcpyAsync(d + b.base, h + b.base, b.o_rx - b.base, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (hipMemcpyAsync(d + b.o_off, h + b.o_off, b.o_rx - b.o_off, hipMemcpyHostToDevice, s) != hipSuccess)
         return QFEC_EHIP;
-    int rc = qfec_unpack_datagrams(code_for(z, b.k, b.n), d + b.base, (long long)b.wp, reinterpret_cast<int*>(d + b.o_wlen),
-                                   (long long)G, b.checksum, b.dec_pkt_size, d + b.o_dsh, (long long)b.sp,
-                                   d + b.o_marks, reinterpret_cast<int*>(d + b.o_rx), reinterpret_cast<int*>(d + b.o_st),
-                                   reinterpret_cast<int*>(d + b.o_ps), s);
+    int rc = qfec_gather_rows(d_rx, reinterpret_cast<const unsigned long long*>(d + b.o_off),
+                              reinterpret_cast<const int*>(d + b.o_len), (long long)R, b.wrap ? b.n : 0,
+                              b.wrap ? b.k : 0, w + b.w_wire, (long long)b.wp, reinterpret_cast<int*>(w + b.w_wlen), s);
     if (rc) return rc;
-    if (hipMemcpyAsync(h + b.o_rx, d + b.o_rx, b.o_hsh - b.o_rx, hipMemcpyDeviceToHost, s) != hipSuccess)
+    rc = qfec_unpack_datagrams(code_for(z, b.k, b.n), w + b.w_wire, (long long)b.wp, reinterpret_cast<int*>(w + b.w_wlen),
+                               (long long)G, b.checksum, b.dec_pkt_size, w + b.w_sh, (long long)b.sp, w + b.w_marks,
+                               reinterpret_cast<int*>(d + b.o_rx), reinterpret_cast<int*>(d + b.o_st),
+                               reinterpret_cast<int*>(d + b.o_ps), s);
+    if (rc) return rc;
+    if (hipMemcpyAsync(h + b.o_rx, d + b.o_rx, (b.o_ps + G * b.k * 4) - b.o_rx, hipMemcpyDeviceToHost, s) != hipSuccess)
         return QFEC_EHIP;
     if (b.want_shards &&  // the k data rows of each group only
-        hipMemcpy2DAsync(h + b.o_hsh, (size_t)b.k * b.sp, d + b.o_dsh, (size_t)b.n * b.sp, (size_t)b.k * b.sp, G,
+        hipMemcpy2DAsync(h + b.o_hsh, (size_t)b.k * b.sp, w + b.w_sh, (size_t)b.n * b.sp, (size_t)b.k * b.sp, G,
                          hipMemcpyDeviceToHost, s) != hipSuccess)
         return QFEC_EHIP;
     b.rx = reinterpret_cast<const int*>(h + b.o_rx);
@@ -451,6 +440,7 @@ struct Verdict {  // of one received FEC datagram
     bool src_ok = false;  // dec_src_pkt_info on it (source packets)
     int src_size = 0;     // its size field
     View payload;
+    int batch = -1, group = -1, ik = 0;  // its place in the verdict launch
 };
 
 struct DecodeKey {
@@ -470,21 +460,22 @@ struct DecodeReq {
 };
 
 struct RxPass {
-    std::map<DecodeKey, DecodeOut>* cache;
+    const std::map<DecodeKey, DecodeOut>* cache;
     std::vector<DecodeReq>* missing;
 };
 
 // the receive side of one session over its queued ops (NetFecCodec.cpp:189-371)
 class RxMachine {
    public:
-    RxMachine(Session& S, int sidx, const std::vector<Verdict>& verd, RxPass& pass, std::vector<std::vector<Emit>>& out)
-        : S(S), R(S.rx), sidx(sidx), verd(verd), pass(pass), out(out) {}
+    RxMachine(Session& S, int sidx, const std::vector<Verdict>& verd, RxPass& pass, std::vector<Emit>& out,
+              const uint8_t* rx)
+        : S(S), R(S.rx), sidx(sidx), verd(verd), pass(pass), out(out), rx(rx) {}
 
     void run() {
         size_t v = 0;
         for (size_t oi = 0; oi < S.ops.size(); ++oi) {
             const Op& op = S.ops[oi];
-            cur = &out[oi];
+            cur = (uint32_t)oi;
             if (op.t == OP_UNPACK) unpack(op, verd[v++]);
             else if (op.t == OP_SETKN) set_kn(op.a, op.b, op.c != 0);
             else if (op.t == OP_SORTED) R.is_sorted = op.a != 0;
@@ -497,15 +488,17 @@ class RxMachine {
     int sidx;
     const std::vector<Verdict>& verd;
     RxPass& pass;
-    std::vector<std::vector<Emit>>& out;
-    std::vector<Emit>* cur = nullptr;
+    std::vector<Emit>& out;
+    const uint8_t* rx;
+    uint32_t cur = 0;
 
     void deliver(const View& v, uint32_t src) {
         Emit e;
+        e.op = cur;
         e.kind = 2;
         e.v = v;
         e.src = src;
-        cur->push_back(std::move(e));
+        out.push_back(e);
     }
     // a decoded row: its payload, or a placeholder (kind 3) naming the request and row
     void deliver_decoded(const DecodeOut* res, int req, int i, uint32_t src) {
@@ -514,11 +507,12 @@ class RxMachine {
             return;
         }
         Emit e;
+        e.op = cur;
         e.kind = 3;
         e.batch = req;
         e.row = i;
         e.src = src;
-        cur->push_back(std::move(e));
+        out.push_back(e);
     }
     void set_kn(int k, int n, bool add) {  // the receive side's codec list (find_codec at :301)
         if (k < 0 || n < 0 || k > n) return;
@@ -566,10 +560,10 @@ class RxMachine {
     }
     // add_packet_fec_buf :485-535; fills `rows` with the first k valid slots (iValid order)
     bool add_packet(uint32_t ipkt, uint32_t isrc, const Verdict& vd, uint64_t uid, int ik, int k, int n,
-                    uint32_t seg_beg, int* max_size, int* rows, int* nrows, bool* undefined) {
+                    uint32_t seg_beg, const Op& op, int* max_size, int* rows, int* nrows, bool* undefined) {
         if (ipkt >= R.first && ipkt < R.second) {
             Slot& s = R.slots[ipkt - R.first];
-            s.set_packet(vd.shard, uid, ik, vd.payload);
+            s.set_packet(vd.shard, uid, ik, vd.payload, op.off, op.size);
             s.iPacket = (int64_t)ipkt;
             s.bSourcePkt = ipkt - seg_beg < (uint32_t)k;
             s.i_source_pkt = isrc;
@@ -601,11 +595,11 @@ class RxMachine {
     }
 
     void unpack(const Op& op, const Verdict& vd) {  // zfec_unpack_input :189-371
-        const uint8_t* d = op.data->data();
-        const uint32_t size = (uint32_t)op.data->size();
+        const uint8_t* d = rx + op.off;
+        const uint32_t size = op.size;
         if (size > (uint32_t)R.dec_pkt_size) R.dec_pkt_size = (int)size;  // unpack_fec_head realloc (:345-352)
         if (!vd.fec) {  // not an FEC datagram: handed over minus its tag, source index 0 (:201-209)
-            if (size >= 1) deliver(View{op.data, 1, size - 1}, 0u);
+            if (size >= 1) deliver(View{SRC_RX, op.off + 1, size - 1}, 0u);
             return;
         }
         R.is_checksum = d[0] == 0xED;  // (:364)
@@ -637,7 +631,7 @@ class RxMachine {
         }
         int max_size = 0, rows[16], nrows = 0;
         bool undefined = false;
-        const bool dec = add_packet(i_recv, src, vd, op.uid, cur_ni, cur_k, cur_n, seg_beg, &max_size, rows, &nrows,
+        const bool dec = add_packet(i_recv, src, vd, op.uid, cur_ni, cur_k, cur_n, seg_beg, op, &max_size, rows, &nrows,
                                     &undefined);
         set_used(i_recv, bused);
         if (!dec && i_recv - R.i_expected_packet >= (uint32_t)(2 * cur_n) && R.is_sorted) {  // :289-293
@@ -708,6 +702,121 @@ void init_rx(RxState& R, int buf_items, int max_pkt, int kmax) {
     R.is_checksum = false;
 }
 
+// ---- the send machine of one session (zfec_pack_input, NetFecCodec.cpp:68-175): its closed
+// groups (session-local ids; PackOut::batch is filled when the sessions' groups are merged) and
+// its emits; the FEC-off datagrams [0x13][payload] go to the session's own buffer
+struct LocalGroup {
+    int k, n;
+    PackGroup g;
+};
+void tx_machine(Session& S, std::vector<Emit>& out, std::vector<LocalGroup>& groups, std::vector<uint8_t>& own,
+                const uint8_t* txa) {
+    TxState& T = S.tx;
+    std::vector<size_t> pending;  // emits of the open group's rows
+    auto open_entry = [&](uint32_t oi, int row) {
+        Emit e;
+        e.op = oi;
+        e.kind = 0;
+        e.row = row;
+        out.push_back(e);
+        pending.push_back(out.size() - 1);
+    };
+    auto close_group = [&]() {  // the open group's rows so far, as one group
+        LocalGroup lg;
+        lg.k = T.gk;
+        lg.n = T.gn;
+        lg.g.sent0 = T.g_sent0;
+        lg.g.src0 = T.g_src0;
+        for (size_t i = 0; i < T.g_pay.size() && i < (size_t)T.gk; ++i) lg.g.pay[i] = T.g_pay[i];
+        const long long gi = (long long)groups.size();
+        groups.push_back(lg);
+        for (size_t e : pending) {
+            out[e].group = gi;
+            out[e].batch = -1;
+        }
+        pending.clear();
+    };
+    for (size_t oi = 0; oi < S.ops.size(); ++oi) {
+        const Op& op = S.ops[oi];
+        if (op.t == OP_SETKN) {  // set_zfec_kn :591-611 (send side); the open group keeps its (k, n)
+            if (op.a < 0 || op.b < 0 || op.a > op.b) continue;
+            const CodecEntry* c = T.codecs.find(op.a, op.b);
+            if (c) {
+                T.have_codec = true;
+                T.k = c->k;
+                T.n = c->n;
+            } else if (op.c) {
+                int rk, rn;
+                T.codecs.add(op.a, op.b, &rk, &rn);
+                T.have_codec = true;
+                T.k = rk;
+                T.n = rn;
+            }
+        } else if (op.t == OP_ENABLE) {
+            T.enabled = op.a != 0;
+        } else if (op.t == OP_DYNKN) {
+            T.dynkn = op.a != 0;
+        } else if (op.t == OP_LOST) {
+            T.lost_rate = op.f;
+        } else if (op.t == OP_PACK) {
+            if (!T.enabled || !T.have_codec) {  // :75-94: [0x13][payload], numbering unchanged
+                Emit e;
+                e.op = (uint32_t)oi;
+                e.kind = 1;
+                e.v = View{SRC_OWN, (uint32_t)own.size(), op.size + 1};
+                own.push_back(0x13);
+                own.insert(own.end(), txa + op.off, txa + op.off + op.size);
+                out.push_back(e);
+                continue;
+            }
+            if (T.g_pay.empty() && T.g_emitted == 0) {  // a group starts (its (k, n) fixed)
+                T.gk = T.k;
+                T.gn = T.n;
+                T.g_sent0 = T.i_sent_pkt;
+                T.g_src0 = T.i_sent_src_pkt;
+            }
+            const int k = T.gk, n = T.gn;
+            const int ik = (int)((T.i_sent_pkt - T.i_cur_segment_beg) % (uint32_t)n);
+            if (ik < k) {
+                T.g_pay.push_back(View{SRC_TX, op.off, op.size});
+                open_entry((uint32_t)oi, ik);
+                T.i_sent_pkt++;
+                T.i_sent_src_pkt++;
+            }
+            if (ik == k - 1) {  // the check packets (:133-172)
+                for (int j = k; j < n; ++j) {
+                    open_entry((uint32_t)oi, j);
+                    T.i_sent_pkt++;
+                }
+                close_group();
+                T.g_pay.clear();
+                T.g_emitted = 0;
+                if (T.dynkn) {  // recalc_zfec_kn (:51-65)
+                    const CodecEntry* c = T.codecs.by_lost(T.lost_rate);
+                    if (c) {
+                        T.k = c->k;
+                        T.n = c->n;
+                    }
+                }
+                T.i_cur_segment_beg = T.i_sent_pkt;
+            }
+        }
+    }
+    // a group still open: its source rows of this flush go out now (they do not depend on
+    // the rest of the group); the group is packed again, whole, when it completes
+    if (!pending.empty()) {
+        close_group();
+        T.g_emitted = (int)T.g_pay.size();
+    }
+}
+
+unsigned flush_threads(size_t work, size_t sessions) {
+    unsigned t = work < 4096 ? 1u : std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (unsigned)sessions}));
+    if (const char* e = getenv("QFEC_ZFEC_RX_THREADS"))  // tests: force the threaded machines
+        t = (unsigned)std::max(1, std::min(64, atoi(e)));
+    return t;
+}
+
 }  // namespace
 
 extern "C" {
@@ -717,9 +826,8 @@ qfec_zfec* qfec_zfec_new(void) { return new (std::nothrow) qfec_zfec(); }
 void qfec_zfec_free(qfec_zfec* z) {
     if (!z) return;
     for (auto& kv : z->codes) qfec_code_free(kv.second);
-    z->pack_arena.release();
-    z->rx_arena.release();
-    z->dec_arena.release();
+    for (auto* a : {&z->rx[0], &z->rx[1], &z->tx[0], &z->tx[1], &z->io}) a->release();
+    for (auto* b : {&z->d_rx, &z->d_tx, &z->d_io, &z->d_work}) b->release();
     delete z;
 }
 
@@ -768,7 +876,6 @@ static int push_op(qfec_zfec* z, int s, Op&& op) {
     if (!z) return QFEC_EINVAL;
     std::lock_guard<std::mutex> lk(z->mu);
     if (s < 0 || s >= (int)z->sessions.size()) return QFEC_EINVAL;
-    if (op.t == OP_UNPACK) op.uid = z->next_uid++;
     z->sessions[s].ops.push_back(std::move(op));
     return QFEC_OK;
 }
@@ -811,22 +918,25 @@ int qfec_zfec_lost_rate(qfec_zfec* z, int s, float lost) {
     o.f = lost;
     return push_op(z, s, std::move(o));
 }
-static Buf copy_bytes(const void* p, unsigned int size) {
-    return std::make_shared<const std::vector<uint8_t>>(static_cast<const uint8_t*>(p), static_cast<const uint8_t*>(p) + size);
+// the bytes go straight into the direction's pinned arena (no per-packet allocation)
+static int queue_bytes(qfec_zfec* z, int s, OpType t, const void* p, unsigned int size) {
+    if (!z || (!p && size)) return QFEC_EINVAL;
+    std::lock_guard<std::mutex> lk(z->mu);
+    if (s < 0 || s >= (int)z->sessions.size()) return QFEC_EINVAL;
+    HostArena& A = t == OP_PACK ? z->tx[z->txc] : z->rx[z->rxc];
+    Op o;
+    o.t = t;
+    o.size = size;
+    if (!A.append(p, size, &o.off)) return QFEC_ENOMEM;
+    if (t == OP_UNPACK) o.uid = z->next_uid++;
+    z->sessions[s].ops.push_back(o);
+    return QFEC_OK;
 }
 int qfec_zfec_pack_input(qfec_zfec* z, int s, const void* data, unsigned int size) {
-    if (!data && size) return QFEC_EINVAL;
-    Op o;
-    o.t = OP_PACK;
-    o.data = copy_bytes(data, size);
-    return push_op(z, s, std::move(o));
+    return queue_bytes(z, s, OP_PACK, data, size);
 }
 int qfec_zfec_unpack_input(qfec_zfec* z, int s, const void* datagram, unsigned int size) {
-    if (!datagram && size) return QFEC_EINVAL;
-    Op o;
-    o.t = OP_UNPACK;
-    o.data = copy_bytes(datagram, size);
-    return push_op(z, s, std::move(o));
+    return queue_bytes(z, s, OP_UNPACK, datagram, size);
 }
 
 int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn unpack_out, void* stream) {
@@ -843,146 +953,105 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     };
     hipStream_t st = (hipStream_t)stream;
     const size_t NS = z->sessions.size();
-    std::vector<std::vector<std::vector<Emit>>> outs(NS);
-    // ---- send: zfec_pack_input (NetFecCodec.cpp:68-175) over every queue; groups to pack
+    HostArena& RXA = z->rx[z->rxc];
+    HostArena& TXA = z->tx[z->txc];
+    std::vector<std::vector<Emit>> tx_out(NS), rx_out(NS);
+    std::vector<std::vector<uint8_t>> own(NS);
+    size_t n_ops = 0;
+    for (auto& S : z->sessions) n_ops += S.ops.size();
+    const unsigned threads = flush_threads(n_ops, NS);
+    int rc = 0;
+    // ---- send: the machines (threaded over sessions), then their groups merged per (k, n)
+    std::vector<std::vector<LocalGroup>> lgroups(NS);
+    parallel_for(NS, threads, [&](size_t si) { tx_machine(z->sessions[si], tx_out[si], lgroups[si], own[si], TXA.h); });
     std::vector<PackBatch> packs;
     std::map<std::pair<int, int>, int> pack_of;  // (k, n) -> index in packs
-    auto batch_for = [&](int k, int n) -> int {
-        auto it = pack_of.find(std::make_pair(k, n));
-        if (it != pack_of.end()) return it->second;
-        PackBatch b;
-        b.k = k;
-        b.n = n;
-        packs.push_back(std::move(b));
-        pack_of.emplace(std::make_pair(k, n), (int)packs.size() - 1);
-        return (int)packs.size() - 1;
-    };
+    z->io.used = 0;
     for (size_t si = 0; si < NS; ++si) {
-        Session& S = z->sessions[si];
-        TxState& T = S.tx;
-        outs[si].resize(S.ops.size());
-        std::vector<std::pair<size_t, int>> pending;  // (op, index in its outputs) of the open group's rows
-        auto open_entry = [&](std::vector<Emit>& out, size_t oi, int row) {
-            Emit e;
-            e.kind = 0;
-            e.row = row;
-            e.batch = batch_for(T.gk, T.gn);
-            out.push_back(e);
-            pending.emplace_back(oi, (int)out.size() - 1);
-        };
-        auto close_group = [&]() {  // the open group's rows so far, as one group of its batch
-            PackBatch& b = packs[(size_t)batch_for(T.gk, T.gn)];
-            PackGroup g;
-            g.sent0 = T.g_sent0;
-            g.src0 = T.g_src0;
-            g.pay.assign((size_t)T.gk, nullptr);
-            for (size_t i = 0; i < T.g_pay.size() && i < (size_t)T.gk; ++i) g.pay[i] = T.g_pay[i];
-            const long long gi = (long long)b.groups.size();
-            b.groups.push_back(std::move(g));
-            for (auto& pr : pending) outs[si][pr.first][(size_t)pr.second].group = gi;
-            pending.clear();
-        };
-        for (size_t oi = 0; oi < S.ops.size(); ++oi) {
-            Op& op = S.ops[oi];
-            std::vector<Emit>& out = outs[si][oi];
-            if (op.t == OP_SETKN) {  // set_zfec_kn :591-611 (send side); the open group keeps its (k, n)
-                if (op.a < 0 || op.b < 0 || op.a > op.b) continue;
-                const CodecEntry* c = T.codecs.find(op.a, op.b);
-                if (c) {
-                    T.have_codec = true;
-                    T.k = c->k;
-                    T.n = c->n;
-                } else if (op.c) {
-                    int rk, rn;
-                    T.codecs.add(op.a, op.b, &rk, &rn);
-                    T.have_codec = true;
-                    T.k = rk;
-                    T.n = rn;
-                }
-            } else if (op.t == OP_ENABLE) {
-                T.enabled = op.a != 0;
-            } else if (op.t == OP_DYNKN) {
-                T.dynkn = op.a != 0;
-            } else if (op.t == OP_LOST) {
-                T.lost_rate = op.f;
-            } else if (op.t == OP_PACK) {
-                if (!T.enabled || !T.have_codec) {  // :75-94: [0x13][payload], numbering unchanged
-                    auto v = std::make_shared<std::vector<uint8_t>>();
-                    v->reserve(op.data->size() + 1);
-                    v->push_back(0x13);
-                    v->insert(v->end(), op.data->begin(), op.data->end());
-                    Emit e;
-                    e.kind = 1;
-                    e.v = View{v, 0, (uint32_t)v->size()};
-                    out.push_back(std::move(e));
-                    continue;
-                }
-                if (T.g_pay.empty() && T.g_emitted == 0) {  // a group starts (its (k, n) fixed)
-                    T.gk = T.k;
-                    T.gn = T.n;
-                    T.g_sent0 = T.i_sent_pkt;
-                    T.g_src0 = T.i_sent_src_pkt;
-                }
-                const int k = T.gk, n = T.gn;
-                const int ik = (int)((T.i_sent_pkt - T.i_cur_segment_beg) % (uint32_t)n);
-                if (ik < k) {
-                    T.g_pay.push_back(op.data);
-                    open_entry(out, oi, ik);
-                    T.i_sent_pkt++;
-                    T.i_sent_src_pkt++;
-                }
-                if (ik == k - 1) {  // the check packets (:133-172)
-                    for (int j = k; j < n; ++j) {
-                        open_entry(out, oi, j);
-                        T.i_sent_pkt++;
-                    }
-                    close_group();
-                    T.g_pay.clear();
-                    T.g_emitted = 0;
-                    if (T.dynkn) {  // recalc_zfec_kn (:51-65)
-                        const CodecEntry* c = T.codecs.by_lost(T.lost_rate);
-                        if (c) {
-                            T.k = c->k;
-                            T.n = c->n;
-                        }
-                    }
-                    T.i_cur_segment_beg = T.i_sent_pkt;
-                }
+        std::vector<std::pair<int, long long>> place(lgroups[si].size());
+        for (size_t i = 0; i < lgroups[si].size(); ++i) {
+            const LocalGroup& lg = lgroups[si][i];
+            auto it = pack_of.find(std::make_pair(lg.k, lg.n));
+            int bi;
+            if (it == pack_of.end()) {
+                PackBatch b;
+                b.k = lg.k;
+                b.n = lg.n;
+                packs.push_back(std::move(b));
+                bi = (int)packs.size() - 1;
+                pack_of.emplace(std::make_pair(lg.k, lg.n), bi);
+            } else {
+                bi = it->second;
             }
+            place[i] = std::make_pair(bi, (long long)packs[(size_t)bi].groups.size());
+            packs[(size_t)bi].groups.push_back(lg.g);
         }
-        // a group still open: its source rows of this flush go out now (they do not depend on
-        // the rest of the group); the group is packed again, whole, when it completes
-        if (!pending.empty()) {
-            close_group();
-            T.g_emitted = (int)T.g_pay.size();
-        }
+        for (auto& e : tx_out[si])
+            if (e.kind == 0) {
+                e.batch = place[(size_t)e.group].first;
+                e.group = place[(size_t)e.group].second;
+            }
     }
     phase("tx machine");
-    int rc = 0;
-    {
-        // batches laid out back to back at their device extents (the device-only shard
-        // scratch is each batch's last region), so no two batches share arena bytes
-        size_t hend = 0, dend = 0;
+    if (!packs.empty()) {
+        // the send arena to the device in one copy; per batch: offsets / sizes / seq in, the
+        // datagrams and their lengths out, all through the pinned io arena
+        Stage io, work;
         for (auto& b : packs) {
-            pack_layout(b, dend);
-            hend = b.o_end;
-            dend = b.o_shards + b.groups.size() * b.n * b.sp;
+            const size_t G = b.groups.size();
+            size_t maxp = 1;
+            for (auto& g : b.groups)
+                for (int i = 0; i < b.k; ++i) maxp = std::max(maxp, (size_t)g.pay[i].len);
+            b.sp = round16(maxp + 4);
+            b.wp = (b.sp + 13 + 63) & ~(size_t)63;  // the 64-B multiple: the fused send writes whole lines
+            b.o_offs = io.take(G * b.k * 8);
+            b.o_sizes = io.take(G * b.k * 4);
+            b.o_seq = io.take(G * 8);
+            b.o_wlen = io.take(G * b.n * 4);
+            b.o_wire = io.take(G * b.n * b.wp);
+            b.d_shards = work.take(G * b.n * b.sp);
         }
-        if (!packs.empty()) {
-            if ((rc = z->pack_arena.ensure(hend, dend))) return rc;
-            for (auto& b : packs)
-                if ((rc = run_pack(z, b, st))) return rc;
+        z->io.used = 0;
+        if (!z->io.reserve(io.o + 16) || (rc = z->d_io.ensure(io.o + 16)) || (rc = z->d_work.ensure(work.o + 16)) ||
+            (rc = z->d_tx.ensure(TXA.used + 16)))
+            return rc ? rc : QFEC_ENOMEM;
+        if (hipMemcpyAsync(z->d_tx.d, TXA.h, TXA.used + 16, hipMemcpyHostToDevice, st) != hipSuccess) return QFEC_EHIP;
+        uint8_t* h = z->io.h;
+        uint8_t* d = z->d_io.d;
+        for (auto& b : packs) {
+            const size_t G = b.groups.size();
+            long long* offs = reinterpret_cast<long long*>(h + b.o_offs);
+            int* sizes = reinterpret_cast<int*>(h + b.o_sizes);
+            uint32_t* seq = reinterpret_cast<uint32_t*>(h + b.o_seq);
+            for (size_t g = 0; g < G; ++g) {
+                seq[2 * g] = b.groups[g].sent0;
+                seq[2 * g + 1] = b.groups[g].src0;
+                for (int i = 0; i < b.k; ++i) {
+                    const View& p = b.groups[g].pay[i];
+                    offs[g * b.k + i] = (long long)p.off;
+                    sizes[g * b.k + i] = (int)p.len;
+                }
+            }
+            if (hipMemcpyAsync(d + b.o_offs, h + b.o_offs, b.o_wlen - b.o_offs, hipMemcpyHostToDevice, st) != hipSuccess)
+                return QFEC_EHIP;
+            if ((rc = qfec_pack_datagrams(code_for(z, b.k, b.n), z->d_tx.d, reinterpret_cast<const long long*>(d + b.o_offs),
+                                          reinterpret_cast<const int*>(d + b.o_sizes),
+                                          reinterpret_cast<const unsigned int*>(d + b.o_seq), (long long)G,
+                                          1 /* is_send_checksum */, z->d_work.d + b.d_shards, (long long)b.sp,
+                                          d + b.o_wire, (long long)b.wp, reinterpret_cast<int*>(d + b.o_wlen), st)))
+                return rc;
+            if (hipMemcpyAsync(h + b.o_wlen, d + b.o_wlen, b.o_wire + G * b.n * b.wp - b.o_wlen, hipMemcpyDeviceToHost,
+                               st) != hipSuccess)
+                return QFEC_EHIP;
         }
+        z->io.used = io.o;  // the datagrams stay until the callbacks (the receive stages go after)
+        if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
     }
     phase("pack launch");
     // ---- receive: verdicts of this flush's FEC datagrams (pseudo-groups by (k, n, tag, dec_pkt_size))
     std::vector<std::vector<Verdict>> verd(NS);
     std::vector<UnpackBatch> vb;
     std::map<std::tuple<int, int, int, int>, int> vb_of;
-    struct Where {
-        int batch = -1, group = -1, ik = 0;
-    };
-    std::vector<std::vector<Where>> where(NS);
     // rows taken in each pseudo-group (shared by all sessions: a row's verdict is its own)
     std::vector<std::vector<uint16_t>> taken;  // per batch, per group: bit ik
     for (size_t si = 0; si < NS; ++si) {
@@ -991,11 +1060,10 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         for (auto& op : S.ops) {
             if (op.t != OP_UNPACK) continue;
             Verdict v;
-            const uint8_t* d = op.data->data();
-            const size_t size = op.data->size();
+            const uint8_t* d = RXA.h + op.off;
+            const size_t size = op.size;
             if ((int)size > dps) dps = (int)size;
             v.fec = size >= 11 && (d[0] == 0xEC || d[0] == 0xED);
-            Where w;
             if (v.fec) {
                 const uint32_t ikn = (uint32_t)d[9] | (uint32_t)d[10] << 8;
                 const int n = (int)(ikn & 0xF), k = (int)((ikn >> 4) & 0xF), ik = (int)((ikn >> 8) & 0xF);
@@ -1031,56 +1099,54 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                         g = b.groups++;
                     }
                     used[(size_t)g] |= (uint16_t)(1u << ik);
-                    b.rows.push_back(UnpackRow{g, ik, View{op.data, 0, (uint32_t)size}, 0});
+                    b.rows.push_back(UnpackRow{g, ik, op.off, (uint32_t)size});
                     // the row bytes dec_src_pkt_info may read: head + the shard's size field
                     const size_t hdr = cs ? 13 : 11;
                     if (ik < k && size >= hdr + 2)
                         b.need = std::max(b.need, (size_t)(cs ? 4 : 2) + (d[hdr] | (size_t)d[hdr + 1] << 8));
-                    w.batch = bi;
-                    w.group = g;
-                    w.ik = ik;
+                    v.batch = bi;
+                    v.group = g;
+                    v.ik = ik;
                 }
             }
-            verd[si].push_back(std::move(v));
-            where[si].push_back(w);
+            verd[si].push_back(v);
         }
     }
     phase("rx grouping");
+    // the receive arena's bytes on the device once: verdict and decode launches gather from it
     if (!vb.empty()) {
-        size_t hend = 0, dend = 0;
-        for (auto& b : vb) {
-            unpack_layout(b, dend);
-            hend = b.o_hend;
-            dend = b.o_dend;
-        }
-        if ((rc = z->rx_arena.ensure(hend, dend))) return rc;
+        if ((rc = z->d_rx.ensure(RXA.used + 16))) return rc;
+        if (hipMemcpyAsync(z->d_rx.d, RXA.h, RXA.used + 16, hipMemcpyHostToDevice, st) != hipSuccess) return QFEC_EHIP;
+    }
+    if (!vb.empty()) {
+        Stage io{round16(z->io.used)}, work;
+        for (auto& b : vb) unpack_layout(b, io, work);
+        if (!z->io.reserve(io.o + 16) || (rc = z->d_io.ensure(io.o + 16)) || (rc = z->d_work.ensure(work.o + 16)))
+            return rc ? rc : QFEC_ENOMEM;
         for (auto& b : vb)
-            if ((rc = run_unpack(z, z->rx_arena, b, st))) return rc;
+            if ((rc = run_unpack(z, b, z->d_rx.d, st))) return rc;
         if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
     }
-    for (size_t si = 0; si < NS; ++si) {
+    parallel_for(NS, threads, [&](size_t si) {
         size_t v = 0;
         for (auto& op : z->sessions[si].ops) {
             if (op.t != OP_UNPACK) continue;
-            Verdict& vd = verd[si][v];
-            const Where& w = where[si][v];
-            ++v;
-            if (w.group < 0) continue;
-            const UnpackBatch& b = vb[(size_t)w.batch];
-            const size_t row = (size_t)w.group * b.n + w.ik;
-            const uint32_t size = (uint32_t)op.data->size();
-            const uint32_t hdr = op.data->data()[0] == 0xED ? 13 : 11;
+            Verdict& vd = verd[si][v++];
+            if (vd.group < 0) continue;
+            const UnpackBatch& b = vb[(size_t)vd.batch];
+            const size_t row = (size_t)vd.group * b.n + vd.ik;
+            const uint32_t hdr = RXA.h[op.off] == 0xED ? 13 : 11;
             vd.ok = b.rx[row] >= 0;
-            if (vd.ok) vd.shard = View{op.data, hdr, size - hdr};
-            if (w.ik < b.k && vd.ok) {
-                const int stt = b.status[(size_t)w.group * b.k + w.ik];
+            if (vd.ok) vd.shard = View{SRC_RX, op.off + hdr, op.size - hdr};
+            if (vd.ik < b.k && vd.ok) {
+                const int stt = b.status[(size_t)vd.group * b.k + vd.ik];
                 vd.src_ok = stt >= 0;
-                vd.src_size = b.psize[(size_t)w.group * b.k + w.ik];
+                vd.src_size = b.psize[(size_t)vd.group * b.k + vd.ik];
                 // a received row's payload is the datagram's own bytes
-                if (vd.src_ok) vd.payload = View{op.data, hdr + (uint32_t)stt, (uint32_t)vd.src_size};
+                if (vd.src_ok) vd.payload = View{SRC_RX, op.off + hdr + (uint32_t)stt, (uint32_t)vd.src_size};
             }
         }
-    }
+    });
     phase("verdicts");
     // ---- the receive machines.  A pass that meets a decode without a device result assumes
     // every row of it decoded and passed (the common case) and leaves placeholders for its
@@ -1089,53 +1155,34 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     std::map<DecodeKey, DecodeOut> cache;
     std::vector<RxState> start(NS);
     for (size_t si = 0; si < NS; ++si) start[si] = z->sessions[si].rx;
-    // sessions are independent: their machines run on several threads (the decode cache is
-    // only read during a pass), each session collecting its own decode requests; the requests
-    // are then numbered in session order, as one thread would have numbered them
-    size_t rx_ops = 0;
-    for (size_t si = 0; si < NS; ++si) rx_ops += verd[si].size();
-    unsigned rx_threads =
-        rx_ops < 4096 ? 1u : std::max(1u, std::min({8u, std::thread::hardware_concurrency(), (unsigned)NS}));
-    if (const char* e = getenv("QFEC_ZFEC_RX_THREADS"))  // tests: force the threaded machines
-        rx_threads = (unsigned)std::max(1, std::min(64, atoi(e)));
+    std::vector<uint8_t> dec_bytes;  // decoded payloads that are not views of an input shard
+    std::vector<DecodeReq> missing;
     for (int pass_no = 0;; ++pass_no) {
-        std::vector<DecodeReq> missing;
+        missing.clear();
         std::vector<std::vector<DecodeReq>> miss_s(NS);
-        auto run_session = [&](size_t si) {
+        parallel_for(NS, threads, [&](size_t si) {  // sessions are independent
             Session& S = z->sessions[si];
             if (pass_no) S.rx = start[si];
-            if (pass_no)
-                for (auto& o : outs[si])
-                    o.erase(std::remove_if(o.begin(), o.end(), [](const Emit& e) { return e.kind >= 2; }), o.end());
+            rx_out[si].clear();
             RxPass pass{&cache, &miss_s[si]};
-            RxMachine m(S, (int)si, verd[si], pass, outs[si]);
+            RxMachine m(S, (int)si, verd[si], pass, rx_out[si], RXA.h);
             m.run();
-        };
-        if (rx_threads <= 1) {
-            for (size_t si = 0; si < NS; ++si) run_session(si);
-        } else {
-            std::atomic<size_t> next{0};
-            std::vector<std::thread> th;
-            for (unsigned t = 0; t < rx_threads; ++t)
-                th.emplace_back([&]() {
-                    for (size_t si; (si = next.fetch_add(1)) < NS;) run_session(si);
-                });
-            for (auto& x : th) x.join();
-        }
+        });
+        // the requests numbered in session order, as one thread would have numbered them
         for (size_t si = 0; si < NS; ++si) {
             const int base = (int)missing.size();
             if (base)
-                for (auto& o : outs[si])
-                    for (auto& e : o)
-                        if (e.kind == 3) e.batch += base;
+                for (auto& e : rx_out[si])
+                    if (e.kind == 3) e.batch += base;
             for (auto& q : miss_s[si]) missing.push_back(std::move(q));
         }
         phase("rx machine");
         if (missing.empty()) break;
         // one launch per (k, n, mode, dec_pkt_size): each decode is a group holding exactly its k
-        // shards, wrapped as 0xEC datagrams (no shard checksum to re-check).  Round 0 decodes at
-        // the shards' own length; a row whose size field reaches past that pitch (only a corrupt
-        // one can) is decoded again at dec_pkt_size + 4 in round 1, as the reference reads it.
+        // shards, an 0xEC header synthesized in front of each (no shard checksum to re-check).
+        // Round 0 decodes at the shards' own length; a row whose size field reaches past that
+        // pitch (only a corrupt one can) is decoded again at dec_pkt_size + 4 in round 1, as the
+        // reference reads it.
         std::vector<const DecodeReq*> todo;
         for (auto& q : missing)
             if (!cache.count(q.key)) {
@@ -1157,6 +1204,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                     b.checksum = q->key.mode;
                     b.dec_pkt_size = q->key.dec_pkt_size;
                     b.want_shards = true;
+                    b.wrap = 1;
                     b.need = round ? (size_t)b.dec_pkt_size + 4 : 0;
                     db.push_back(std::move(b));
                     reqs.emplace_back();
@@ -1167,18 +1215,15 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 }
                 UnpackBatch& b = db[(size_t)bi];
                 const int g = b.groups++;
-                for (auto& sh : q->shards) b.rows.push_back(UnpackRow{g, sh.second, sh.first, 1});
+                for (auto& sh : q->shards) b.rows.push_back(UnpackRow{g, sh.second, sh.first.off, sh.first.len});
                 reqs[(size_t)bi].push_back(q);
             }
-            size_t hend = 0, dend = 0;
-            for (auto& b : db) {
-                unpack_layout(b, dend);
-                hend = b.o_hend;
-                dend = b.o_dend;
-            }
-            if ((rc = z->dec_arena.ensure(hend, dend))) return rc;
+            Stage io{round16(z->io.used)}, work;
+            for (auto& b : db) unpack_layout(b, io, work);
+            if (!z->io.reserve(io.o + 16) || (rc = z->d_io.ensure(io.o + 16)) || (rc = z->d_work.ensure(work.o + 16)))
+                return rc ? rc : QFEC_ENOMEM;
             for (auto& b : db)
-                if ((rc = run_unpack(z, z->dec_arena, b, st))) return rc;
+                if ((rc = run_unpack(z, b, z->d_rx.d, st))) return rc;
             if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
             std::vector<const DecodeReq*> again;
             for (size_t bi = 0; bi < db.size(); ++bi) {
@@ -1187,47 +1232,30 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 const int head = b.checksum ? 4 : 2;
                 // A decode's input rows come back unchanged (zero past their shard), so a
                 // delivered payload that lies inside its input shard is a view of that shard;
-                // only the rebuilt rows (and payloads reaching past an input's shard) outlive
-                // this round's arena as one owned copy per batch.
-                std::vector<std::pair<size_t, size_t>> copy;  // (row in b.shards, bytes)
-                std::vector<const View*> src_of((size_t)b.k);
-                size_t keep_bytes = 0;
+                // only the rebuilt rows (and payloads reaching past an input's shard) are copied
+                // into the flush's decoded bytes.
                 for (size_t g = 0; g < rq.size(); ++g) {
                     bool cut = false;
                     DecodeOut& o = cache[rq[g]->key];
-                    std::fill(src_of.begin(), src_of.end(), nullptr);
+                    const View* src_of[16] = {};
                     for (auto& sh : rq[g]->shards)
-                        if (sh.second < b.k) src_of[(size_t)sh.second] = &sh.first;
+                        if (sh.second < b.k) src_of[sh.second] = &sh.first;
                     for (int i = 0; i < b.k; ++i) {
                         const int stt = b.status[g * b.k + i], ps = b.psize[g * b.k + i];
                         cut |= stt == -1 && ps < b.dec_pkt_size && (size_t)(head + ps) > b.sp;
                         o.ok[i] = stt >= 0;
                         o.payload[i] = View{};
                         if (stt < 0) continue;
-                        const View* in = src_of[(size_t)i];
+                        const View* in = src_of[i];
                         if (in && (size_t)stt + (size_t)ps <= in->len) {
-                            o.payload[i] = View{in->b, in->off + (uint32_t)stt, (uint32_t)ps};
+                            o.payload[i] = View{SRC_RX, in->off + (uint32_t)stt, (uint32_t)ps};
                         } else {
-                            o.payload[i] = View{nullptr, (uint32_t)keep_bytes, (uint32_t)ps};  // buffer set below
-                            copy.emplace_back((g * b.k + i) * b.sp + (size_t)stt, (size_t)ps);
-                            keep_bytes += (size_t)ps;
+                            o.payload[i] = View{SRC_DEC, (uint32_t)dec_bytes.size(), (uint32_t)ps};
+                            const uint8_t* p = b.shards + (g * b.k + i) * b.sp + (size_t)stt;
+                            dec_bytes.insert(dec_bytes.end(), p, p + ps);
                         }
                     }
                     if (cut && round == 0) again.push_back(rq[g]);
-                }
-                if (!copy.empty()) {
-                    auto keep = std::make_shared<std::vector<uint8_t>>(keep_bytes);
-                    size_t o = 0;
-                    for (auto& c : copy) {
-                        if (c.second) memcpy(keep->data() + o, b.shards + c.first, c.second);
-                        o += c.second;
-                    }
-                    const Buf kb = keep;
-                    for (size_t g = 0; g < rq.size(); ++g) {
-                        DecodeOut& o2 = cache[rq[g]->key];
-                        for (int i = 0; i < b.k; ++i)
-                            if (o2.ok[i] && !o2.payload[i].b) o2.payload[i].b = kb;
-                    }
                 }
             }
             todo.swap(again);
@@ -1240,37 +1268,74 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         }
         if (!all_ok) continue;  // replay with the results
         for (size_t si = 0; si < NS; ++si)  // the assumption held: fill the placeholders
-            for (auto& o : outs[si])
-                for (auto& e : o)
-                    if (e.kind == 3) {
-                        e.kind = 2;
-                        e.v = cache[missing[(size_t)e.batch].key].payload[e.row];
-                    }
+            for (auto& e : rx_out[si])
+                if (e.kind == 3) {
+                    e.kind = 2;
+                    e.v = cache[missing[(size_t)e.batch].key].payload[e.row];
+                }
         break;
     }  // (terminates: a pass that asks for decodes adds their keys to the cache)
-    if (!packs.empty() && hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
-    // ---- callbacks, session by session, op by op
+    // ---- callbacks, session by session, op by op (a send op's emits and a receive op's
+    // deliveries never share an op, so the two lists merge by op index)
+    Bufs B;
+    B.rx = RXA.h;
+    B.tx = TXA.h;
+    B.dec = dec_bytes.data();
+    B.own = &own;
     int calls = 0;
     for (size_t si = 0; si < NS; ++si) {
         Session& S = z->sessions[si];
-        for (size_t oi = 0; oi < S.ops.size(); ++oi) {
-            for (auto& e : outs[si][oi]) {
-                if (e.kind == 0) {
-                    const PackBatch& b = packs[(size_t)e.batch];
-                    const size_t row = (size_t)e.group * b.n + e.row;
-                    if (b.wlen[row] > 0 && pack_out)
-                        pack_out(S.peer, reinterpret_cast<const char*>(b.wire + row * b.wp), (unsigned)b.wlen[row]);
-                } else if (e.kind == 1) {
-                    if (pack_out) pack_out(S.peer, reinterpret_cast<const char*>(e.v.p()), e.v.len);
-                } else if (unpack_out) {
-                    unpack_out(S.peer, reinterpret_cast<const char*>(e.v.p()), e.v.len, e.src);
-                }
-                ++calls;
+        const auto& to = tx_out[si];
+        const auto& ro = rx_out[si];
+        size_t a = 0, c = 0;
+        while (a < to.size() || c < ro.size()) {
+            const bool take_tx = c >= ro.size() || (a < to.size() && to[a].op <= ro[c].op);
+            const Emit& e = take_tx ? to[a++] : ro[c++];
+            if (e.kind == 0) {
+                const PackBatch& b = packs[(size_t)e.batch];
+                const size_t row = (size_t)e.group * b.n + e.row;
+                const int wl = reinterpret_cast<const int*>(z->io.h + b.o_wlen)[row];
+                if (wl > 0 && pack_out)
+                    pack_out(S.peer, reinterpret_cast<const char*>(z->io.h + b.o_wire + row * b.wp), (unsigned)wl);
+            } else if (e.kind == 1) {
+                if (pack_out) pack_out(S.peer, reinterpret_cast<const char*>(B.p(e.v, si)), e.v.len);
+            } else if (unpack_out) {
+                unpack_out(S.peer, reinterpret_cast<const char*>(B.p(e.v, si)), e.v.len, e.src);
             }
+            ++calls;
         }
         S.ops.clear();
     }
     phase("callbacks");
+    // ---- what the state still refers to moves to the spare arenas: the window slots'
+    // datagrams and the open send groups' payloads; everything else is dropped
+    {
+        HostArena& NR = z->rx[z->rxc ^ 1];
+        NR.used = 0;
+        for (auto& S : z->sessions)
+            for (auto& s : S.rx.slots) {
+                if (!s.bValid) continue;
+                uint32_t no = 0;
+                if (!NR.append(RXA.h + s.dg_off, s.dg_len, &no)) return QFEC_ENOMEM;
+                const uint32_t delta = no - s.dg_off;  // (mod 2^32: offsets move together)
+                s.dg_off = no;
+                s.shard.off += delta;
+                s.payload.off += delta;
+            }
+        RXA.used = 0;
+        z->rxc ^= 1;
+        HostArena& NT = z->tx[z->txc ^ 1];
+        NT.used = 0;
+        for (auto& S : z->sessions)
+            for (auto& p : S.tx.g_pay) {
+                uint32_t no = 0;
+                if (!NT.append(TXA.h + p.off, p.len, &no)) return QFEC_ENOMEM;
+                p.off = no;
+            }
+        TXA.used = 0;
+        z->txc ^= 1;
+    }
+    phase("compact");
     return calls;
 }
 

@@ -126,6 +126,31 @@ int qfec_unpack_datagrams(qfec_code* code, const unsigned char* wire, long long 
     return QFEC_OK;
 }
 
+// qfec_gather_rows (qfec_wire.hip k_gather_rows): rows copied into the pitched batch, an 0xEC
+// header synthesized in front of bare shards (wrap_n > 0)
+int qfec_gather_rows(const unsigned char* base, const unsigned long long* off, const int* len, long long rows, int wrap_n,
+                     int wrap_k, unsigned char* out, long long out_pitch, int* out_len, void*) {
+    const int H = wrap_n > 0 ? 11 : 0;
+    for (long long r = 0; r < rows; ++r) {
+        const int n = len[r];
+        if (n <= 0 || H + n > out_pitch) {
+            out_len[r] = n <= 0 ? 0 : -1;
+            continue;
+        }
+        uint8_t* dst = out + r * out_pitch;
+        memset(dst, 0, (size_t)out_pitch);
+        if (H) {
+            const unsigned ikn = (unsigned)wrap_n | (unsigned)wrap_k << 4 | (unsigned)(r % wrap_n) << 8;
+            dst[0] = 0xEC;
+            dst[9] = (uint8_t)(ikn & 0xFF);
+            dst[10] = (uint8_t)(ikn >> 8);
+        }
+        memcpy(dst + H, base + off[r], (size_t)n);
+        out_len[r] = H + n;
+    }
+    return QFEC_OK;
+}
+
 // the HIP runtime, as host memory
 hipError_t hipMalloc(void** p, size_t n) {
     *p = malloc(n);
@@ -154,6 +179,7 @@ hipError_t hipHostFree(void* p) {
     free(p);
     return hipSuccess;
 }
+hipError_t hipGetLastError(void) { return hipSuccess; }
 hipError_t hipGetDevice(int* d) {
     *d = 0;
     return hipSuccess;

@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
 """Rate of the exact NetFecCodec layer (include/qfec_zfec.h) on one GPU: S sender sessions
-packing P payloads each, one flush; their datagrams (a fraction dropped) into S receiver
-sessions, one flush.  Prints payload GiB/s and packets/s for each flush and checks every
-payload arrives (n - k losses per group are recoverable).
+packing P payloads each, one flush; their datagrams (a fraction dropped, at most n - k per
+group so every payload is recoverable) into S receiver sessions, one flush.  Both flushes call
+C callbacks (tools/zfec_sink.c: the send side copies every datagram out, as a socket layer
+would; the receive side counts and byte-sums every delivery), so the numbers are the layer's,
+not Python's.  Prints payload GiB/s and packets/s per flush, and checks that every payload
+arrived (count, bytes and byte sum).
 
   python tools/zfec_rate.py [--sessions 64 --packets 2000 --size 1024 --k 10 --n 13 --loss 0.1]
+  --json: one JSON line with the best rep (bench.py's zfec field)
 """
 import argparse
+import ctypes as C
+import json
 import os
 import random
+import subprocess
 import sys
 import time
 
@@ -16,6 +23,79 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import quicknet_amd as qa  # noqa: E402
+from quicknet_amd.codec import _PACK_OUT, _UNPACK_OUT  # noqa: E402
+
+SINK_SRC = os.path.join(ROOT, "tools", "zfec_sink.c")
+SINK_SO = os.path.join(ROOT, "tools", "_build", "libzfec_sink.so")
+
+
+def load_sink():
+    if not os.path.exists(SINK_SO) or os.path.getmtime(SINK_SO) < os.path.getmtime(SINK_SRC):
+        os.makedirs(os.path.dirname(SINK_SO), exist_ok=True)
+        subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", SINK_SO, SINK_SRC], check=True)
+    s = C.CDLL(SINK_SO)
+    for f, t in (("sink_count", C.c_size_t), ("sink_buf", C.c_void_p), ("sink_offs", C.c_void_p),
+                 ("sink_lens", C.c_void_p), ("sink_peers", C.c_void_p), ("sink_ndeliv", C.c_ulonglong),
+                 ("sink_dbytes", C.c_ulonglong), ("sink_dsum", C.c_ulonglong)):
+        getattr(s, f).restype = t
+    return s
+
+
+def run(a, sink, rep, pay):
+    import numpy as np
+    rng = random.Random(100 + rep)
+    L = qa.lib()
+    pack_cb = _PACK_OUT(C.cast(sink.sink_pack, C.c_void_p).value)
+    unpack_cb = _UNPACK_OUT(C.cast(sink.sink_unpack, C.c_void_p).value)
+    z = qa.Zfec()
+    tx = [z.session(max_pkt_size=2048, kmax=15, k=a.k, n=a.n, is_sorted=bool(a.sorted)) for _ in range(a.sessions)]
+    rx = [z.session(max_pkt_size=2048, kmax=15, k=a.k, n=a.n, is_sorted=bool(a.sorted)) for _ in range(a.sessions)]
+    t0 = time.perf_counter()
+    expect_sum = 0
+    for i, s in enumerate(tx):
+        for p in range(a.packets):
+            j = (i * 7 + p) % len(pay)
+            z.pack_input(s, pay[j][0])
+            expect_sum += pay[j][1]
+    t1 = time.perf_counter()
+    sink.sink_reset()
+    rc = L.qfec_zfec_flush(z._h, pack_cb, unpack_cb, None)
+    t2 = time.perf_counter()
+    assert rc >= 0, rc
+    cnt = sink.sink_count()
+    buf = C.string_at(sink.sink_buf(), int(np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_offs()))[-1])
+                      + int(np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_lens()))[-1]))
+    offs = np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_offs())).copy()
+    lens = np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_lens())).copy()
+    peers = np.ctypeslib.as_array((C.c_ssize_t * cnt).from_address(sink.sink_peers())).copy()
+    per = {}
+    for o, ln, pr in zip(offs, lens, peers):
+        per.setdefault(int(pr) - 1, []).append(buf[int(o):int(o) + int(ln)])
+    nlost = min(a.n - a.k, int(round(a.loss * a.n)))
+    for i, s in enumerate(tx):
+        ds = per.get(s, [])
+        for g0 in range(0, len(ds), a.n):
+            grp = ds[g0:g0 + a.n]
+            drop = set(rng.sample(range(len(grp)), min(len(grp), nlost)))
+            for j, d in enumerate(grp):
+                if j not in drop:
+                    z.unpack_input(rx[i], d)
+    t3 = time.perf_counter()
+    sink.sink_reset()
+    rc = L.qfec_zfec_flush(z._h, pack_cb, unpack_cb, None)
+    t4 = time.perf_counter()
+    assert rc >= 0, rc
+    npk = a.sessions * a.packets
+    by = npk * a.size
+    ok = sink.sink_ndeliv() == npk and sink.sink_dbytes() == by and sink.sink_dsum() == expect_sum
+    z.close()
+    return {"sessions": a.sessions, "packets_per_session": a.packets, "payload_bytes": a.size, "k": a.k, "n": a.n,
+            "loss": a.loss, "dropped_per_group": nlost, "sorted": bool(a.sorted), "datagrams": int(cnt),
+            "queue_tx_s": round(t1 - t0, 4), "send_flush_s": round(t2 - t1, 4),
+            "send_gibs": round(by / (t2 - t1) / 2**30, 3), "send_mpkts": round(npk / (t2 - t1) / 1e6, 3),
+            "queue_rx_s": round(t3 - t2, 4), "recv_flush_s": round(t4 - t3, 4),
+            "recv_gibs": round(by / (t4 - t3) / 2**30, 3), "recv_mpkts": round(npk / (t4 - t3) / 1e6, 3),
+            "delivered": int(sink.sink_ndeliv()), "verified": bool(ok)}
 
 
 def main():
@@ -28,50 +108,28 @@ def main():
     ap.add_argument("--loss", type=float, default=0.1)
     ap.add_argument("--sorted", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--callbacks", type=int, default=0, help="1: time the receive flush with Python callbacks")
+    ap.add_argument("--json", action="store_true")
     a = ap.parse_args()
-    rng = random.Random(1)
-    pay = [rng.randbytes(a.size) for _ in range(257)]
+    sink = load_sink()
+    r = random.Random(1)
+    pay = []
+    for _ in range(257):
+        b = r.randbytes(a.size)
+        pay.append((b, sum(b)))
+    best = None
     for rep in range(a.reps):
-        z = qa.Zfec()
-        tx = [z.session(max_pkt_size=2048, kmax=15, k=a.k, n=a.n, is_sorted=bool(a.sorted)) for _ in range(a.sessions)]
-        rx = [z.session(max_pkt_size=2048, kmax=15, k=a.k, n=a.n, is_sorted=bool(a.sorted)) for _ in range(a.sessions)]
-        t0 = time.perf_counter()
-        for i, s in enumerate(tx):
-            for p in range(a.packets):
-                z.pack_input(s, pay[(i * 7 + p) % 257])
-        t1 = time.perf_counter()
-        sent, _ = z.flush()
-        t2 = time.perf_counter()
-        # drop at most n - k per group so every payload is recoverable
-        per = {}
-        for sess, d in sent:
-            per.setdefault(sess, []).append(d)
-        for i, s in enumerate(tx):
-            ds = per.get(s, [])
-            for g0 in range(0, len(ds), a.n):
-                grp = ds[g0:g0 + a.n]
-                drop = set(rng.sample(range(len(grp)), min(a.n - a.k, int(round(a.loss * len(grp))))))
-                for j, d in enumerate(grp):
-                    if j not in drop:
-                        z.unpack_input(rx[i], d)
-        t3 = time.perf_counter()
-        if a.callbacks:
-            _, got = z.flush()
-            ndel = len(got)
-        else:  # the layer alone: no callbacks, the return value counts the deliveries
-            ndel = z._L.qfec_zfec_flush(z._h, None, None, None)
-        t4 = time.perf_counter()
-        npk = a.sessions * a.packets
-        by = npk * a.size
-        ok = ndel == npk
-        got = range(ndel)
-        print(f"rep {rep}: {a.sessions} sessions x {a.packets} x {a.size} B, RS({a.k},{a.n}), loss {a.loss}: "
-              f"queue {t1 - t0:.3f}s, pack flush {t2 - t1:.3f}s ({by / (t2 - t1) / 2**30:.2f} GiB/s, "
-              f"{npk / (t2 - t1) / 1e6:.2f} Mpkt/s), queue rx {t3 - t2:.3f}s, unpack flush {t4 - t3:.3f}s "
-              f"({by / (t4 - t3) / 2**30:.2f} GiB/s, {npk / (t4 - t3) / 1e6:.2f} Mpkt/s), delivered {len(got)} ok={ok}",
-              flush=True)
-        z.close()
+        res = run(a, sink, rep, pay)
+        if not a.json:
+            print(f"rep {rep}: {a.sessions} sessions x {a.packets} x {a.size} B, RS({a.k},{a.n}), loss {a.loss} "
+                  f"({res['dropped_per_group']} of {a.n} per group): queue {res['queue_tx_s']:.3f}s, send flush "
+                  f"{res['send_flush_s']:.4f}s ({res['send_gibs']:.2f} GiB/s, {res['send_mpkts']:.2f} Mpkt/s), "
+                  f"queue rx {res['queue_rx_s']:.3f}s, receive flush {res['recv_flush_s']:.4f}s "
+                  f"({res['recv_gibs']:.2f} GiB/s, {res['recv_mpkts']:.2f} Mpkt/s), delivered {res['delivered']} "
+                  f"verified={res['verified']}", flush=True)
+        if best is None or res["send_gibs"] + res["recv_gibs"] > best["send_gibs"] + best["recv_gibs"]:
+            best = res
+    if a.json:
+        print(json.dumps(best), flush=True)
 
 
 if __name__ == "__main__":
