@@ -189,7 +189,10 @@ def test_unpack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session):
                 if status[g, i] >= 0:
                     sz = psize[g, i]
                     assert np.array_equal(sh[g, i, :head + sz], want[0][g, i, :head + sz]), (g, i)
-                    if (g, i) not in kinds:
+                    # without checksums a corrupted shard inside a good frame is undetectable: the
+                    # group then decodes garbage (as the reference would); no truth check for it
+                    silent = not checksum and any(kg == g and kd == 5 for (kg, _), kd in kinds.items())
+                    if (g, i) not in kinds and not silent:
                         assert sz == sizes[g * k + i]
                         o = offs[g * k + i]
                         assert np.array_equal(sh[g, i, head:head + sz], payload[o:o + sz]), (g, i)
