@@ -358,7 +358,8 @@ struct UnpackBatch {
     int k, n, checksum, dec_pkt_size;
     int groups = 0;
     int wrap = 0;              // decodes: rows are shards (an 0xEC header synthesized on the device)
-    bool want_shards = false;  // decodes: the data rows come back
+    bool want_shards = false;  // decodes: rows of the shard matrix come back (`fetch`)
+    std::vector<uint32_t> fetch;  // decodes: the rows (g * n + i) to bring back, in this order
     size_t need = 0;           // row bytes dec_src_pkt_info may read (head + size field), if known
     std::vector<UnpackRow> rows;
     size_t sp = 0, wp = 0;
@@ -367,7 +368,8 @@ struct UnpackBatch {
     // device work buffer: gathered wire, its lengths, marks, shard matrix
     size_t w_wire = 0, w_wlen = 0, w_marks = 0, w_sh = 0;
     const int *rx = nullptr, *status = nullptr, *psize = nullptr;
-    const uint8_t* shards = nullptr;  // want_shards: the data rows, [G][k][sp]
+    const uint8_t* shards = nullptr;  // want_shards: the fetched rows, [fetch.size()][sp]
+    size_t o_foff = 0, o_flen = 0, w_cmp = 0;
 };
 
 // shard rows hold every shard and every byte dec_src_pkt_info may read (the reference's buffers
@@ -385,7 +387,11 @@ void unpack_layout(UnpackBatch& b, Stage& io, Stage& work) {
     b.o_rx = io.take(R * 4);
     b.o_st = io.take(G * b.k * 4);
     b.o_ps = io.take(G * b.k * 4);
-    b.o_hsh = b.want_shards ? io.take(G * b.k * b.sp) : 0;
+    const size_t F = b.fetch.size();
+    b.o_hsh = b.want_shards ? io.take(F * b.sp) : 0;
+    b.o_foff = b.want_shards ? io.take(F * 8) : 0;
+    b.o_flen = b.want_shards ? io.take(F * 4) : 0;
+    b.w_cmp = b.want_shards ? work.take(F * b.sp + 16) : 0;
     b.w_wire = work.take(R * b.wp);
     b.w_wlen = work.take(R * 4);
     b.w_marks = work.take(R);
@@ -420,10 +426,23 @@ int run_unpack(qfec_zfec* z, UnpackBatch& b, const uint8_t* d_rx, hipStream_t s)
     if (rc) return rc;
     if (hipMemcpyAsync(h + b.o_rx, d + b.o_rx, (b.o_ps + G * b.k * 4) - b.o_rx, hipMemcpyDeviceToHost, s) != hipSuccess)
         return QFEC_EHIP;
-    if (b.want_shards &&  // the k data rows of each group only
-        hipMemcpy2DAsync(h + b.o_hsh, (size_t)b.k * b.sp, w + b.w_sh, (size_t)b.n * b.sp, (size_t)b.k * b.sp, G,
-                         hipMemcpyDeviceToHost, s) != hipSuccess)
-        return QFEC_EHIP;
+    if (b.want_shards && !b.fetch.empty()) {  // only the rows asked for, gathered on the device first
+        const size_t F = b.fetch.size();
+        unsigned long long* fo = reinterpret_cast<unsigned long long*>(h + b.o_foff);
+        int* fl = reinterpret_cast<int*>(h + b.o_flen);
+        for (size_t i = 0; i < F; ++i) {
+            fo[i] = (unsigned long long)b.fetch[i] * b.sp;
+            fl[i] = (int)b.sp;
+        }
+        if (hipMemcpyAsync(d + b.o_foff, h + b.o_foff, b.o_flen + F * 4 - b.o_foff, hipMemcpyHostToDevice, s) !=
+            hipSuccess)
+            return QFEC_EHIP;
+        rc = qfec_gather_rows(w + b.w_sh, reinterpret_cast<const unsigned long long*>(d + b.o_foff),
+                              reinterpret_cast<const int*>(d + b.o_flen), (long long)F, 0, 0, w + b.w_cmp,
+                              (long long)b.sp, reinterpret_cast<int*>(d + b.o_flen), s);
+        if (rc) return rc;
+        if (hipMemcpyAsync(h + b.o_hsh, w + b.w_cmp, F * b.sp, hipMemcpyDeviceToHost, s) != hipSuccess) return QFEC_EHIP;
+    }
     b.rx = reinterpret_cast<const int*>(h + b.o_rx);
     b.status = reinterpret_cast<const int*>(h + b.o_st);
     b.psize = reinterpret_cast<const int*>(h + b.o_ps);
@@ -952,6 +971,11 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         t_prev = t;
     };
     hipStream_t st = (hipStream_t)stream;
+    auto tsync = [&](const char* name) {  // timing only: attribute the stream's work to its phase
+        if (!timing) return;
+        (void)hipStreamSynchronize(st);
+        phase(name);
+    };
     const size_t NS = z->sessions.size();
     HostArena& RXA = z->rx[z->rxc];
     HostArena& TXA = z->tx[z->txc];
@@ -1016,8 +1040,13 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             (rc = z->d_tx.ensure(TXA.used + 16)))
             return rc ? rc : QFEC_ENOMEM;
         if (hipMemcpyAsync(z->d_tx.d, TXA.h, TXA.used + 16, hipMemcpyHostToDevice, st) != hipSuccess) return QFEC_EHIP;
+        tsync("pack h2d");
         uint8_t* h = z->io.h;
         uint8_t* d = z->d_io.d;
+        // QFEC_ZFEC_TX_ZC=1 (A/B): the kernels write the datagrams straight into the pinned io
+        // arena over PCIe instead of HBM + one copy back
+        static const bool tx_zc = getenv("QFEC_ZFEC_TX_ZC") && atoi(getenv("QFEC_ZFEC_TX_ZC")) == 1;
+        const bool zc = tx_zc && z->io.pinned;
         for (auto& b : packs) {
             const size_t G = b.groups.size();
             long long* offs = reinterpret_cast<long long*>(h + b.o_offs);
@@ -1034,16 +1063,22 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             }
             if (hipMemcpyAsync(d + b.o_offs, h + b.o_offs, b.o_wlen - b.o_offs, hipMemcpyHostToDevice, st) != hipSuccess)
                 return QFEC_EHIP;
+            uint8_t* out = zc ? h : d;
             if ((rc = qfec_pack_datagrams(code_for(z, b.k, b.n), z->d_tx.d, reinterpret_cast<const long long*>(d + b.o_offs),
                                           reinterpret_cast<const int*>(d + b.o_sizes),
                                           reinterpret_cast<const unsigned int*>(d + b.o_seq), (long long)G,
                                           1 /* is_send_checksum */, z->d_work.d + b.d_shards, (long long)b.sp,
-                                          d + b.o_wire, (long long)b.wp, reinterpret_cast<int*>(d + b.o_wlen), st)))
+                                          out + b.o_wire, (long long)b.wp, reinterpret_cast<int*>(out + b.o_wlen), st)))
                 return rc;
-            if (hipMemcpyAsync(h + b.o_wlen, d + b.o_wlen, b.o_wire + G * b.n * b.wp - b.o_wlen, hipMemcpyDeviceToHost,
-                               st) != hipSuccess)
-                return QFEC_EHIP;
         }
+        tsync("pack kernels");
+        if (!zc)
+            for (auto& b : packs) {
+                const size_t G = b.groups.size();
+                if (hipMemcpyAsync(h + b.o_wlen, d + b.o_wlen, b.o_wire + G * b.n * b.wp - b.o_wlen, hipMemcpyDeviceToHost,
+                                   st) != hipSuccess)
+                    return QFEC_EHIP;
+            }
         z->io.used = io.o;  // the datagrams stay until the callbacks (the receive stages go after)
         if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
     }
@@ -1117,6 +1152,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     if (!vb.empty()) {
         if ((rc = z->d_rx.ensure(RXA.used + 16))) return rc;
         if (hipMemcpyAsync(z->d_rx.d, RXA.h, RXA.used + 16, hipMemcpyHostToDevice, st) != hipSuccess) return QFEC_EHIP;
+        tsync("rx h2d");
     }
     if (!vb.empty()) {
         Stage io{round16(z->io.used)}, work;
@@ -1215,7 +1251,13 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 }
                 UnpackBatch& b = db[(size_t)bi];
                 const int g = b.groups++;
-                for (auto& sh : q->shards) b.rows.push_back(UnpackRow{g, sh.second, sh.first.off, sh.first.len});
+                uint32_t have = 0;
+                for (auto& sh : q->shards) {
+                    b.rows.push_back(UnpackRow{g, sh.second, sh.first.off, sh.first.len});
+                    have |= 1u << sh.second;
+                }
+                for (int i = 0; i < b.k; ++i)  // the rebuilt rows come back; inputs are views
+                    if (!((have >> i) & 1u)) b.fetch.push_back((uint32_t)(g * b.n + i));
                 reqs[(size_t)bi].push_back(q);
             }
             Stage io{round16(z->io.used)}, work;
@@ -1230,6 +1272,8 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 const UnpackBatch& b = db[bi];
                 const auto& rq = reqs[bi];
                 const int head = b.checksum ? 4 : 2;
+                std::vector<int> fidx((size_t)b.groups * b.n, -1);  // row -> its fetched copy
+                for (size_t f = 0; f < b.fetch.size(); ++f) fidx[b.fetch[f]] = (int)f;
                 // A decode's input rows come back unchanged (zero past their shard), so a
                 // delivered payload that lies inside its input shard is a view of that shard;
                 // only the rebuilt rows (and payloads reaching past an input's shard) are copied
@@ -1251,8 +1295,19 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                             o.payload[i] = View{SRC_RX, in->off + (uint32_t)stt, (uint32_t)ps};
                         } else {
                             o.payload[i] = View{SRC_DEC, (uint32_t)dec_bytes.size(), (uint32_t)ps};
-                            const uint8_t* p = b.shards + (g * b.k + i) * b.sp + (size_t)stt;
-                            dec_bytes.insert(dec_bytes.end(), p, p + ps);
+                            const int fi = fidx[g * b.n + (size_t)i];
+                            if (fi >= 0) {
+                                const uint8_t* p = b.shards + (size_t)fi * b.sp + (size_t)stt;
+                                dec_bytes.insert(dec_bytes.end(), p, p + ps);
+                            } else {  // an input whose size field reaches past its shard (corrupt): rare
+                                const size_t at = dec_bytes.size();
+                                dec_bytes.resize(at + (size_t)ps);
+                                if (ps && (hipMemcpyAsync(dec_bytes.data() + at,
+                                                          z->d_work.d + b.w_sh + (g * b.n + (size_t)i) * b.sp + (size_t)stt,
+                                                          (size_t)ps, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                                           hipStreamSynchronize(st) != hipSuccess))
+                                    return QFEC_EHIP;
+                            }
                         }
                     }
                     if (cut && round == 0) again.push_back(rq[g]);

@@ -3,9 +3,10 @@
 packing P payloads each, one flush; their datagrams (a fraction dropped, at most n - k per
 group so every payload is recoverable) into S receiver sessions, one flush.  Both flushes call
 C callbacks (tools/zfec_sink.c: the send side copies every datagram out, as a socket layer
-would; the receive side counts and byte-sums every delivery), so the numbers are the layer's,
-not Python's.  Prints payload GiB/s and packets/s per flush, and checks that every payload
-arrived (count, bytes and byte sum).
+would; the receive side copies every delivery into an application ring and folds it into a
+sum of 64-bit words), so the numbers are the layer's, not Python's.  Prints payload GiB/s and
+packets/s per flush, and checks that every payload arrived (count, bytes, and the word sum of
+all payloads sent).
 
   python tools/zfec_rate.py [--sessions 64 --packets 2000 --size 1024 --k 10 --n 13 --loss 0.1]
   --json: one JSON line with the best rep (bench.py's zfec field)
@@ -34,9 +35,10 @@ def load_sink():
         os.makedirs(os.path.dirname(SINK_SO), exist_ok=True)
         subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", SINK_SO, SINK_SRC], check=True)
     s = C.CDLL(SINK_SO)
+    s.sink_fold.argtypes = [C.c_char_p, C.c_uint]
     for f, t in (("sink_count", C.c_size_t), ("sink_buf", C.c_void_p), ("sink_offs", C.c_void_p),
                  ("sink_lens", C.c_void_p), ("sink_peers", C.c_void_p), ("sink_ndeliv", C.c_ulonglong),
-                 ("sink_dbytes", C.c_ulonglong), ("sink_dsum", C.c_ulonglong)):
+                 ("sink_dbytes", C.c_ulonglong), ("sink_dsum", C.c_ulonglong), ("sink_fold", C.c_ulonglong)):
         getattr(s, f).restype = t
     return s
 
@@ -87,7 +89,7 @@ def run(a, sink, rep, pay):
     assert rc >= 0, rc
     npk = a.sessions * a.packets
     by = npk * a.size
-    ok = sink.sink_ndeliv() == npk and sink.sink_dbytes() == by and sink.sink_dsum() == expect_sum
+    ok = sink.sink_ndeliv() == npk and sink.sink_dbytes() == by and sink.sink_dsum() == expect_sum % 2**64
     z.close()
     return {"sessions": a.sessions, "packets_per_session": a.packets, "payload_bytes": a.size, "k": a.k, "n": a.n,
             "loss": a.loss, "dropped_per_group": nlost, "sorted": bool(a.sorted), "datagrams": int(cnt),
@@ -115,7 +117,7 @@ def main():
     pay = []
     for _ in range(257):
         b = r.randbytes(a.size)
-        pay.append((b, sum(b)))
+        pay.append((b, int(sink.sink_fold(b, len(b)))))
     best = None
     for rep in range(a.reps):
         res = run(a, sink, rep, pay)
