@@ -804,15 +804,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         uint4 v = r < K ? x[r] : acc[r - K];
         if (r >= K) ps[r] = sum16(v, 0);
         if constexpr (FP != 0) {  // XOR the frame's bytes only: padding past it stays 0
-            // the words of the row's last chunk depend on the row alone (scalar for GPW 1);
-            // per lane it is a select: inside, the last chunk, or past the frame
             const int total = FP + HDR + (r < K ? size[r] + HEAD : gmax);
-            const int tend = total >> 4, nend = total & 15;
-            const uint32_t e0 = mm[r] & byte_mask(0, nend, 0), e1 = mm[r] & byte_mask(0, nend, 1),
-                           e2 = mm[r] & byte_mask(0, nend, 2), e3 = mm[r] & byte_mask(0, nend, 3);
-            const bool in = t < tend, last = t == tend;
-            v = make_uint4(v.x ^ (in ? mm[r] : last ? e0 : 0u), v.y ^ (in ? mm[r] : last ? e1 : 0u),
-                           v.z ^ (in ? mm[r] : last ? e2 : 0u), v.w ^ (in ? mm[r] : last ? e3 : 0u));
+            v = make_uint4(v.x ^ (mm[r] & byte_mask(0, total - 16 * t, 0)), v.y ^ (mm[r] & byte_mask(0, total - 16 * t, 1)),
+                           v.z ^ (mm[r] & byte_mask(0, total - 16 * t, 2)), v.w ^ (mm[r] & byte_mask(0, total - 16 * t, 3)));
         }
         if (ok) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
     }

@@ -1264,9 +1264,11 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             for (auto& b : db) unpack_layout(b, io, work);
             if (!z->io.reserve(io.o + 16) || (rc = z->d_io.ensure(io.o + 16)) || (rc = z->d_work.ensure(work.o + 16)))
                 return rc ? rc : QFEC_ENOMEM;
+            phase("decode plan");
             for (auto& b : db)
                 if ((rc = run_unpack(z, b, z->d_rx.d, st))) return rc;
             if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
+            phase("decode launch");
             std::vector<const DecodeReq*> again;
             for (size_t bi = 0; bi < db.size(); ++bi) {
                 const UnpackBatch& b = db[bi];
@@ -1315,7 +1317,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             }
             todo.swap(again);
         }
-        phase("decodes");
+        phase("decode results");
         bool all_ok = true;
         for (auto& q : missing) {
             const DecodeOut& o = cache[q.key];

@@ -14,5 +14,4 @@ QFEC_ZFEC_TIMING=1 timeout -k 10 300 python tools/zfec_rate.py > $OUT/rate.txt 2
 cat $OUT/rate.txt
 timeout -k 10 300 python tools/zfec_rate.py --sorted 1 --reps 2 > $OUT/rate_sorted.txt 2>&1 || { tail -40 $OUT/rate_sorted.txt; exit 4; }
 cat $OUT/rate_sorted.txt
-QFEC_ZFEC_TIMING=1 QFEC_ZFEC_TX_ZC=1 timeout -k 10 300 python tools/zfec_rate.py --reps 2 > $OUT/rate_txzc.txt 2>&1 || { tail -40 $OUT/rate_txzc.txt; exit 5; }
-cat $OUT/rate_txzc.txt
+

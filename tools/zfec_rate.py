@@ -2,9 +2,10 @@
 """Rate of the exact NetFecCodec layer (include/qfec_zfec.h) on one GPU: S sender sessions
 packing P payloads each, one flush; their datagrams (a fraction dropped, at most n - k per
 group so every payload is recoverable) into S receiver sessions, one flush.  Both flushes call
-C callbacks (tools/zfec_sink.c: the send side copies every datagram out, as a socket layer
-would; the receive side copies every delivery into an application ring and folds it into a
-sum of 64-bit words), so the numbers are the layer's, not Python's.  Prints payload GiB/s and
+C callbacks (tools/zfec_sink.c: the send side hands every datagram it does not drop straight to
+a second context's qfec_zfec_unpack_input -- one copy, as a socket would make; the receive side
+folds every delivery into a sum of 64-bit words where it lies), so the numbers are the layer's,
+not Python's.  The contexts live across reps (rep 0 allocates their arenas and is not the best).  Prints payload GiB/s and
 packets/s per flush, and checks that every payload arrived (count, bytes, and the word sum of
 all payloads sent).
 
@@ -36,6 +37,7 @@ def load_sink():
         subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-o", SINK_SO, SINK_SRC], check=True)
     s = C.CDLL(SINK_SO)
     s.sink_fold.argtypes = [C.c_char_p, C.c_uint]
+    s.sink_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
     for f, t in (("sink_count", C.c_size_t), ("sink_buf", C.c_void_p), ("sink_offs", C.c_void_p),
                  ("sink_lens", C.c_void_p), ("sink_peers", C.c_void_p), ("sink_ndeliv", C.c_ulonglong),
                  ("sink_dbytes", C.c_ulonglong), ("sink_dsum", C.c_ulonglong), ("sink_fold", C.c_ulonglong)):
@@ -43,61 +45,62 @@ def load_sink():
     return s
 
 
-def run(a, sink, rep, pay):
-    import numpy as np
-    rng = random.Random(100 + rep)
-    L = qa.lib()
-    pack_cb = _PACK_OUT(C.cast(sink.sink_pack, C.c_void_p).value)
-    unpack_cb = _UNPACK_OUT(C.cast(sink.sink_unpack, C.c_void_p).value)
-    z = qa.Zfec()
-    tx = [z.session(max_pkt_size=2048, kmax=15, k=a.k, n=a.n, is_sorted=bool(a.sorted)) for _ in range(a.sessions)]
-    rx = [z.session(max_pkt_size=2048, kmax=15, k=a.k, n=a.n, is_sorted=bool(a.sorted)) for _ in range(a.sessions)]
+def zlib(a):
+    """libqfec, or (--host-stub, CPU check of this tool) the CPU build of tests/test_zfec_host.py"""
+    if not a.host_stub:
+        return qa.lib()
+    from quicknet_amd._lib import bind_zfec
+    return bind_zfec(C.CDLL(os.path.join(ROOT, "tests", "zfec_host", "_build", "libzfec_host.so")))
+
+
+def run(a, sink, st, rep, pay):
+    """One rep on the contexts in `st` (created once: their arenas stay warm, as a long-lived
+    transport's would).  The send flush's C callback forwards every datagram it keeps straight
+    into the receiving context (qfec_zfec_unpack_input), so the send flush includes handing the
+    datagrams over; the receive flush's callback folds every payload where it lies."""
+    L = st["L"]
+    ztx, zrx, tx, rx = st["ztx"], st["zrx"], st["tx"], st["rx"]
     t0 = time.perf_counter()
     expect_sum = 0
     for i, s in enumerate(tx):
         for p in range(a.packets):
-            j = (i * 7 + p) % len(pay)
-            z.pack_input(s, pay[j][0])
+            j = (i * 7 + p + rep) % len(pay)
+            ztx.pack_input(s, pay[j][0])
             expect_sum += pay[j][1]
     t1 = time.perf_counter()
     sink.sink_reset()
-    rc = L.qfec_zfec_flush(z._h, pack_cb, unpack_cb, None)
+    rc = L.qfec_zfec_flush(ztx._h, st["fwd"], st["fold"], None)
     t2 = time.perf_counter()
     assert rc >= 0, rc
     cnt = sink.sink_count()
-    buf = C.string_at(sink.sink_buf(), int(np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_offs()))[-1])
-                      + int(np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_lens()))[-1]))
-    offs = np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_offs())).copy()
-    lens = np.ctypeslib.as_array((C.c_uint32 * cnt).from_address(sink.sink_lens())).copy()
-    peers = np.ctypeslib.as_array((C.c_ssize_t * cnt).from_address(sink.sink_peers())).copy()
-    per = {}
-    for o, ln, pr in zip(offs, lens, peers):
-        per.setdefault(int(pr) - 1, []).append(buf[int(o):int(o) + int(ln)])
-    nlost = min(a.n - a.k, int(round(a.loss * a.n)))
-    for i, s in enumerate(tx):
-        ds = per.get(s, [])
-        for g0 in range(0, len(ds), a.n):
-            grp = ds[g0:g0 + a.n]
-            drop = set(rng.sample(range(len(grp)), min(len(grp), nlost)))
-            for j, d in enumerate(grp):
-                if j not in drop:
-                    z.unpack_input(rx[i], d)
-    t3 = time.perf_counter()
     sink.sink_reset()
-    rc = L.qfec_zfec_flush(z._h, pack_cb, unpack_cb, None)
-    t4 = time.perf_counter()
+    rc = L.qfec_zfec_flush(zrx._h, st["fwd"], st["fold"], None)
+    t3 = time.perf_counter()
     assert rc >= 0, rc
     npk = a.sessions * a.packets
     by = npk * a.size
     ok = sink.sink_ndeliv() == npk and sink.sink_dbytes() == by and sink.sink_dsum() == expect_sum % 2**64
-    z.close()
     return {"sessions": a.sessions, "packets_per_session": a.packets, "payload_bytes": a.size, "k": a.k, "n": a.n,
-            "loss": a.loss, "dropped_per_group": nlost, "sorted": bool(a.sorted), "datagrams": int(cnt),
+            "loss": a.loss, "dropped_per_group": st["nlost"], "sorted": bool(a.sorted), "datagrams_kept": int(cnt),
             "queue_tx_s": round(t1 - t0, 4), "send_flush_s": round(t2 - t1, 4),
             "send_gibs": round(by / (t2 - t1) / 2**30, 3), "send_mpkts": round(npk / (t2 - t1) / 1e6, 3),
-            "queue_rx_s": round(t3 - t2, 4), "recv_flush_s": round(t4 - t3, 4),
-            "recv_gibs": round(by / (t4 - t3) / 2**30, 3), "recv_mpkts": round(npk / (t4 - t3) / 1e6, 3),
+            "recv_flush_s": round(t3 - t2, 4),
+            "recv_gibs": round(by / (t3 - t2) / 2**30, 3), "recv_mpkts": round(npk / (t3 - t2) / 1e6, 3),
             "delivered": int(sink.sink_ndeliv()), "verified": bool(ok)}
+
+
+def setup(a, sink):
+    L = zlib(a)
+    ztx, zrx = qa.Zfec(_lib=L), qa.Zfec(_lib=L)
+    kw = dict(max_pkt_size=2048, kmax=15, k=a.k, n=a.n, is_sorted=bool(a.sorted))
+    tx = [ztx.session(**kw) for _ in range(a.sessions)]
+    rx = [zrx.session(**kw) for _ in range(a.sessions)]
+    nlost = min(a.n - a.k, int(round(a.loss * a.n)))
+    rx_of = (C.c_int * a.sessions)(*rx)
+    sink.sink_forward(zrx._h, C.cast(L.qfec_zfec_unpack_input, C.c_void_p), rx_of, a.sessions, a.n, nlost)
+    return {"L": L, "ztx": ztx, "zrx": zrx, "tx": tx, "rx": rx, "nlost": nlost,
+            "fwd": _PACK_OUT(C.cast(sink.sink_pack_forward, C.c_void_p).value),
+            "fold": _UNPACK_OUT(C.cast(sink.sink_unpack_fold, C.c_void_p).value)}
 
 
 def main():
@@ -109,8 +112,9 @@ def main():
     ap.add_argument("--n", type=int, default=13)
     ap.add_argument("--loss", type=float, default=0.1)
     ap.add_argument("--sorted", type=int, default=0)
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=4)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--host-stub", action="store_true", help="CPU build of the layer (checks this tool without a GPU)")
     a = ap.parse_args()
     sink = load_sink()
     r = random.Random(1)
@@ -119,17 +123,20 @@ def main():
         b = r.randbytes(a.size)
         pay.append((b, int(sink.sink_fold(b, len(b)))))
     best = None
+    st = setup(a, sink)
     for rep in range(a.reps):
-        res = run(a, sink, rep, pay)
+        res = run(a, sink, st, rep, pay)
         if not a.json:
             print(f"rep {rep}: {a.sessions} sessions x {a.packets} x {a.size} B, RS({a.k},{a.n}), loss {a.loss} "
                   f"({res['dropped_per_group']} of {a.n} per group): queue {res['queue_tx_s']:.3f}s, send flush "
                   f"{res['send_flush_s']:.4f}s ({res['send_gibs']:.2f} GiB/s, {res['send_mpkts']:.2f} Mpkt/s), "
-                  f"queue rx {res['queue_rx_s']:.3f}s, receive flush {res['recv_flush_s']:.4f}s "
+                  f"receive flush {res['recv_flush_s']:.4f}s "
                   f"({res['recv_gibs']:.2f} GiB/s, {res['recv_mpkts']:.2f} Mpkt/s), delivered {res['delivered']} "
                   f"verified={res['verified']}", flush=True)
-        if best is None or res["send_gibs"] + res["recv_gibs"] > best["send_gibs"] + best["recv_gibs"]:
-            best = res
+        if rep and (best is None or res["send_gibs"] + res["recv_gibs"] > best["send_gibs"] + best["recv_gibs"]):
+            best = res  # rep 0 pays the arenas' first allocation
+    st["ztx"].close()
+    st["zrx"].close()
     if a.json:
         print(json.dumps(best), flush=True)
 

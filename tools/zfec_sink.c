@@ -13,6 +13,65 @@ static intptr_t *peers;
 static size_t n, ncap;
 static unsigned long long ndeliv, dbytes, dsum;
 
+/* sum of the payload's little-endian 64-bit words (the last one zero-padded): order-free, so the
+ * rate tool compares the total with the one of the payloads it sent */
+static unsigned long long fold(const unsigned char *q, unsigned int size) {
+    unsigned long long s = 0, w;
+    unsigned int i = 0;
+    for (; i + 8 <= size; i += 8) {
+        memcpy(&w, q + i, 8);
+        s += w;
+    }
+    if (i < size) {
+        w = 0;
+        memcpy(&w, q + i, size - i);
+        s += w;
+    }
+    return s;
+}
+
+
+/* forwarding mode (sink_forward): the send flush's datagrams go straight into a receiving
+ * context's qfec_zfec_unpack_input, session s -> rx session rx_of[s], dropping `ndrop` of
+ * every n consecutive datagrams of a session (positions g, g+1, .. mod n of its g-th group) */
+typedef int (*unpack_input_fn)(void *z, int s, const void *d, unsigned int size);
+static void *fwd_z;
+static unpack_input_fn fwd_fn;
+static int *fwd_rx, fwd_n, fwd_ndrop;
+static unsigned long long *fwd_cnt;
+
+void sink_forward(void *z, void *fn, const int *rx_of, int nsess, int n, int ndrop) {
+    fwd_z = z;
+    fwd_fn = (unpack_input_fn)fn;
+    free(fwd_rx);
+    free(fwd_cnt);
+    fwd_rx = malloc(sizeof(int) * (size_t)nsess);
+    fwd_cnt = calloc((size_t)nsess, sizeof(unsigned long long));
+    memcpy(fwd_rx, rx_of, sizeof(int) * (size_t)nsess);
+    fwd_n = n;
+    fwd_ndrop = ndrop;
+}
+
+int sink_pack_forward(void *peer, const char *p, unsigned int size) {
+    const int s = (int)(intptr_t)peer - 1;
+    const unsigned long long c = fwd_cnt[s]++;
+    const int j = (int)(c % (unsigned long long)fwd_n), g = (int)(c / (unsigned long long)fwd_n);
+    for (int t = 0; t < fwd_ndrop; ++t)
+        if ((g + t) % fwd_n == j) return 0;
+    ++n;
+    return fwd_fn(fwd_z, fwd_rx[s], p, size);
+}
+
+/* receive side without a copy: fold the payload where the layer hands it over */
+int sink_unpack_fold(void *peer, const char *p, unsigned int size, unsigned int src) {
+    (void)peer;
+    (void)src;
+    ndeliv++;
+    dbytes += size;
+    dsum += fold((const unsigned char *)p, size);
+    return 0;
+}
+
 int sink_pack(void *peer, const char *p, unsigned int size) {
     if (used + size > cap) {
         size_t c = (used + size) * 2 + (1 << 20);
@@ -46,23 +105,6 @@ int sink_pack(void *peer, const char *p, unsigned int size) {
 /* the application's copy of a delivered payload (a ring it consumes from) */
 static unsigned char app[1 << 22];
 static size_t app_pos;
-
-/* sum of the payload's little-endian 64-bit words (the last one zero-padded): order-free, so the
- * rate tool compares the total with the one of the payloads it sent */
-static unsigned long long fold(const unsigned char *q, unsigned int size) {
-    unsigned long long s = 0, w;
-    unsigned int i = 0;
-    for (; i + 8 <= size; i += 8) {
-        memcpy(&w, q + i, 8);
-        s += w;
-    }
-    if (i < size) {
-        w = 0;
-        memcpy(&w, q + i, size - i);
-        s += w;
-    }
-    return s;
-}
 
 int sink_unpack(void *peer, const char *p, unsigned int size, unsigned int src) {
     (void)peer;
