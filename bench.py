@@ -62,6 +62,9 @@ GIB = float(1 << 30)
 # the kernel sources whose PMC traffic profiles/traffic.json holds (stale if they change)
 KERNEL_SOURCES = ("quicknet_amd/csrc/qfec_kernels.hip", "quicknet_amd/csrc/qfec_internal.hpp",
                   "quicknet_amd/csrc/qfec_device.hpp")
+# ... and those of the datagram / framing legs (their own traffic.json entry)
+WIRE_KERNEL_SOURCES = KERNEL_SOURCES + ("quicknet_amd/csrc/qfec_wire.hip",)
+TRAFFIC_PATH = os.path.join(ROOT, "profiles", "traffic.json")
 
 
 def parse(argv=None):
@@ -100,7 +103,7 @@ def parse(argv=None):
     p.add_argument("--no-numa-bind", action="store_true", help="do not bind ranks to their GPU's NUMA node")
     p.add_argument("--force-dist", action="store_true",
                    help="init the process group even at one rank (exercises the RCCL path on a one-GPU box)")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+    p.add_argument("--traffic", default=TRAFFIC_PATH,
                    help="PMC-derived HBM bytes per launch (tools/pmc_traffic.py), if present")
     return p.parse_args(argv)
 
@@ -655,7 +658,7 @@ def wire_leg(rank, G=100_000, k=10, m=3, S=1024, steps=20, warmup=10, spinup_ms=
                        torch.arange(G, dtype=torch.int32, device=dev) * k], 1).contiguous()
     lost = torch.from_numpy(erasure_marks(rank_seed(SEED_DECODE ^ 0x77, rank), G, n, m).astype(bool)).to(dev)
     s = torch.cuda.current_stream()
-    out = {}
+    out = {}  # PMC traffic fields, merged into the leg's record
 
     def timed(fn):
         _spin(fn, spinup_ms)  # the same clock spin-up as the other legs
@@ -701,17 +704,64 @@ def wire_leg(rank, G=100_000, k=10, m=3, S=1024, steps=20, warmup=10, spinup_ms=
     pay = G * k * S
     pack_traffic = pay + int(wlen.sum().item())
     unpack_traffic = int(rx_len.sum().item()) + G * k * ((S + 4 + 15) // 16 * 16)
-    out = {"config": f"RS({k},{n}) fec_new (system/fec.c), {G:,} groups x {k} x {S} B payloads, checksums on, "
+    # the same batch straight to / from ProtocolUdp frames in one pass (qfec_pack_frames /
+    # qfec_unpack_frames; SessionDesc.cpp:69-77 + ProtocolBasic.cpp:111-199 on every datagram)
+    fp = (sp + 13 + 4 + 63) // 64 * 64
+    masks = (torch.arange(G * n, dtype=torch.int32, device=dev) * 7 & 0xFF).to(torch.uint8)
+    frames = torch.empty((G, n, fp), dtype=torch.uint8, device=dev)
+    flen = torch.empty((G, n), dtype=torch.int32, device=dev)
+    fst = torch.empty((G, n), dtype=torch.int32, device=dev)
+
+    def pack_frames():
+        rc = L.qfec_pack_frames(code._h, payload.data_ptr(), offsets.data_ptr(), sizes.data_ptr(), seq.data_ptr(), G, 1,
+                                shards.data_ptr(), sp, masks.data_ptr(), None, 0x3C, 0x11, 0xFF, frames.data_ptr(), fp,
+                                flen.data_ptr(), st)
+        assert rc == 0, rc
+
+    def unpack_frames():
+        rc = L.qfec_unpack_frames(code._h, frames.data_ptr(), fp, rx_flen.data_ptr(), G, 0x3C, 0, 1, 2068,
+                                  osh.data_ptr(), sp, marks.data_ptr(), rxs.data_ptr(), status.data_ptr(),
+                                  psize.data_ptr(), fst.data_ptr(), None, st)
+        assert rc == 0, rc
+
+    pack_frames_ms, _ = timed(pack_frames)
+    rx_flen = torch.where(lost, torch.zeros_like(flen), flen).contiguous()
+    status.fill_(-9)
+    unpack_frames_ms, _ = timed(unpack_frames)
+    fok = bool((status == 4).all().item()) and bool((psize == S).all().item()) and bool((fst[~lost] == 0).all().item())
+    fok = fok and bool(torch.equal(osh[:, :k, 4:4 + S].reshape(-1), payload[:G * k * S]))
+    fok = fok and torch.equal(flen, wlen + 4)
+    ok = ok and fok
+    pack_frames_traffic = pay + int(flen.sum().item())
+    unpack_frames_traffic = int(rx_flen.sum().item()) + G * k * sp
+    framed = {"what": "the same batch to ProtocolUdp frames in one pass (qfec_pack_frames: 4-byte prefix, per-datagram "
+                      "mask, FEC cmd/protocol) and back (qfec_unpack_frames: RecvPacket verdicts + unpack)",
+              "frame_pitch": fp,
+              "pack_frames_avg_ms": round(pack_frames_ms, 4), "unpack_frames_avg_ms": round(unpack_frames_ms, 4),
+              "pack_frames_gibs": round(pay / (pack_frames_ms * 1e-3) / GIB, 2),
+              "unpack_frames_gibs": round(pay / (unpack_frames_ms * 1e-3) / GIB, 2),
+              "pack_frames_frac": round(pack_frames_traffic / (pack_frames_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "unpack_frames_frac": round(unpack_frames_traffic / (unpack_frames_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+              "pack_frames_min_traffic": pack_frames_traffic, "unpack_frames_min_traffic": unpack_frames_traffic,
+              "traffic_basis": "min traffic: payload in + frames out / frames received in + data shard rows out",
+              "parity": "framing bytes parity unpinned (ProtocolBasic.cpp does not build here; oracle restatement)",
+              "verified": fok}
+    wtr, wsrc = load_traffic(TRAFFIC_PATH, f"wire_rs{k}_{n}_s{S}_g{G}", WIRE_KERNEL_SOURCES)
+    for key, alg in (("pack", pack_traffic), ("unpack", unpack_traffic), ("pack_frames", pack_frames_traffic),
+                     ("unpack_frames", unpack_frames_traffic)):
+        t = wtr.get(key) if isinstance(wtr, dict) else None
+        tgt = framed if "frames" in key else out
+        tgt[f"{key}_traffic"] = t
+        tgt[f"{key}_traffic_over_min"] = round(t / alg, 4) if t else None
+    out["traffic_source"] = wsrc
+    return {"config": f"RS({k},{n}) fec_new (system/fec.c), {G:,} groups x {k} x {S} B payloads, checksums on, "
                      f"{m} of {n} datagrams lost per group",
            "pack_gibs": round(pay / (pack_ms * 1e-3) / GIB, 2), "unpack_gibs": round(pay / (unpack_ms * 1e-3) / GIB, 2),
            "pack_avg_ms": round(pack_ms, 4), "unpack_avg_ms": round(unpack_ms, 4),
            "pack_frac": round(pack_traffic / (pack_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "unpack_frac": round(unpack_traffic / (unpack_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "traffic_basis": "min traffic: payload in + datagrams out / datagrams received in + data shard rows out",
-           "verified": ok}
-    del payload, shards, wire, wlen, osh, rx_len, marks, rxs, status, psize
-    torch.cuda.empty_cache()
-    return out
+           "framed": framed, "verified": ok, **out}
 
 
 def per_call_leg(reps=2000, ref_lib=None, batched=True):
@@ -778,7 +828,7 @@ def per_call_leg(reps=2000, ref_lib=None, batched=True):
     return out
 
 
-def load_traffic(path, workload_key):
+def load_traffic(path, workload_key, sources=KERNEL_SOURCES):
     """PMC bytes per launch for this workload from profiles/traffic.json, or None when absent
     or measured on other kernel sources (the file records their sha256)."""
     try:
@@ -789,15 +839,15 @@ def load_traffic(path, workload_key):
     ent = t.get(workload_key)
     if not isinstance(ent, dict):
         return None, "no entry for this workload"
-    want = kernel_sources_hash()
+    want = kernel_sources_hash(sources)
     if ent.get("kernel_sources_sha256") != want:
         return None, f"stale: measured on kernel sources {ent.get('kernel_sources_sha256')}, now {want}"
     return ent, f"{os.path.relpath(path, ROOT)} ({ent.get('run', 'PMC run')}, kernel sources {want})"
 
 
-def kernel_sources_hash():
+def kernel_sources_hash(sources=KERNEL_SOURCES):
     h = hashlib.sha256()
-    for f in KERNEL_SOURCES:
+    for f in sources:
         with open(os.path.join(ROOT, f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]

@@ -22,27 +22,31 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"encode": "k_encode_perm<{k}, {m}>", "reconstruct": "k_reconstruct_perm<{k}, {m},", "probe": "k_probe_xor"}
+# --workload wire: bench.py's `wire` leg (tools/side_legs.py), RS(10,13) 1 KiB payloads
+WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0>", "unpack": "k_unpack_v2<10, 3, 4, true, 0>",
+                "pack_frames": "k_pack_wave64<10, 3, 1, 4>", "unpack_frames": "k_unpack_v2<10, 3, 4, true, 4>"}
 
 
-def run_pass(counter, out, bench_args, k, m):
+def run_pass(counter, out, bench_args, k, m, kernels=KERNELS, script="bench.py"):
     d = os.path.abspath(os.path.join(out, counter.lower()))
     os.makedirs(d, exist_ok=True)
+    extra = ["--no-cpu"] if script == "bench.py" else []
     cmd = ["rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", counter.lower(), "--",
-           sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu"] + bench_args
+           sys.executable, os.path.join(ROOT, script)] + extra + bench_args
     env = dict(os.environ, TMPDIR="/tmp")
     with open(os.path.join(d, "run.log"), "w") as log:
         subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=env, cwd="/tmp", timeout=600)
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise RuntimeError(f"no counter_collection.csv under {d}")
-    per = {k: [] for k in KERNELS}
+    per = {k: [] for k in kernels}
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row.get("Kernel_Name", "")
-                for key, pat in KERNELS.items():
+                for key, pat in kernels.items():
                     if pat.format(k=k, m=m) in name:
                         per[key].append(float(row["Counter_Value"]))
     return per
@@ -57,7 +61,10 @@ def main():
     p.add_argument("--block", type=int, default=1024)
     p.add_argument("--groups", type=int, default=100_000)
     p.add_argument("--tag", default="PMC run", help="which run produced the numbers (recorded in the JSON)")
+    p.add_argument("--workload", choices=["headline", "wire"], default="headline")
     a = p.parse_args()
+    if a.workload == "wire":
+        return wire_main(a)
     bench_args = ["--steps", "5", "--warmup", "1", "--k", str(a.k), "--m", str(a.m), "--block", str(a.block),
                   "--groups", str(a.groups), "--no-side", "--no-config4", "--no-host"]
     fetch = run_pass("FETCH_SIZE", a.out, bench_args, a.k, a.m)
@@ -92,6 +99,37 @@ def main():
         "raw": res,
     }
     os.makedirs(os.path.dirname(a.json), exist_ok=True)
+    with open(a.json, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(json.dumps(doc[key], indent=1))
+
+
+def wire_main(a):
+    """PMC bytes per launch of the datagram and one-pass frame kernels of bench.py's `wire` leg."""
+    args = ["--steps", "20", "--warmup", "2"]
+    fetch = run_pass("FETCH_SIZE", a.out, args, 10, 3, WIRE_KERNELS, "tools/side_legs.py")
+    write = run_pass("WRITE_SIZE", a.out, args, 10, 3, WIRE_KERNELS, "tools/side_legs.py")
+    res = {}
+    for key in WIRE_KERNELS:
+        if not fetch[key] or not write[key]:
+            continue
+        f = sum(fetch[key]) / len(fetch[key])
+        w = sum(write[key]) / len(write[key])
+        res[key] = {"fetch_kib_raw": f, "write_kib_raw": w, "read_bytes": 2 * f * 1024, "write_bytes": w * 1024,
+                    "bytes_per_launch": 2 * f * 1024 + w * 1024, "launches": len(fetch[key])}
+    doc = {}
+    if os.path.exists(a.json):
+        with open(a.json) as fh:
+            doc = json.load(fh)
+    sys.path.insert(0, ROOT)
+    from bench import WIRE_KERNEL_SOURCES, kernel_sources_hash
+    key = "wire_rs10_13_s1024_g100000"
+    doc[key] = {"kernel_sources_sha256": kernel_sources_hash(WIRE_KERNEL_SOURCES), "run": a.tag,
+                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over tools/side_legs.py; "
+                          "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 corrections)",
+                "raw": res}
+    for k2, v in res.items():
+        doc[key][k2] = v["bytes_per_launch"]
     with open(a.json, "w") as fh:
         json.dump(doc, fh, indent=1)
     print(json.dumps(doc[key], indent=1))
