@@ -93,6 +93,13 @@ __device__ __forceinline__ uint4 xor16(uint4 v, uint32_t mm) {
     return make_uint4(v.x ^ mm, v.y ^ mm, v.z ^ mm, v.w ^ mm);
 }
 
+// 16-byte keep mask for the chunk's bytes below n (n clamped to 0..16), as two 64-bit words
+__device__ __forceinline__ void keep_words(int n, uint64_t& lo, uint64_t& hi) {
+    const int c = min(max(n, 0), 16);
+    lo = c >= 8 ? ~0ull : (1ull << (8 * c)) - 1ull;
+    hi = c >= 16 ? ~0ull : c <= 8 ? 0ull : (1ull << (8 * (c - 8))) - 1ull;
+}
+
 // XOR with mm only the chunk's bytes below n: a frame's padding stays zero
 __device__ __forceinline__ uint4 xor16n(uint4 v, uint32_t mm, int n) {
     return make_uint4(v.x ^ (mm & byte_mask(0, n, 0)), v.y ^ (mm & byte_mask(0, n, 1)), v.z ^ (mm & byte_mask(0, n, 2)),
@@ -745,8 +752,11 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
 // loads are unaligned anyway); line 0's dword ln is datagram dword ln - FP/4, the prefix below
 // it.  The frame checksum is the datagram's byte sum (header + the shard sum the wave already
 // has) plus the prefix bytes, so no byte is read twice.  Bytes of a row past its frame are 0.
+#ifndef FRAME_WAVES
+#define FRAME_WAVES 3  // waves per SIMD the one-pass frame send is compiled for (A/B: 4 spills)
+#endif
 template <int K, int M, int GPW, int FP = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? FRAME_WAVES : 4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
                                                      const int64_t* __restrict__ offsets,
                                                      const int32_t* __restrict__ sizes,
                                                      const uint32_t* __restrict__ seq,
@@ -775,12 +785,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     int64_t off[K];
 #pragma unroll
     for (int i = 0; i < K; ++i) off[i] = ok ? offsets[g * K + i] : 0;
-    uint32_t mm[FP ? N : 1];  // per-row XOR word (frame bytes 1..)
-    if constexpr (FP != 0) {
-#pragma unroll
-        for (int r = 0; r < N; ++r)
-            mm[r] = ok ? ((fs.mask[g * N + r] ^ fs.gmask ^ 0x5Au) & 0xFFu) * 0x01010101u : 0u;
-    }
     uint8_t* out_g = a.wire + g * (uint64_t)N * a.wire_pitch;
     uint4 x[K];
 #pragma unroll
@@ -798,6 +802,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     encode_cols<K, M>(x, acc, tab);
 #pragma unroll
     for (int r = 0; r < M; ++r) pin16(acc[r]);
+    // FP: the group's N mask bytes, from the aligned dwords that hold them (scalar loads for
+    // GPW 1; an aligned dword never reaches past the page its first byte is on); row r's XOR
+    // word is formed where it is used, so no N registers stay live across the encode
+    uint32_t mw5[FP ? 5 : 1];
+    int msh = 0;
+    if constexpr (FP != 0) {
+        const uint64_t b0 = g * (uint64_t)N;
+        const uint32_t* mw = reinterpret_cast<const uint32_t*>(fs.mask + (b0 & ~(uint64_t)3));
+        msh = (int)(b0 & 3);
+#pragma unroll
+        for (int d = 0; d < 5; ++d) mw5[d] = 4 * d < msh + N ? mw[d] : 0u;
+    }
+    auto mm_of = [&](int r) -> uint32_t {  // (mask ^ gmask ^ 0x5a) in every byte
+        if constexpr (FP == 0) {
+            return 0u;
+        } else {
+            const int bpos = msh + r;
+            const uint32_t byte = (mw5[bpos >> 2] >> (8 * (bpos & 3))) ^ fs.gmask ^ 0x5Au;
+            return (byte & 0xFFu) * 0x01010101u;
+        }
+    };
     uint8_t* out = out_g + 16 * t;
 #pragma unroll
     for (int r = 0; r < N; ++r) {
@@ -805,8 +830,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if (r >= K) ps[r] = sum16(v, 0);
         if constexpr (FP != 0) {  // XOR the frame's bytes only: padding past it stays 0
             const int total = FP + HDR + (r < K ? size[r] + HEAD : gmax);
-            v = make_uint4(v.x ^ (mm[r] & byte_mask(0, total - 16 * t, 0)), v.y ^ (mm[r] & byte_mask(0, total - 16 * t, 1)),
-                           v.z ^ (mm[r] & byte_mask(0, total - 16 * t, 2)), v.w ^ (mm[r] & byte_mask(0, total - 16 * t, 3)));
+            uint64_t klo, khi;  // bytes of this chunk below the frame's end
+            int rel = total - 16 * t;
+            asm volatile("" : "+v"(rel));  // formed here, after the encode: not hoisted into it
+            keep_words(rel, klo, khi);
+            const uint32_t mr = mm_of(r);
+            const uint64_t m2 = ((uint64_t)mr << 32) | mr;
+            const uint64_t xl = m2 & klo, xh = m2 & khi;
+            v = make_uint4(v.x ^ (uint32_t)xl, v.y ^ (uint32_t)(xl >> 32), v.z ^ (uint32_t)xh, v.w ^ (uint32_t)(xh >> 32));
         }
         if (ok) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
     }
@@ -898,8 +929,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             if (ln == 0) d = (c | (fcmd << 8) | (fproto << 16)) << 8;
             else if (FP == 12 && ln == 1) d = conv;
             else if (FP == 12 && ln == 2) d = hid;
-            d ^= mm[r] & byte_mask(ln == 0 ? 1 : 0, total - 4 * ln, 0);
-            if (ln == 0) d |= fs.mask[g * N + r];
+            d ^= mm_of(r) & byte_mask(ln == 0 ? 1 : 0, total - 4 * ln, 0);
+            if (ln == 0) d |= (mw5[(msh + r) >> 2] >> (8 * ((msh + r) & 3))) & 0xFFu;  // the raw mask byte
         }
         if (ln < 16) {
             uint32_t* dst = reinterpret_cast<uint32_t*>(out_g + (uint64_t)r * a.wire_pitch + 4 * ln);

@@ -39,6 +39,7 @@
 #include <mutex>
 #include <thread>
 #include <tuple>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -462,11 +463,26 @@ struct Verdict {  // of one received FEC datagram
     int batch = -1, group = -1, ik = 0;  // its place in the verdict launch
 };
 
-struct DecodeKey {
-    int session, k, n, mode, dec_pkt_size;
-    std::vector<std::pair<uint64_t, int>> rows;  // (slot uid, ik) in iValid order
-    bool operator<(const DecodeKey& o) const {
-        return std::tie(session, k, n, mode, dec_pkt_size, rows) < std::tie(o.session, o.k, o.n, o.mode, o.dec_pkt_size, o.rows);
+struct DecodeKey {  // a decode by content: the session, code, mode and exactly which rows
+    int session = 0, k = 0, n = 0, mode = 0, dec_pkt_size = 0, nrows = 0;
+    uint64_t uid[16] = {};  // slot uids in iValid order
+    uint8_t ik[16] = {};
+    bool operator==(const DecodeKey& o) const {
+        if (session != o.session || k != o.k || n != o.n || mode != o.mode || dec_pkt_size != o.dec_pkt_size ||
+            nrows != o.nrows)
+            return false;
+        for (int i = 0; i < nrows; ++i)
+            if (uid[i] != o.uid[i] || ik[i] != o.ik[i]) return false;
+        return true;
+    }
+};
+struct DecodeKeyHash {
+    size_t operator()(const DecodeKey& x) const {
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)x.session * 0x100000001B3ull;
+        h = (h ^ ((uint64_t)x.k << 40 | (uint64_t)x.n << 32 | (uint64_t)x.mode << 24 | (uint64_t)(uint32_t)x.dec_pkt_size)) *
+            0x100000001B3ull;
+        for (int i = 0; i < x.nrows; ++i) h = (h ^ (x.uid[i] * 31 + x.ik[i])) * 0x100000001B3ull;
+        return (size_t)(h ^ (h >> 29));
     }
 };
 struct DecodeOut {
@@ -475,11 +491,14 @@ struct DecodeOut {
 };
 struct DecodeReq {
     DecodeKey key;
-    std::vector<std::pair<View, int>> shards;  // (shard, ik)
+    int nsh = 0;
+    View shard[16];  // the k shards, ik in key.ik
+    DecodeOut* out = nullptr;
 };
+using DecodeCache = std::unordered_map<DecodeKey, DecodeOut, DecodeKeyHash>;
 
 struct RxPass {
-    const std::map<DecodeKey, DecodeOut>* cache;
+    const DecodeCache* cache;
     std::vector<DecodeReq>* missing;
 };
 
@@ -673,16 +692,20 @@ class RxMachine {
         key.n = cur_n;
         key.mode = R.is_checksum ? 1 : 0;
         key.dec_pkt_size = R.dec_pkt_size;
-        key.rows.reserve((size_t)nrows);
-        for (int r = 0; r < nrows; ++r) key.rows.emplace_back(R.slots[rows[r]].uid, R.slots[rows[r]].ik);
+        key.nrows = nrows;
+        for (int r = 0; r < nrows; ++r) {
+            key.uid[r] = R.slots[rows[r]].uid;
+            key.ik[r] = (uint8_t)R.slots[rows[r]].ik;
+        }
         auto it = pass.cache->find(key);
         const DecodeOut* res = it == pass.cache->end() ? nullptr : &it->second;
         int req = -1;  // index of this decode's request (placeholders refer to it)
         if (!res) {
-            DecodeReq q;
-            q.key = std::move(key);
-            for (int r = 0; r < nrows; ++r) q.shards.emplace_back(R.slots[rows[r]].shard, R.slots[rows[r]].ik);
-            pass.missing->push_back(std::move(q));
+            pass.missing->emplace_back();
+            DecodeReq& q = pass.missing->back();
+            q.key = key;
+            q.nsh = nrows;
+            for (int r = 0; r < nrows; ++r) q.shard[r] = R.slots[rows[r]].shard;
             req = (int)pass.missing->size() - 1;
         }
         for (int i = 0; i < cur_k; ++i) {  // :308-366
@@ -985,6 +1008,23 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     for (auto& S : z->sessions) n_ops += S.ops.size();
     const unsigned threads = flush_threads(n_ops, NS);
     int rc = 0;
+    // the arenas' bytes start for the device now, so the copies run while the machines do
+    // (a context with no device -- FEC-off sessions only -- skips this; whatever needs the
+    // device later fails there)
+    bool tx_staged = false, rx_staged = false;
+    {
+        bool any_pack = false, any_unpack = false;
+        for (auto& S : z->sessions)
+            for (auto& op : S.ops) {
+                any_pack |= op.t == OP_PACK;
+                any_unpack |= op.t == OP_UNPACK;
+            }
+        if (any_pack && TXA.used && z->d_tx.ensure(TXA.used + 16) == QFEC_OK)
+            tx_staged = hipMemcpyAsync(z->d_tx.d, TXA.h, TXA.used + 16, hipMemcpyHostToDevice, st) == hipSuccess;
+        if (any_unpack && RXA.used && z->d_rx.ensure(RXA.used + 16) == QFEC_OK)
+            rx_staged = hipMemcpyAsync(z->d_rx.d, RXA.h, RXA.used + 16, hipMemcpyHostToDevice, st) == hipSuccess;
+        (void)hipGetLastError();
+    }
     // ---- send: the machines (threaded over sessions), then their groups merged per (k, n)
     std::vector<std::vector<LocalGroup>> lgroups(NS);
     parallel_for(NS, threads, [&](size_t si) { tx_machine(z->sessions[si], tx_out[si], lgroups[si], own[si], TXA.h); });
@@ -1036,10 +1076,13 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             b.d_shards = work.take(G * b.n * b.sp);
         }
         z->io.used = 0;
-        if (!z->io.reserve(io.o + 16) || (rc = z->d_io.ensure(io.o + 16)) || (rc = z->d_work.ensure(work.o + 16)) ||
-            (rc = z->d_tx.ensure(TXA.used + 16)))
+        if (!z->io.reserve(io.o + 16) || (rc = z->d_io.ensure(io.o + 16)) || (rc = z->d_work.ensure(work.o + 16)))
             return rc ? rc : QFEC_ENOMEM;
-        if (hipMemcpyAsync(z->d_tx.d, TXA.h, TXA.used + 16, hipMemcpyHostToDevice, st) != hipSuccess) return QFEC_EHIP;
+        if (!tx_staged) {
+            if ((rc = z->d_tx.ensure(TXA.used + 16))) return rc;
+            if (hipMemcpyAsync(z->d_tx.d, TXA.h, TXA.used + 16, hipMemcpyHostToDevice, st) != hipSuccess)
+                return QFEC_EHIP;
+        }
         tsync("pack h2d");
         uint8_t* h = z->io.h;
         uint8_t* d = z->d_io.d;
@@ -1089,6 +1132,8 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     std::map<std::tuple<int, int, int, int>, int> vb_of;
     // rows taken in each pseudo-group (shared by all sessions: a row's verdict is its own)
     std::vector<std::vector<uint16_t>> taken;  // per batch, per group: bit ik
+    std::tuple<int, int, int, int> last_key{-1, -1, -1, -1};
+    int last_bi = -1;
     for (size_t si = 0; si < NS; ++si) {
         Session& S = z->sessions[si];
         int dps = S.rx.dec_pkt_size;  // its growth over the queue (unpack_fec_head realloc)
@@ -1106,9 +1151,12 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 if (v.usable) {
                     const int cs = d[0] == 0xED ? 1 : 0;
                     const auto key = std::make_tuple(k, n, cs, dps);
-                    auto it = vb_of.find(key);
                     int bi;
-                    if (it == vb_of.end()) {
+                    if (key == last_key && last_bi >= 0) {
+                        bi = last_bi;
+                    } else if (vb_of.count(key)) {
+                        bi = vb_of[key];
+                    } else {
                         UnpackBatch b;
                         b.k = k;
                         b.n = n;
@@ -1118,9 +1166,9 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                         taken.emplace_back();
                         bi = (int)vb.size() - 1;
                         vb_of.emplace(key, bi);
-                    } else {
-                        bi = it->second;
                     }
+                    last_key = key;
+                    last_bi = bi;
                     UnpackBatch& b = vb[(size_t)bi];
                     auto& used = taken[(size_t)bi];
                     int g = -1;
@@ -1149,11 +1197,11 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     }
     phase("rx grouping");
     // the receive arena's bytes on the device once: verdict and decode launches gather from it
-    if (!vb.empty()) {
+    if (!vb.empty() && !rx_staged) {
         if ((rc = z->d_rx.ensure(RXA.used + 16))) return rc;
         if (hipMemcpyAsync(z->d_rx.d, RXA.h, RXA.used + 16, hipMemcpyHostToDevice, st) != hipSuccess) return QFEC_EHIP;
-        tsync("rx h2d");
     }
+    tsync("rx h2d");
     if (!vb.empty()) {
         Stage io{round16(z->io.used)}, work;
         for (auto& b : vb) unpack_layout(b, io, work);
@@ -1188,10 +1236,11 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     // every row of it decoded and passed (the common case) and leaves placeholders for its
     // deliveries; after the launches the placeholders are filled when that held for every such
     // decode, and otherwise the machines are replayed from the flush's starting state.
-    std::map<DecodeKey, DecodeOut> cache;
+    DecodeCache cache;
     std::vector<RxState> start(NS);
     for (size_t si = 0; si < NS; ++si) start[si] = z->sessions[si].rx;
     std::vector<uint8_t> dec_bytes;  // decoded payloads that are not views of an input shard
+    dec_bytes.reserve((size_t)4 << 20);
     std::vector<DecodeReq> missing;
     for (int pass_no = 0;; ++pass_no) {
         missing.clear();
@@ -1220,11 +1269,12 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         // pitch (only a corrupt one can) is decoded again at dec_pkt_size + 4 in round 1, as the
         // reference reads it.
         std::vector<const DecodeReq*> todo;
-        for (auto& q : missing)
-            if (!cache.count(q.key)) {
-                cache[q.key];  // filled below
-                todo.push_back(&q);
-            }
+        cache.reserve(cache.size() + missing.size());
+        for (auto& q : missing) {
+            auto ins = cache.emplace(q.key, DecodeOut{});  // (node addresses survive rehashing)
+            q.out = &ins.first->second;
+            if (ins.second) todo.push_back(&q);
+        }
         for (int round = 0; round < 2 && !todo.empty(); ++round) {
             std::vector<UnpackBatch> db;
             std::map<std::tuple<int, int, int, int>, int> db_of;
@@ -1252,9 +1302,9 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 UnpackBatch& b = db[(size_t)bi];
                 const int g = b.groups++;
                 uint32_t have = 0;
-                for (auto& sh : q->shards) {
-                    b.rows.push_back(UnpackRow{g, sh.second, sh.first.off, sh.first.len});
-                    have |= 1u << sh.second;
+                for (int r = 0; r < q->nsh; ++r) {
+                    b.rows.push_back(UnpackRow{g, (int)q->key.ik[r], q->shard[r].off, q->shard[r].len});
+                    have |= 1u << q->key.ik[r];
                 }
                 for (int i = 0; i < b.k; ++i)  // the rebuilt rows come back; inputs are views
                     if (!((have >> i) & 1u)) b.fetch.push_back((uint32_t)(g * b.n + i));
@@ -1282,10 +1332,10 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                 // into the flush's decoded bytes.
                 for (size_t g = 0; g < rq.size(); ++g) {
                     bool cut = false;
-                    DecodeOut& o = cache[rq[g]->key];
+                    DecodeOut& o = *rq[g]->out;
                     const View* src_of[16] = {};
-                    for (auto& sh : rq[g]->shards)
-                        if (sh.second < b.k) src_of[sh.second] = &sh.first;
+                    for (int r = 0; r < rq[g]->nsh; ++r)
+                        if (rq[g]->key.ik[r] < b.k) src_of[rq[g]->key.ik[r]] = &rq[g]->shard[r];
                     for (int i = 0; i < b.k; ++i) {
                         const int stt = b.status[g * b.k + i], ps = b.psize[g * b.k + i];
                         cut |= stt == -1 && ps < b.dec_pkt_size && (size_t)(head + ps) > b.sp;
@@ -1320,7 +1370,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         phase("decode results");
         bool all_ok = true;
         for (auto& q : missing) {
-            const DecodeOut& o = cache[q.key];
+            const DecodeOut& o = *q.out;
             for (int i = 0; i < q.key.k; ++i) all_ok &= o.ok[i];
         }
         if (!all_ok) continue;  // replay with the results
@@ -1328,7 +1378,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             for (auto& e : rx_out[si])
                 if (e.kind == 3) {
                     e.kind = 2;
-                    e.v = cache[missing[(size_t)e.batch].key].payload[e.row];
+                    e.v = missing[(size_t)e.batch].out->payload[e.row];
                 }
         break;
     }  // (terminates: a pass that asks for decodes adds their keys to the cache)
