@@ -54,7 +54,7 @@ inline int packed_size(int size) { return size < 0 ? 0 : size + 4 + 12 + 4; }  /
 inline int cmod(int a, int b) { return a % b; }                                   // C's % (truncating), as in :277
 
 // where a View's bytes live
-enum Src : uint8_t { SRC_NONE = 0, SRC_RX, SRC_TX, SRC_DEC, SRC_OWN };
+enum Src : uint8_t { SRC_NONE = 0, SRC_RX, SRC_TX, SRC_DEC, SRC_OWN, SRC_IO };
 struct View {  // bytes [off, off + len) of one of the flush's buffers
     uint8_t src = SRC_NONE;
     uint32_t off = 0, len = 0;
@@ -299,6 +299,7 @@ struct Bufs {
     const uint8_t* rx = nullptr;
     const uint8_t* tx = nullptr;
     const uint8_t* dec = nullptr;
+    const uint8_t* io = nullptr;
     const std::vector<std::vector<uint8_t>>* own = nullptr;  // per session
     const uint8_t* p(const View& v, size_t session) const {
         switch (v.src) {
@@ -306,6 +307,7 @@ struct Bufs {
             case SRC_TX: return tx + v.off;
             case SRC_DEC: return dec + v.off;
             case SRC_OWN: return (*own)[session].data() + v.off;
+            case SRC_IO: return io + v.off;
             default: return nullptr;
         }
     }
@@ -853,7 +855,9 @@ void tx_machine(Session& S, std::vector<Emit>& out, std::vector<LocalGroup>& gro
 }
 
 unsigned flush_threads(size_t work, size_t sessions) {
-    unsigned t = work < 4096 ? 1u : std::max(1u, std::min({16u, std::thread::hardware_concurrency(), (unsigned)sessions}));
+    // at most 8: a CPU quota (the box gives a process 16 CPUs) throttles a flush that runs more
+    // threads than it allows for a whole scheduling period
+    unsigned t = work < 4096 ? 1u : std::max(1u, std::min({8u, std::thread::hardware_concurrency(), (unsigned)sessions}));
     if (const char* e = getenv("QFEC_ZFEC_RX_THREADS"))  // tests: force the threaded machines
         t = (unsigned)std::max(1, std::min(64, atoi(e)));
     return t;
@@ -1275,6 +1279,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             q.out = &ins.first->second;
             if (ins.second) todo.push_back(&q);
         }
+        phase("decode dedup");
         for (int round = 0; round < 2 && !todo.empty(); ++round) {
             std::vector<UnpackBatch> db;
             std::map<std::tuple<int, int, int, int>, int> db_of;
@@ -1348,9 +1353,8 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                         } else {
                             o.payload[i] = View{SRC_DEC, (uint32_t)dec_bytes.size(), (uint32_t)ps};
                             const int fi = fidx[g * b.n + (size_t)i];
-                            if (fi >= 0) {
-                                const uint8_t* p = b.shards + (size_t)fi * b.sp + (size_t)stt;
-                                dec_bytes.insert(dec_bytes.end(), p, p + ps);
+                            if (fi >= 0) {  // the rebuilt row where it came back (the io arena keeps it)
+                                o.payload[i] = View{SRC_IO, (uint32_t)(b.o_hsh + (size_t)fi * b.sp + (size_t)stt), (uint32_t)ps};
                             } else {  // an input whose size field reaches past its shard (corrupt): rare
                                 const size_t at = dec_bytes.size();
                                 dec_bytes.resize(at + (size_t)ps);
@@ -1365,6 +1369,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
                     if (cut && round == 0) again.push_back(rq[g]);
                 }
             }
+            z->io.used = io.o;  // this round's rebuilt rows stay until the callbacks
             todo.swap(again);
         }
         phase("decode results");
@@ -1388,6 +1393,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     B.rx = RXA.h;
     B.tx = TXA.h;
     B.dec = dec_bytes.data();
+    B.io = z->io.h;
     B.own = &own;
     int calls = 0;
     for (size_t si = 0; si < NS; ++si) {
