@@ -764,6 +764,27 @@ def wire_leg(rank, G=100_000, k=10, m=3, S=1024, steps=20, warmup=10, spinup_ms=
            "framed": framed, "verified": ok, **out}
 
 
+def zfec_leg(timeout=240):
+    """SURVEY 8(f) rank 1 in the line: the exact NetFecCodec layer (include/qfec_zfec.h) --
+    64 sender sessions x 2 000 x 1 KiB payloads, RS(10,13), one send flush whose C callback hands
+    every datagram it keeps to a receiving context (1 of 13 dropped per group), then one receive
+    flush whose C callback folds every delivered payload; the best of reps 1-3 after a warm-up rep
+    (tools/zfec_rate.py, its own process).  Rates count payload bytes over each flush's wall time;
+    the reference's own per-packet pipeline on one core is cpu_baseline.wire.  Parity of the
+    control flow is unpinned (NetFecCodec.cpp does not build here; tests/test_gpu_zfec.py)."""
+    try:
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "zfec_rate.py"), "--json"], capture_output=True,
+                           text=True, timeout=timeout)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": (r.stderr or r.stdout)[-300:], "verified": False}
+        out = json.loads(lines[-1])
+        out["parity"] = "control flow parity unpinned (oracle/zfec_ref.py restatement); bytes pinned via FecCodecBuf.cpp"
+        return out
+    except Exception as exc:  # report, never fake
+        return {"error": repr(exc), "verified": False}
+
+
 def per_call_leg(reps=2000, ref_lib=None, batched=True):
     """The unchanged drop-in's per-call cost: what network/FecCodecBuf.cpp pays per
     packet when it links libqfec instead of system/fec.c.  RS(10,3) with 1 KiB payloads:
@@ -1010,7 +1031,7 @@ def main(argv=None):
         except Exception as exc:  # report, never fake
             per_call = {"error": repr(exc)}
 
-    side = wire = None
+    side = wire = zfec = None
     if rank == 0 and not args.no_side:
         side = [side_config(fl, sk, sm, sB, sG, sE, rank) for fl, sk, sm, sB, sG, sE in SIDE]
         try:
@@ -1019,6 +1040,8 @@ def main(argv=None):
             wire = {"error": repr(exc), "verified": False}
         ok = ok and bool(wire.get("verified"))
         ok = ok and all(x["verified"] for x in side)
+        zfec = zfec_leg()
+        ok = ok and bool(zfec.get("verified"))
 
     cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -1108,6 +1131,7 @@ def main(argv=None):
             "process_group": torch.distributed.get_backend() if _dist_on() else None,
             "side_configs": side,
             "wire": wire,
+            "zfec": zfec,
         }
         print(json.dumps(out), flush=True)
     if _dist_on():
