@@ -389,16 +389,16 @@ __device__ __forceinline__ void ldv_plain(uint32_t (&v)[D], const uint8_t* p) {
 // byte offsets the record's header lists (RecordLayout::coff).  The compact form reads only
 // the record's header, so the records of all patterns stay cache-resident (RS(16,4): 4 844
 // records of 2.4 KB would not fit the 4 MB L2; their headers do).
-template <bool CT>
+template <int CT>
 struct RTab;
 template <>
-struct RTab<false> {
+struct RTab<0> {
     const uint32_t* __restrict__ tab;
     __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const { return tab + (j * K + c) * QFEC_TAB_STRIDE; }
     __device__ __forceinline__ bool quirk(int j, int K) const { return tab[(j * K) * QFEC_TAB_STRIDE + 5] != 0; }
 };
 template <>
-struct RTab<true> {
+struct RTab<1> {
     const uint32_t* __restrict__ offs;
     const uint32_t* __restrict__ t256;
     __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const {
@@ -406,7 +406,6 @@ struct RTab<true> {
     }
     __device__ __forceinline__ bool quirk(int j, int K) const { return (offs[j * K] & 1u) != 0; }
 };
-
 template <int K, int E, int D, class TT>
 __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
                                                uint64_t lost_bits, const TT& T, uint64_t pitch, uint64_t off) {
@@ -475,7 +474,7 @@ __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K]
 // while the decode record (coefficients only) is still in flight.
 // One wave per 64 16-B columns of a group: a group of `cols` columns gets
 // wpg = ceil(cols / 64) waves (B = 1400 -> 2), all in flight together, no column loop.
-template <int K, int M, int IMPL, bool CT>
+template <int K, int M, int IMPL, int CT>
 __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ parity,
                                                           const uint8_t* __restrict__ marks,
@@ -486,7 +485,7 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    const uint32_t wpg = IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
+    const uint32_t wpg = IMPL == 5 ? 1u : IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
     if (g >= a.groups) return;
@@ -504,8 +503,8 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
     }
     const int rec = __builtin_amdgcn_readfirstlane(lut[mask]);
     const uint32_t* tab = records + rec + a.hdr;
-    const RTab<false> TD{tab};
-    const RTab<true> TC{records + rec + a.coff, a.t256};
+    const RTab<0> TD{tab};
+    const RTab<1> TC{records + rec + a.coff, a.t256};
     const uint64_t pitch = a.pitch;
     uint8_t* data_g = data + g * a.dgs;
     const uint8_t* par_g = parity + g * a.pgs;
@@ -516,9 +515,16 @@ __global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* 
         avail &= avail - 1;
         src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : par_g + (uint64_t)(s - K) * pitch;
     }
+    if constexpr (IMPL == 5) {  // one wave per group: the scalar setup above once, then the 8-B slabs
+        for (uint32_t col = lane; col < a.cols8; col += 64u) {
+            if constexpr (CT != 0) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 8u);
+            else recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 8u);
+        }
+        return;
+    }
     const uint32_t col = part * 64u + lane;
     if (col < (IMPL == 3 ? a.cols8 : IMPL == 4 ? a.cols12 : a.cols)) {
-        if constexpr (CT) {
+        if constexpr (CT != 0) {
             if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 16u);
             else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 8u);
             else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 12u);
@@ -685,10 +691,10 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 #define QFEC_REC_LAUNCH(KK, MM, AR)                                                                        \
     do {                                                                                                   \
         if (AR >= 2 && a.compact && a.t256)                                                                \
-            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, AR >= 2>), dim3(pgrid), dim3(256), 0, stream, a, \
+            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, (AR >= 2) * 1>), dim3(pgrid), dim3(256), 0, stream, a, \
                                a.data, a.parity, a.marks, a.lut, a.records);                               \
         else                                                                                               \
-            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, false>), dim3(pgrid), dim3(256), 0, stream, a, \
+            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, 0>), dim3(pgrid), dim3(256), 0, stream, a, \
                                a.data, a.parity, a.marks, a.lut, a.records);                               \
     } while (0)
 
@@ -700,8 +706,9 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
         int im = a.impl < 0 ? (KK * MM <= 64 ? (KK * MM <= 30 && lanes12 ? 4 : (lanes8 || wide8) ? 3 : 2) : 0) \
                             : a.impl;                                              \
         if (im == 4 && !lanes12_ok) im = 2;                                        \
-        const unsigned pgrid = im == 3 ? pgrid8 : im == 4 ? pgrid12 : pgrid16;     \
-        if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                                   \
+        const unsigned pgrid = im == 5 ? grid : im == 3 ? pgrid8 : im == 4 ? pgrid12 : pgrid16; \
+        if (im == 5) QFEC_REC_LAUNCH(KK, MM, 5);                                   \
+        else if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                              \
         else if (im == 3) QFEC_REC_LAUNCH(KK, MM, 3);                              \
         else if (im == 2) QFEC_REC_LAUNCH(KK, MM, 2);                              \
         else if (im == 1) QFEC_REC_LAUNCH(KK, MM, 1);                              \

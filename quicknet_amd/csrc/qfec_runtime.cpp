@@ -639,7 +639,7 @@ int qfec_get_kernel_variant(void) { return g_variant.load(); }
 // experiment knobs, for A/B timing in one process (tools/ab.py); not needed in production
 int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
-    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 4) { tuning().recon_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 5) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "host_chunk") && value >= 0) { tuning().host_chunk = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
@@ -650,7 +650,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
     if (!strcmp(key, "host_zero_copy") && (value == 0 || value == 1)) { tuning().host_zero_copy = value; return QFEC_OK; }
-    if (!strcmp(key, "recon_compact") && (value == 0 || value == 1)) { tuning().recon_compact = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_compact") && value >= 0 && value <= 2) { tuning().recon_compact = value; return QFEC_OK; }
     if (!strcmp(key, "recon_full_lines") && (value == 0 || value == 1)) { tuning().recon_full_lines = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_lds") && value >= 0 && value <= 2) { tuning().wire_rx_lds = value; return QFEC_OK; }
     if (!strcmp(key, "frame_rows") && value >= 1 && value <= 4) { tuning().frame_rows = value; return QFEC_OK; }
