@@ -232,7 +232,7 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "encode_impl"      0 all rows | 1 row loop
  *   "recon_impl"       -1 auto | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B
  *   "recon_compact"    1 tables via the 256-entry table at the record header's offsets | 0 from the record
- *   "recon_full_lines" 1 8-/12-B lanes cover the 16-B columns' span | 0 stop at B
+ *   "recon_full_lines" 1 8-/12-B lanes cover the 16-B columns' span for k < 14 | 2 always | 0 stop at B
  *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies
  *   "host_chunk"       groups per staged host chunk (0: ~32 MiB)
  *   "wire_fused"       1 fused datagram send where a (k, m) instance exists | 0 staged build -> encode -> emit

@@ -496,10 +496,15 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.wpg = (a.cols + 63) / 64;
     a.cols8 = (uint32_t)((block + 7) / 8);
     a.cols12 = (uint32_t)((block + 11) / 12);
-    if (a.vec16 && tuning().recon_full_lines) {
+    // recon_full_lines 1 (auto): for k < 14; 2: always; 0: never
+    const int fl = tuning().recon_full_lines;
+    if (a.vec16 && (fl == 2 || (fl == 1 && c->k < 14))) {
         // cover the 16-B columns' span, which the 16-B body writes anyway (it stays inside
         // the pitch): a row that ends part-way into a 64-B line costs a partial-line write
-        // (B = 1400: 175 -> 176 8-B columns, rows end on 1408 = 22 lines)
+        // (B = 1400: 175 -> 176 8-B columns, rows end on 1408 = 22 lines).  It also reads the
+        // extra 8 B of every survivor, and with k = 16 survivors per row written that costs
+        // more than it saves: RS(16,4) B=1400 5 404 GB/s full against 5 508 partial, RS(10,3)
+        // B=1024 6 009 against 5 949 (interleaved A/B, profiles/r03_recon/r03k_ab.txt)
         a.cols8 = 2u * a.cols;
         a.cols12 = std::max(a.cols12, a.cols * 16u / 12u);
     }
@@ -651,7 +656,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
     if (!strcmp(key, "host_zero_copy") && (value == 0 || value == 1)) { tuning().host_zero_copy = value; return QFEC_OK; }
     if (!strcmp(key, "recon_compact") && value >= 0 && value <= 2) { tuning().recon_compact = value; return QFEC_OK; }
-    if (!strcmp(key, "recon_full_lines") && (value == 0 || value == 1)) { tuning().recon_full_lines = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_full_lines") && value >= 0 && value <= 2) { tuning().recon_full_lines = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_lds") && value >= 0 && value <= 2) { tuning().wire_rx_lds = value; return QFEC_OK; }
     if (!strcmp(key, "frame_rows") && value >= 1 && value <= 4) { tuning().frame_rows = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }

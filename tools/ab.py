@@ -76,7 +76,7 @@ def main():
         ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
         ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
         ("recon impl2 (exact e rows)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),
-        ("recon impl3 (exact e, 8-B lanes)", lambda: (qa.tune("recon_full_lines", 1), qa.tune("recon_impl", 3)), rec,
+        ("recon impl3 (exact e, 8-B lanes, full lines)", lambda: (qa.tune("recon_full_lines", 2), qa.tune("recon_impl", 3)), rec,
          dec_bytes),
         ("recon impl3 partial last line", lambda: (qa.tune("recon_full_lines", 0), qa.tune("recon_impl", 3)), rec,
          dec_bytes),
