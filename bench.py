@@ -829,7 +829,12 @@ def per_call_leg(reps=2000, ref_lib=None, batched=True):
     if ref_lib is not None:  # the cpu_baseline leg's reference system/fec.c
         run(ref_lib, "ref_cpu_")
         return out
+    st0 = qa.percall_stats()
     run(qa.lib(), "gpu_")
+    st = qa.percall_stats()
+    out["gpu_path"] = ("resident server (percall_resident 1, qfec_percall.hpp)" if st["calls"] > st0["calls"]
+                       else "one launch per call (qfec_percall.hpp k_percall)")
+    out["gpu_server_launches"] = st["launches"] - st0["launches"]
     if not batched:
         return out
     # batched: qfec_encode_host (pinned host buffers in and out) per group vs 3 reference calls

@@ -251,8 +251,18 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *                      keeps 3/4 of the waves | 2 whenever they fit 16 KiB | 0 row by row
  *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged
  *   "percall_spin"     1 a per-call launch of one block is waited for by spinning on the completion
- *                      word the kernel stores in coherent pinned memory | 0 hipStreamSynchronize */
+ *                      word the kernel stores in coherent pinned memory | 0 hipStreamSynchronize
+ *   "percall_resident" 1 fec_encode / fec_decode of packets up to 4 KiB go to a resident one-block
+ *                      server that polls a request word in device memory and exits by itself after
+ *                      1 ms without a request | 0 one launch per call (setting 0 stops the servers) */
 int qfec_tune(const char *key, int value);
+
+/* The resident per-call server of the current device (qfec_tune "percall_resident"): out[0] calls
+ * it served, out[1] launches, out[2] relaunches because it had exited (idle) just before a request
+ * arrived, out[3] 1 while its block may still be running (it exits 1 ms after the last request),
+ * out[4] 1 set up | -1 unavailable on this device (device memory not CPU-mapped) | 0 not yet used.
+ * Returns QFEC_OK, or an error without a device. */
+int qfec_percall_stats(unsigned long long out[5]);
 
 int qfec_set_kernel_variant(int variant);
 int qfec_get_kernel_variant(void);

@@ -70,6 +70,14 @@ def tune(key, value):
     check(lib().qfec_tune(key.encode(), int(value)), f"qfec_tune({key})")
 
 
+def percall_stats():
+    """The current device's resident per-call server (include/qfec.h qfec_percall_stats)."""
+    out = (C.c_ulonglong * 5)()
+    check(lib().qfec_percall_stats(out), "qfec_percall_stats")
+    usable = out[4] if out[4] < 2**63 else out[4] - 2**64
+    return {"calls": out[0], "launches": out[1], "relaunches": out[2], "running": bool(out[3]), "usable": usable}
+
+
 def synth_fill(t, seed, stream=None):
     """Fill a device uint8 tensor with quicknet_amd.synth.synth_bytes(seed, t.numel())."""
     check(lib().qfec_synth_fill(_dev_ptr(t, what="synth_fill"), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(stream)),

@@ -28,4 +28,32 @@ struct PcArgs {
 
 hipError_t launch_percall(const PcArgs& a, hipStream_t s);
 
+// ---- the resident per-call server (tuning "percall_resident" 1, the default where the device
+// memory below is host-mapped).  A launch costs ~6 us and reading the packets across PCIe
+// from pinned host memory another ~3-7 us (profiles/r02zk_launch_lat.txt,
+// profiles/r03k_doorbell_probe.txt), so instead one block stays resident on the device between
+// calls: the CPU writes the input packets, the coefficient tables and the request number into
+// device memory it can map (fine-grained, host-visible), the block -- polling that word in its
+// own memory, not across PCIe -- computes the outputs into pinned host memory and stores the
+// request number into a completion word there, and the CPU spins on it.  Only posted writes
+// cross PCIe.  The block exits by itself after kPcIdleTicks without a request (or at once
+// when `stop` is set), so no grid outlives an idle caller, and the host relaunches it when
+// the next request finds it gone.
+constexpr int kPcMaxChunks = 256;             // 16-B columns per packet row (4 KiB)
+constexpr uint64_t kPcIdleTicks = 100000;     // 1 ms at the 100 MHz wall clock
+struct PcBell {                               // fine-grained device memory, written by the CPU
+    uint32_t req;                             // request number (0: none yet)
+    uint32_t stop;                            // 1: exit now
+    uint32_t k, e, chunks, pitch;
+    uint32_t pad[10];
+    uint32_t tab[kPcMaxCoef * 5];             // [e][k] perm tables
+};
+struct PcStatus {                             // coherent pinned host memory, written by the block
+    uint32_t done;                            // the last request served
+    uint32_t state;                           // (launch generation << 1) | running
+    uint32_t pad[14];
+};
+hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,
+                                 uint32_t gen, hipStream_t s);
+
 }  // namespace qfec

@@ -98,6 +98,21 @@ struct DevCtx {
     uint32_t* d_pc_done = nullptr;
     uint32_t pc_seq = 0;
     uint32_t pc_unsynced = 0;       // spin-completed launches since the last stream query
+    // the resident per-call server (qfec_percall.hpp): set up on first use
+    struct PcServer {
+        int usable = 0;              // 0 not tried, 1 ready, -1 unavailable on this device
+        hipStream_t stream = nullptr;
+        PcBell* bell = nullptr;      // fine-grained device memory the CPU stores into
+        uint8_t* in = nullptr;       // ditto: kPcMaxCoef rows of kPcMaxChunks * 16 bytes
+        uint8_t* h_out = nullptr;    // coherent pinned host memory, same shape
+        uint8_t* d_out = nullptr;
+        PcStatus* h_st = nullptr;    // coherent pinned host memory
+        PcStatus* d_st = nullptr;
+        uint32_t req = 0;            // the last request number stored into bell->req
+        uint32_t gen = 0;            // the last launch's generation
+        bool launched = false;
+        unsigned long long calls = 0, launches = 0, relaunches = 0;
+    } srv;
     int init_rc = QFEC_ENODEV;
     // qfec_encode_host: two chunk slots, each with its own stream, event, device buffers
     // and pinned staging (created on first use)
@@ -196,6 +211,153 @@ int ensure_pc(DevCtx& c, size_t bytes) {
     HIP_TRY(hipHostGetDevicePointer((void**)&c.d_pc, c.h_pc, 0));
     c.pc_cap = cap;
     return QFEC_OK;
+}
+
+// ---- the resident per-call server (qfec_percall.hpp)
+std::atomic<int> g_percall_resident{1};  // qfec_tune "percall_resident"
+constexpr size_t kPcSrvBytes = (size_t)kPcMaxCoef * kPcMaxChunks * 16;
+
+// true if [p, p + n) lies inside one readable, writable mapping of this process.  Fine-grained
+// device memory is mapped for the CPU through the PCIe BAR where the BAR spans all of HBM (as on
+// the MI355X); elsewhere its range is reserved without access and a store would fault.
+bool cpu_mapped(const void* p, size_t n) {
+    FILE* f = fopen("/proc/self/maps", "r");
+    if (!f) return false;
+    const unsigned long a = (unsigned long)p, b = a + n;
+    char line[512];
+    bool ok = false;
+    while (fgets(line, sizeof line, f)) {
+        unsigned long lo = 0, hi = 0;
+        char perm[8] = {0};
+        if (sscanf(line, "%lx-%lx %7s", &lo, &hi, perm) != 3) continue;
+        if (lo <= a && a < hi) {
+            ok = b <= hi && perm[0] == 'r' && perm[1] == 'w';
+            break;
+        }
+    }
+    fclose(f);
+    return ok;
+}
+
+void pc_server_stop_all();
+
+// allocate the server's buffers once; on any failure the device keeps the launch-per-call path
+int pc_server_setup(DevCtx& c) {
+    DevCtx::PcServer& s = c.srv;
+    if (s.usable) return s.usable > 0 ? QFEC_OK : QFEC_EHIP;
+    s.usable = -1;
+    auto fail = [&](hipError_t e, const char* what) {
+        (void)hipGetLastError();
+        fprintf(stderr, "[qfec] per-call server unavailable (%s: %s); launching per call\n", what,
+                hipGetErrorString(e));
+        return QFEC_EHIP;
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess) return fail(e, "stream");
+    if ((e = hipExtMallocWithFlags((void**)&s.bell, sizeof(PcBell), hipDeviceMallocFinegrained)) != hipSuccess)
+        return fail(e, "bell");
+    if ((e = hipExtMallocWithFlags((void**)&s.in, kPcSrvBytes, hipDeviceMallocFinegrained)) != hipSuccess)
+        return fail(e, "input rows");
+    if ((e = hipHostMalloc((void**)&s.h_out, kPcSrvBytes, hipHostMallocMapped | hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0)) != hipSuccess)
+        return fail(e, "output rows");
+    if ((e = hipHostMalloc((void**)&s.h_st, sizeof(PcStatus), hipHostMallocMapped | hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&s.d_st, s.h_st, 0)) != hipSuccess)
+        return fail(e, "status word");
+    if (!cpu_mapped(s.bell, sizeof(PcBell)) || !cpu_mapped(s.in, kPcSrvBytes)) {
+        fprintf(stderr, "[qfec] per-call server unavailable (device memory not CPU-mapped); launching per call\n");
+        return QFEC_EHIP;
+    }
+    memset(s.bell, 0, sizeof(PcBell));
+    memset(s.h_st, 0, sizeof(PcStatus));
+    __builtin_ia32_sfence();
+    static std::once_flag once;
+    std::call_once(once, [] { atexit(pc_server_stop_all); });  // after the runtime's own handlers
+    s.usable = 1;
+    return QFEC_OK;
+}
+
+bool pc_server_alive(const DevCtx::PcServer& s) {
+    return s.launched && __atomic_load_n(&s.h_st->state, __ATOMIC_ACQUIRE) != (s.gen << 1);
+}
+
+// stop the server and wait for it (a few microseconds: it polls `stop`)
+hipError_t pc_server_stop(DevCtx& c) {
+    DevCtx::PcServer& s = c.srv;
+    if (s.usable <= 0 || !s.launched) return hipSuccess;
+    __atomic_store_n(&s.bell->stop, 1u, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+    hipError_t e = hipStreamSynchronize(s.stream);
+    __atomic_store_n(&s.bell->stop, 0u, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+    s.launched = false;
+    return e;
+}
+
+// one call through the server: QFEC_OK, or an error (the server then is stopped)
+int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, unsigned char* const* in,
+                   unsigned char* const* out, int sz, size_t pitch) {
+    DevCtx::PcServer& s = c.srv;
+    PcBell* b = s.bell;
+    for (int r = 0; r < k; ++r) memcpy(s.in + (size_t)r * pitch, in[r], (size_t)sz);
+    uint32_t hdr[4] = {(uint32_t)k, (uint32_t)e, (uint32_t)(pitch / 16), (uint32_t)pitch};
+    uint32_t t5[kPcMaxCoef * 5];
+    for (int i = 0; i < k * e; ++i) memcpy(&t5[i * 5], &tab[(size_t)i * QFEC_TAB_STRIDE], 5 * sizeof(uint32_t));
+    memcpy(&b->k, hdr, sizeof hdr);
+    memcpy(b->tab, t5, (size_t)k * e * 5 * sizeof(uint32_t));
+    // the device memory is write-combined for the CPU: the rows and tables must be out of the
+    // write-combining buffers before the request number is
+    __builtin_ia32_sfence();
+    const uint32_t prev = s.req;
+    uint32_t req = prev + 1;
+    if (req == 0) req = 1;
+    s.req = req;
+    __atomic_store_n(&b->req, req, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+    auto launch = [&]() {
+        ++s.gen;
+        s.launched = true;
+        ++s.launches;
+        return launch_percall_server(b, s.in, s.d_out, s.d_st, prev, s.gen, s.stream);
+    };
+    hipError_t he = hipSuccess;
+    if (!pc_server_alive(s)) he = launch();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 1; he == hipSuccess; ++it) {
+        if (__atomic_load_n(&s.h_st->done, __ATOMIC_ACQUIRE) == req) {
+            ++s.calls;
+            for (int j = 0; j < e; ++j) memcpy(out[j], s.h_out + (size_t)j * pitch, (size_t)sz);
+            return QFEC_OK;
+        }
+        __builtin_ia32_pause();
+        if ((it & 63) == 0 && __atomic_load_n(&s.h_st->state, __ATOMIC_ACQUIRE) == (s.gen << 1)) {
+            // the server went idle and exited just before the request arrived: its exit is
+            // published after its last completion, so the request is not served -- relaunch
+            if (__atomic_load_n(&s.h_st->done, __ATOMIC_ACQUIRE) == req) continue;
+            ++s.relaunches;
+            he = launch();
+        }
+        if ((it & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            set_error("per-call server: request %u not served within 2 s", req);
+            (void)pc_server_stop(c);
+            return QFEC_EHIP;
+        }
+    }
+    (void)pc_server_stop(c);
+    return hip_fail(he, "per-call server launch");
+}
+
+void pc_server_stop_all() {
+    for (DevCtx& c : g_ctx) {
+        if (c.srv.usable <= 0 || !c.srv.launched) continue;
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(c.device);
+        (void)pc_server_stop(c);
+        (void)hipSetDevice(prev);
+    }
 }
 
 int ensure_small(DevCtx& c, size_t words) {
@@ -662,8 +824,37 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
     if (!strcmp(key, "percall_spin") && (value == 0 || value == 1)) { g_percall_spin = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_resident") && (value == 0 || value == 1)) {
+        g_percall_resident = value;
+        if (!value)
+            for (DevCtx& c : g_ctx) {
+                std::lock_guard<std::mutex> lk(c.mu);
+                if (c.srv.usable <= 0 || !c.srv.launched) continue;
+                int prev = 0;
+                (void)hipGetDevice(&prev);
+                (void)hipSetDevice(c.device);
+                (void)pc_server_stop(c);
+                (void)hipSetDevice(prev);
+            }
+        return QFEC_OK;
+    }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
     return QFEC_EINVAL;
+}
+
+int qfec_percall_stats(unsigned long long out[5]) {
+    if (!out) return QFEC_EINVAL;
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const DevCtx::PcServer& s = ctx->srv;
+    out[0] = s.calls;
+    out[1] = s.launches;
+    out[2] = s.relaunches;
+    out[3] = s.usable > 0 && pc_server_alive(s);
+    out[4] = (unsigned long long)(long long)s.usable;
+    return QFEC_OK;
 }
 
 qfec_code* qfec_code_new(int flavour, int k, int m) {
@@ -1923,6 +2114,9 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
     const size_t pitch = round_up((size_t)sz, 16);
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!dev && k * e <= kPcMaxCoef && g_percall_fast.load() && !is_device_ptr(out[0])) {
+        // the resident server (packets of up to 4 KiB)
+        if (pitch <= (size_t)kPcMaxChunks * 16 && g_percall_resident.load() && pc_server_setup(*ctx) == QFEC_OK)
+            return pc_server_call(*ctx, tab, k, e, in, out, sz, pitch);
         // host packets: CPU staging into mapped pinned memory, one launch, one synchronise
         if ((rc = ensure_pc(*ctx, (size_t)(k + e) * pitch))) return rc;
         for (int c = 0; c < k; ++c) memcpy(ctx->h_pc + (size_t)c * pitch, in[c], (size_t)sz);

@@ -210,20 +210,25 @@ def test_two_ranks_share_gpu_match_single(oracle):
     assert all(x[1] for x in out)  # every rank's reconstruct restored its slice
 
 
-@pytest.mark.parametrize("fast,spin", [(1, 1), (1, 0), (0, 1)])
-@pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 37), (3, 5, 2052), (16, 20, 1400), (3, 5, 8200)])
-def test_per_packet_paths_vs_oracle(oracle, fast, spin, k, n, sz):
-    """fec_encode / fec_decode on host packets through the per-call kernel (percall_fast 1:
-    mapped pinned staging, tables in the kernel arguments, one launch; percall_spin 1: the
-    caller waits on the kernel's completion word, 0: on the stream) and through the staged DMA
-    path (percall_fast 0), against the oracle's fec.c restatement.  sz 8200 needs a
-    multi-block launch, which is always waited for on the stream."""
+@pytest.mark.parametrize("fast,spin,resident", [(1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 1, 0)])
+@pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 37), (3, 5, 2052), (16, 20, 1400), (3, 5, 4096),
+                                    (3, 5, 8200), (1, 161, 64), (160, 161, 100)])
+def test_per_packet_paths_vs_oracle(oracle, fast, spin, resident, k, n, sz):
+    """fec_encode / fec_decode on host packets through the resident server (percall_resident 1:
+    rows and tables stored into device memory, a request word polled by one resident block),
+    the per-call kernel (percall_fast 1: mapped pinned staging, tables in the kernel arguments,
+    one launch; percall_spin 1: the caller waits on the kernel's completion word, 0: on the
+    stream) and the staged DMA path (percall_fast 0), against the oracle's fec.c restatement.
+    sz 4096 is the server's largest packet; sz 8200 needs a multi-block launch, which is always
+    waited for on the stream; (1, 161) and (160, 161) are the 160-coefficient limit's two ends."""
     rng = np.random.default_rng(k * 100 + sz)
     fp = qa.FecParms(k, n)
     full = fp.matrix
     data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
     qa.tune("percall_fast", fast)
     qa.tune("percall_spin", spin)
+    qa.tune("percall_resident", resident)
+    before = qa.percall_stats()
     try:
         for idx in range(k, n):
             dst = np.zeros(sz, np.uint8)
@@ -242,31 +247,111 @@ def test_per_packet_paths_vs_oracle(oracle, fast, spin, k, n, sz):
         assert rc == rc2 == 0
         assert np.array_equal(pk, pk2) and np.array_equal(ix, ix2)
         assert np.array_equal(pk, data)
+        after = qa.percall_stats()
+        served = after["calls"] - before["calls"]
+        if fast and resident and sz <= 4096 and after["usable"] > 0:
+            assert served == (n - k) * 2 + (1 if min(n - k, k) else 0), served  # every encode + the decode
+        else:
+            assert served == 0
     finally:
         qa.tune("percall_fast", 1)
         qa.tune("percall_spin", 1)
+        qa.tune("percall_resident", 1)
 
 
-def test_per_packet_spin_back_to_back(oracle):
-    """2 000 back-to-back fec_encode calls on fresh data each, waited for on the kernel's
-    completion word: every output is the oracle's (a stale completion word or an output read
-    before it landed would show up as a mismatch)."""
-    k, n, sz = 10, 13, 1028
-    fp = qa.FecParms(k, n)
+def _encode_checker(oracle, fp, k, n):
     full = fp.matrix
-    mul = np.array([[oracle.mul(a, b) for b in range(256)] for a in sorted(set(full[k:].ravel().tolist()))], np.uint8)
-    row_of = {c: i for i, c in enumerate(sorted(set(full[k:].ravel().tolist())))}
-    rng = np.random.default_rng(2024)
-    qa.tune("percall_spin", 1)
-    for call in range(2000):
-        data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
-        idx = k + call % (n - k)
-        dst = np.zeros(sz, np.uint8)
-        fp.encode(data, dst, idx, sz)
-        exp = np.zeros(sz, np.uint8)
+    coefs = sorted(set(full[k:].ravel().tolist()))
+    mul = np.array([[oracle.mul(a, b) for b in range(256)] for a in coefs], np.uint8)
+    row_of = {c: i for i, c in enumerate(coefs)}
+
+    def expect(data, idx):
+        exp = np.zeros(data.shape[1], np.uint8)
         for c in range(k):
             exp ^= mul[row_of[int(full[idx, c])]][data[c]]
-        assert np.array_equal(dst, exp), call
+        return exp
+    return expect
+
+
+@pytest.mark.parametrize("resident", [1, 0])
+def test_per_packet_spin_back_to_back(oracle, resident):
+    """2 000 back-to-back fec_encode calls on fresh data each, through the resident server (1)
+    or one launch per call waited for on its completion word (0): every output is the oracle's
+    (a stale completion word, rows read before the CPU's stores landed, or an output read before
+    it landed would show up as a mismatch).  Back to back, the server is launched about once."""
+    k, n, sz = 10, 13, 1028
+    fp = qa.FecParms(k, n)
+    expect = _encode_checker(oracle, fp, k, n)
+    rng = np.random.default_rng(2024)
+    qa.tune("percall_spin", 1)
+    qa.tune("percall_resident", resident)
+    try:
+        before = qa.percall_stats()
+        for call in range(2000):
+            data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+            idx = k + call % (n - k)
+            dst = np.zeros(sz, np.uint8)
+            fp.encode(data, dst, idx, sz)
+            assert np.array_equal(dst, expect(data, idx)), call
+        st = qa.percall_stats()
+        if resident and st["usable"] > 0:
+            assert st["calls"] - before["calls"] == 2000
+            # the Python loop between calls (fresh data, the oracle check) stays well under 1 ms
+            assert st["launches"] - before["launches"] <= 20, st
+        else:
+            assert st["calls"] == before["calls"]
+    finally:
+        qa.tune("percall_resident", 1)
+
+
+def test_percall_server_idle_exit_and_relaunch(oracle):
+    """The resident server exits by itself 1 ms after its last request (so no block outlives an
+    idle caller, and a device synchronise never waits on it for long), a call after an idle gap
+    relaunches it, calls spaced around the 1 ms idle limit (where a request can meet a server on
+    its way out) are all served correctly, and percall_resident 0 stops it at once."""
+    import time
+
+    import torch
+    k, n, sz = 10, 13, 1028
+    fp = qa.FecParms(k, n)
+    expect = _encode_checker(oracle, fp, k, n)
+    rng = np.random.default_rng(77)
+
+    def call(i):
+        data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+        idx = k + i % (n - k)
+        dst = np.zeros(sz, np.uint8)
+        fp.encode(data, dst, idx, sz)
+        assert np.array_equal(dst, expect(data, idx)), i
+
+    qa.tune("percall_resident", 1)
+    call(0)
+    st = qa.percall_stats()
+    if st["usable"] < 0:
+        pytest.skip("device memory not CPU-mapped on this box: the launch-per-call path serves")
+    assert st["usable"] == 1 and st["calls"] >= 1
+    time.sleep(0.02)
+    assert not qa.percall_stats()["running"]  # exited within 20 ms (its limit is 1 ms idle)
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 0.5
+    l0 = qa.percall_stats()["launches"]
+    call(1)
+    st = qa.percall_stats()
+    assert st["launches"] == l0 + 1 and st["running"]
+    # gaps from 0.5 to 1.5 ms: some requests find the server alive, some find it gone, some
+    # arrive as it leaves
+    for i in range(300):
+        t = time.perf_counter() + (0.5 + (i % 11) * 0.1) * 1e-3
+        while time.perf_counter() < t:
+            pass
+        call(2 + i)
+    st = qa.percall_stats()
+    assert st["launches"] > l0 + 1  # the longer gaps did meet an exited server
+    qa.tune("percall_resident", 0)
+    assert not qa.percall_stats()["running"]
+    qa.tune("percall_resident", 1)
+    call(400)
 
 
 def _gf_row(oracle, c, row):

@@ -2,7 +2,7 @@
 """Per-call cost of the unchanged drop-in (fec_encode / fec_decode on host packets, RS(10,3),
 sz 1028) under qfec_tune knob settings, alternated in one process; medians over rounds.
 
-  python tools/percall_ab.py [--variants "percall_spin=1;percall_spin=0" --rounds 5 --reps 2000]
+  python tools/percall_ab.py [--variants "percall_resident=1;percall_resident=0" --rounds 5 --reps 2000]
 """
 import argparse
 import os
@@ -13,12 +13,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
+bench._load()
 import quicknet_amd as qa  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="percall_spin=1;percall_spin=0")
+    ap.add_argument("--variants", default="percall_resident=1;percall_resident=0,percall_spin=1;percall_resident=0,percall_spin=0")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=2000)
     a = ap.parse_args()
