@@ -50,81 +50,100 @@ __global__ void __launch_bounds__(256) k_percall(PcArgs a) {
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {  // polls: past the caches, no invalidation
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ __forceinline__ void st_rel_sys(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One block of 256 lanes, lane = one 16-B column of the packets.  Lane 0 polls the request word
-// (system-scope loads that bypass the caches; a system-scope acquire fence once a request is
-// seen invalidates them, so the block then reads what the CPU wrote); the tables go to LDS once
-// per request.  Every iteration ends in the same place
-// for every lane, and the loop exits on idle or stop, so the grid always drains.
+// e output columns from k input rows (x: the first min(k, KB) rows, loaded by the caller) with
+// the [e][k] tables in LDS
+template <int KB>
+__device__ __forceinline__ void pc_serve_cols(const uint8_t* in, uint8_t* out, const uint32_t* s_tab, uint32_t k,
+                                              uint32_t e, uint32_t pitch, uint64_t off, const uint4 (&x0)[KB]) {
+    for (uint32_t j0 = 0; j0 < e; j0 += 4) {
+        const uint32_t ej = min(4u, e - j0);
+        uint4 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = make_uint4(0, 0, 0, 0);
+        for (uint32_t c0 = 0; c0 < k; c0 += KB) {
+            uint4 x[KB];
+#pragma unroll
+            for (int i = 0; i < KB; ++i) {
+                if (c0 == 0) {
+                    x[i] = x0[i];
+                } else {
+                    const uint32_t c = min(c0 + i, k - 1);
+                    x[i] = *reinterpret_cast<const uint4*>(in + (uint64_t)c * pitch + off);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < KB; ++i) {
+                if (c0 + i >= k) continue;
+                Sel s[4];
+                sel16(s, x[i]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if ((uint32_t)j < ej) gf_mac16(acc[j], s, s_tab + ((j0 + j) * k + c0 + i) * 5);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if ((uint32_t)j < ej) *reinterpret_cast<uint4*>(out + (uint64_t)(j0 + j) * pitch + off) = acc[j];
+    }
+}
+
+// One block of 256 lanes, lane = one 16-B column of the packets.  Lane 0 polls the 8-byte request
+// word (system-scope loads that bypass the caches), which carries the call's shape; a
+// system-scope acquire fence once a request is seen invalidates the caches, so the block then
+// reads what the CPU wrote.  Each lane issues its first 16 input rows' loads before the table
+// loads into LDS, so the two round trips overlap.  Every iteration ends in the same place for
+// every lane, and the loop exits on idle or stop, so the grid always drains.
 __global__ void __launch_bounds__(256) k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st,
                                                         uint32_t served, uint32_t gen) {
+    constexpr int KB = 16;
     __shared__ uint32_t s_tab[kPcMaxCoef * 5];
-    __shared__ uint32_t s_req, s_quit, s_k, s_e, s_chunks, s_pitch;
+    __shared__ uint64_t s_bell;
+    __shared__ uint32_t s_quit;
     const uint32_t t = threadIdx.x;
     if (t == 0) st_rel_sys(&st->state, (gen << 1) | 1u);
     uint64_t t0 = wall_clock64();
     for (;;) {
         if (t == 0) {
-            uint32_t r = served, quit = 0;
+            uint64_t b = 0;
+            uint32_t quit = 0;
             for (;;) {
-                r = ld_sys(&bell->req);
-                if (r != served) break;
+                b = ld_sys64(&bell->bell);
+                if ((uint32_t)b != served) break;
                 if (ld_sys(&bell->stop) || wall_clock64() - t0 > kPcIdleTicks) {
                     quit = 1;
                     break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(1);
             }
-            s_req = r;
+            if (!quit) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: what the CPU wrote first
+            s_bell = b;
             s_quit = quit;
-            if (!quit) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: what the CPU wrote first
-                s_k = ld_sys(&bell->k);
-                s_e = ld_sys(&bell->e);
-                s_chunks = ld_sys(&bell->chunks);
-                s_pitch = ld_sys(&bell->pitch);
-            }
         }
         __syncthreads();
         if (s_quit) break;
-        const uint32_t r = s_req, k = s_k, e = s_e, chunks = s_chunks, pitch = s_pitch;
+        const uint64_t b = s_bell;
+        const uint32_t r = (uint32_t)b, k = (uint32_t)(b >> 32) & 0xFFu, e = (uint32_t)(b >> 40) & 0xFFu,
+                       chunks = (uint32_t)(b >> 48) + 1u, pitch = chunks * 16u;
+        const uint64_t off = (uint64_t)t * 16u;
+        const bool col = t < chunks;
+        uint4 x0[KB];
+#pragma unroll
+        for (int i = 0; i < KB; ++i) {
+            x0[i] = make_uint4(0, 0, 0, 0);
+            if (col && (uint32_t)i < k) x0[i] = *reinterpret_cast<const uint4*>(in + (uint64_t)i * pitch + off);
+        }
         for (uint32_t i = t; i < k * e * 5; i += 256) s_tab[i] = bell->tab[i];
         __syncthreads();
-        if (t < chunks) {
-            const uint64_t off = (uint64_t)t * 16u;
-            constexpr int KB = 16;
-            for (uint32_t j0 = 0; j0 < e; j0 += 4) {
-                const uint32_t ej = min(4u, e - j0);
-                uint4 acc[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) acc[j] = make_uint4(0, 0, 0, 0);
-                for (uint32_t c0 = 0; c0 < k; c0 += KB) {
-                    uint4 x[KB];
-#pragma unroll
-                    for (int i = 0; i < KB; ++i) {
-                        const uint32_t c = min(c0 + i, k - 1);
-                        x[i] = *reinterpret_cast<const uint4*>(in + (uint64_t)c * pitch + off);
-                    }
-#pragma unroll
-                    for (int i = 0; i < KB; ++i) {
-                        if (c0 + i >= k) continue;
-                        Sel s[4];
-                        sel16(s, x[i]);
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if ((uint32_t)j < ej) gf_mac16(acc[j], s, s_tab + ((j0 + j) * k + c0 + i) * 5);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if ((uint32_t)j < ej) *reinterpret_cast<uint4*>(out + (uint64_t)(j0 + j) * pitch + off) = acc[j];
-            }
-        }
+        if (col) pc_serve_cols<KB>(in, out, s_tab, k, e, pitch, off, x0);
         __threadfence_system();  // every lane's outputs reach the host before the completion word
-        __syncthreads();
+        __syncthreads();         // (and no lane still reads s_tab when the next request refills it)
         if (t == 0) st_rel_sys(&st->done, r);
         served = r;
         t0 = wall_clock64();

@@ -42,12 +42,16 @@ hipError_t launch_percall(const PcArgs& a, hipStream_t s);
 constexpr int kPcMaxChunks = 256;             // 16-B columns per packet row (4 KiB)
 constexpr uint64_t kPcIdleTicks = 100000;     // 1 ms at the 100 MHz wall clock
 struct PcBell {                               // fine-grained device memory, written by the CPU
-    uint32_t req;                             // request number (0: none yet)
+    // the request word: number (low 32 bits, 0: none yet) | k << 32 | e << 40 | (chunks - 1) << 48,
+    // stored as one 8-byte write, so the block learns the shape with the request (one round trip)
+    uint64_t bell;
     uint32_t stop;                            // 1: exit now
-    uint32_t k, e, chunks, pitch;
-    uint32_t pad[10];
+    uint32_t pad[13];
     uint32_t tab[kPcMaxCoef * 5];             // [e][k] perm tables
 };
+__host__ __device__ constexpr uint64_t pc_bell(uint32_t req, uint32_t k, uint32_t e, uint32_t chunks) {
+    return (uint64_t)req | ((uint64_t)k << 32) | ((uint64_t)e << 40) | ((uint64_t)(chunks - 1) << 48);
+}
 struct PcStatus {                             // coherent pinned host memory, written by the block
     uint32_t done;                            // the last request served
     uint32_t state;                           // (launch generation << 1) | running

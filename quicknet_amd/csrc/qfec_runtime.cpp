@@ -108,7 +108,9 @@ struct DevCtx {
         uint8_t* d_out = nullptr;
         PcStatus* h_st = nullptr;    // coherent pinned host memory
         PcStatus* d_st = nullptr;
-        uint32_t req = 0;            // the last request number stored into bell->req
+        uint32_t req = 0;            // the last request number stored into the bell word
+        uint32_t tab_last[kPcMaxCoef * 5];  // the tables the bell holds (tab_bytes of them)
+        size_t tab_bytes = 0;
         uint32_t gen = 0;            // the last launch's generation
         bool launched = false;
         unsigned long long calls = 0, launches = 0, relaunches = 0;
@@ -302,19 +304,24 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
     DevCtx::PcServer& s = c.srv;
     PcBell* b = s.bell;
     for (int r = 0; r < k; ++r) memcpy(s.in + (size_t)r * pitch, in[r], (size_t)sz);
-    uint32_t hdr[4] = {(uint32_t)k, (uint32_t)e, (uint32_t)(pitch / 16), (uint32_t)pitch};
+    // the tables go out only when they differ from the last call's (fec_encode of one parity
+    // index, or a repeated loss pattern, sends none)
+    const size_t tb = (size_t)k * e * 5 * sizeof(uint32_t);
     uint32_t t5[kPcMaxCoef * 5];
     for (int i = 0; i < k * e; ++i) memcpy(&t5[i * 5], &tab[(size_t)i * QFEC_TAB_STRIDE], 5 * sizeof(uint32_t));
-    memcpy(&b->k, hdr, sizeof hdr);
-    memcpy(b->tab, t5, (size_t)k * e * 5 * sizeof(uint32_t));
+    if (tb != s.tab_bytes || memcmp(s.tab_last, t5, tb)) {
+        memcpy(b->tab, t5, tb);
+        memcpy(s.tab_last, t5, tb);
+        s.tab_bytes = tb;
+    }
     // the device memory is write-combined for the CPU: the rows and tables must be out of the
-    // write-combining buffers before the request number is
+    // write-combining buffers before the request word is
     __builtin_ia32_sfence();
     const uint32_t prev = s.req;
     uint32_t req = prev + 1;
     if (req == 0) req = 1;
     s.req = req;
-    __atomic_store_n(&b->req, req, __ATOMIC_RELEASE);
+    __atomic_store_n(&b->bell, pc_bell(req, (uint32_t)k, (uint32_t)e, (uint32_t)(pitch / 16)), __ATOMIC_RELEASE);
     __builtin_ia32_sfence();
     auto launch = [&]() {
         ++s.gen;
@@ -811,7 +818,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
     if (!strcmp(key, "wire_chunk") && value >= 0) { tuning().wire_chunk = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_send_wave") && (value == 0 || value == 1)) { tuning().wire_send_wave = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_send_wave") && value >= 0 && value <= 2) { tuning().wire_send_wave = value; return QFEC_OK; }
     if (!strcmp(key, "wire_line") && (value == 0 || value == 1)) { tuning().wire_line = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_tail") && (value == 0 || value == 1)) { tuning().wire_rx_tail = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
@@ -2102,7 +2109,18 @@ struct fec_handle {
     int k, n;
     qfec_code* code;
     std::vector<uint8_t> full;  // n x k systematic matrix (identity on top)
+    // per-call tables, built once (the reference rebuilds its decode matrix on every call,
+    // fec.c:778-808; here only the first call with a given pattern pays for the inversion)
+    std::mutex mu;
+    std::vector<std::vector<uint32_t>> enc_tab;  // [index] perm tables of parity row `index`
+    struct Dec {
+        std::vector<int> idx;    // the shuffled index[] this entry is for
+        std::vector<int> slots;  // slots holding parity: the rows to recover
+        std::vector<uint32_t> tab;
+    };
+    std::unordered_map<uint64_t, std::shared_ptr<const Dec>> dec;  // keyed by a hash of the shuffled index[]
 };
+constexpr size_t kFecDecCacheMax = 4096;
 
 // run `rows` (e x k coefficient rows) over k input packets of sz bytes -> e outputs
 int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* const* in, unsigned char* const* out,
@@ -2202,6 +2220,7 @@ void* fec_new(int k, int n) {
     for (int i = 0; i < k; ++i) h->full[(size_t)i * k + i] = 1;
     memcpy(h->full.data() + (size_t)k * k, rows.data(), rows.size());
     h->code = make_code(k, n - k, std::move(rows), 0);
+    h->enc_tab.resize((size_t)n);
     return h;
 }
 
@@ -2243,10 +2262,18 @@ void fec_encode(void* code, unsigned char** src, unsigned char* dst, int index, 
         return;
     }
     if (sz <= 0) return;
-    std::vector<uint32_t> tab((size_t)k * QFEC_TAB_STRIDE);
-    for (int i = 0; i < k; ++i) perm_entry(h->full[(size_t)index * k + i], &tab[(size_t)i * QFEC_TAB_STRIDE]);
+    const std::vector<uint32_t>* tab = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        std::vector<uint32_t>& t = h->enc_tab[(size_t)index];
+        if (t.empty()) {
+            t.resize((size_t)k * QFEC_TAB_STRIDE);
+            for (int i = 0; i < k; ++i) perm_entry(h->full[(size_t)index * k + i], &t[(size_t)i * QFEC_TAB_STRIDE]);
+        }
+        tab = &t;  // never resized again: stable after the lock is released
+    }
     unsigned char* outs[1] = {dst};
-    int rc = apply_rows(tab, k, 1, src, outs, sz);
+    int rc = apply_rows(*tab, k, 1, src, outs, sz);
     if (rc) fprintf(stderr, "[qfec] fec_encode: %s\n", qfec_last_error());
 }
 
@@ -2263,36 +2290,51 @@ int fec_decode(void* code, unsigned char** pkt, int* index, int sz) {
         std::swap(index[i], index[c]);
         std::swap(pkt[i], pkt[c]);
     }
-    // build_decode_matrix (fec.c:778-808)
-    std::vector<uint8_t> dm((size_t)k * k, 0);
-    for (int r = 0; r < k; ++r) {
-        if (index[r] < k) {
-            dm[(size_t)r * k + r] = 1;
-        } else if (index[r] < n) {
-            memcpy(&dm[(size_t)r * k], &h->full[(size_t)index[r] * k], (size_t)k);
-        } else {
+    for (int r = 0; r < k; ++r)
+        if (index[r] >= n) {
             fprintf(stderr, "decode: invalid index %d (max %d)\n", index[r], n - 1);
             return 1;
         }
+    // the pattern's recovery rows, cached per shuffled index[]
+    uint64_t key = 1469598103934665603ull;  // FNV-1a over the indices
+    for (int r = 0; r < k; ++r) key = (key ^ (uint64_t)(uint32_t)index[r]) * 1099511628211ull;
+    std::shared_ptr<const fec_handle::Dec> d;  // held for the call: a cache clear on another thread does not free it
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        auto it = h->dec.find(key);
+        if (it != h->dec.end() && std::equal(index, index + k, it->second->idx.begin())) d = it->second;
     }
-    if (!gf_invert(dm.data(), k)) {
-        fprintf(stderr, "singular matrix\n");
-        return 1;
+    if (!d) {
+        // build_decode_matrix (fec.c:778-808)
+        std::vector<uint8_t> dm((size_t)k * k, 0);
+        for (int r = 0; r < k; ++r) {
+            if (index[r] < k) dm[(size_t)r * k + r] = 1;
+            else memcpy(&dm[(size_t)r * k], &h->full[(size_t)index[r] * k], (size_t)k);
+        }
+        if (!gf_invert(dm.data(), k)) {
+            fprintf(stderr, "singular matrix\n");
+            return 1;
+        }
+        auto fresh = std::make_shared<fec_handle::Dec>();
+        fresh->idx.assign(index, index + k);
+        // rows to recover: slots holding parity (fec.c:840-858)
+        for (int r = 0; r < k; ++r)
+            if (index[r] >= k) fresh->slots.push_back(r);
+        const int e = (int)fresh->slots.size();
+        fresh->tab.resize((size_t)e * k * QFEC_TAB_STRIDE);
+        for (int j = 0; j < e; ++j)
+            for (int c = 0; c < k; ++c)
+                perm_entry(dm[(size_t)fresh->slots[j] * k + c], &fresh->tab[((size_t)j * k + c) * QFEC_TAB_STRIDE]);
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (h->dec.size() >= kFecDecCacheMax) h->dec.clear();
+        h->dec[key] = fresh;  // a hash collision replaces the older pattern
+        d = std::move(fresh);
     }
-    if (sz <= 0) return 0;
-    // rows to recover: slots holding parity (fec.c:840-858)
-    std::vector<int> slots;
-    for (int r = 0; r < k; ++r)
-        if (index[r] >= k) slots.push_back(r);
-    if (slots.empty()) return 0;
-    const int e = (int)slots.size();
-    std::vector<uint32_t> tab((size_t)e * k * QFEC_TAB_STRIDE);
-    for (int j = 0; j < e; ++j)
-        for (int c = 0; c < k; ++c)
-            perm_entry(dm[(size_t)slots[j] * k + c], &tab[((size_t)j * k + c) * QFEC_TAB_STRIDE]);
-    std::vector<unsigned char*> outs(e);
-    for (int j = 0; j < e; ++j) outs[j] = pkt[slots[j]];
-    const int rc = apply_rows(tab, k, e, pkt, outs.data(), sz);
+    if (sz <= 0 || d->slots.empty()) return 0;
+    const int e = (int)d->slots.size();
+    unsigned char* outs[256];
+    for (int j = 0; j < e; ++j) outs[j] = pkt[d->slots[j]];
+    const int rc = apply_rows(d->tab, k, e, pkt, outs, sz);
     if (rc) {
         fprintf(stderr, "[qfec] fec_decode: %s\n", qfec_last_error());
         return 1;

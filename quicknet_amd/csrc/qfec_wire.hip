@@ -755,7 +755,13 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
 #ifndef FRAME_WAVES
 #define FRAME_WAVES 3  // waves per SIMD the one-pass frame send is compiled for (A/B: 4 spills)
 #endif
-template <int K, int M, int GPW, int FP = 0>
+//
+// NP (GPW 1 only): passes over the body's chunks.  NP 1 covers wire pitches up to 1088 (body
+// chunks 4 .. wire_pitch / 16 - 1, lanes past them idle); NP 2 covers 1104 .. 2112, e.g. the
+// 1472-B pitch of 1400-B (MTU-size) payloads: pass 0 chunks 4..67, pass 1 chunks 68.. on the
+// first wire_pitch / 16 - 68 lanes.  Row sums accumulate over the passes, so line 0 is
+// unchanged.
+template <int K, int M, int GPW, int FP = 0, int NP = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? FRAME_WAVES : 4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
                                                      const int64_t* __restrict__ offsets,
                                                      const int32_t* __restrict__ sizes,
@@ -765,16 +771,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? F
     constexpr int N = K + M, HDR = 13, HEAD = 4, LPG = 64 / GPW;  // lanes per group
     constexpr int FD = FP / 4;                                      // prefix dwords of line 0
     static_assert(FP == 0 || FP == 4 || FP == 12, "frame prefix");
+    static_assert(NP == 1 || GPW == 1, "passes");
     const int lane = threadIdx.x & 63;
-    const int ln = GPW == 1 ? lane : lane % LPG;  // lane within its group: chunk 4 + ln
+    const int ln = GPW == 1 ? lane : lane % LPG;  // lane within its group: chunk 4 + ln (+ 64 per pass)
     const uint64_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));  // wave-uniform
     if (w * GPW >= groups) return;  // whole waves
     // GPW 1: g is wave-uniform (scalar loads of sizes / offsets); GPW 2: two groups per wave,
     // a dead second group still joins the cross-lane sums
     const uint64_t g = GPW == 1 ? w : w * GPW + (uint64_t)(lane / LPG);
     const bool live = GPW == 1 || g < groups;
-    const int t = 4 + ln;
-    const int p = 16 * t - FP - HDR - HEAD;  // payload offset of this chunk's first byte (>= 35)
+    const int tend = GPW == 1 ? (int)(a.wire_pitch / 16) : 4 + LPG;  // body chunks end here
     int size[K], gmax = 0;
     bool ok = false;
     if (live) ok = group_sizes<K, HEAD>(sizes, g, (int)a.pitch, size, gmax);
@@ -786,22 +792,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? F
 #pragma unroll
     for (int i = 0; i < K; ++i) off[i] = ok ? offsets[g * K + i] : 0;
     uint8_t* out_g = a.wire + g * (uint64_t)N * a.wire_pitch;
-    uint4 x[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
-    if (ok) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) x[i] = ldu16(payload + off[i] + min(p, size[i]));
-#pragma unroll
-        for (int i = 0; i < K; ++i) x[i] = mask16(x[i], 0, size[i] - p);
-    }
-    uint32_t ps[N];  // per-lane byte sums of each row's chunk (payload / check bytes)
-#pragma unroll
-    for (int i = 0; i < K; ++i) ps[i] = sum16(x[i], 0);
-    uint4 acc[M];
-    encode_cols<K, M>(x, acc, tab);
-#pragma unroll
-    for (int r = 0; r < M; ++r) pin16(acc[r]);
     // FP: the group's N mask bytes, from the aligned dwords that hold them (scalar loads for
     // GPW 1; an aligned dword never reaches past the page its first byte is on); row r's XOR
     // word is formed where it is used, so no N registers stay live across the encode
@@ -823,23 +813,47 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? F
             return (byte & 0xFFu) * 0x01010101u;
         }
     };
-    uint8_t* out = out_g + 16 * t;
+    uint32_t ps[N];  // per-lane byte sums of each row's chunks (payload / check bytes)
 #pragma unroll
-    for (int r = 0; r < N; ++r) {
-        uint4 v = r < K ? x[r] : acc[r - K];
-        if (r >= K) ps[r] = sum16(v, 0);
-        if constexpr (FP != 0) {  // XOR the frame's bytes only: padding past it stays 0
-            const int total = FP + HDR + (r < K ? size[r] + HEAD : gmax);
-            uint64_t klo, khi;  // bytes of this chunk below the frame's end
-            int rel = total - 16 * t;
-            asm volatile("" : "+v"(rel));  // formed here, after the encode: not hoisted into it
-            keep_words(rel, klo, khi);
-            const uint32_t mr = mm_of(r);
-            const uint64_t m2 = ((uint64_t)mr << 32) | mr;
-            const uint64_t xl = m2 & klo, xh = m2 & khi;
-            v = make_uint4(v.x ^ (uint32_t)xl, v.y ^ (uint32_t)(xl >> 32), v.z ^ (uint32_t)xh, v.w ^ (uint32_t)(xh >> 32));
+    for (int r = 0; r < N; ++r) ps[r] = 0;
+#pragma unroll
+    for (int pp = 0; pp < NP; ++pp) {
+        const int t = 4 + ln + 64 * pp;
+        const bool act = ok && t < tend;         // idle lanes carry zeros: they add nothing to the sums
+        const int p = 16 * t - FP - HDR - HEAD;  // payload offset of this chunk's first byte (>= 35)
+        uint4 x[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) x[i] = make_uint4(0, 0, 0, 0);
+        if (act) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) x[i] = ldu16(payload + off[i] + min(p, size[i]));
+#pragma unroll
+            for (int i = 0; i < K; ++i) x[i] = mask16(x[i], 0, size[i] - p);
         }
-        if (ok) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
+#pragma unroll
+        for (int i = 0; i < K; ++i) ps[i] = sum16(x[i], ps[i]);
+        uint4 acc[M];
+        encode_cols<K, M>(x, acc, tab);
+#pragma unroll
+        for (int r = 0; r < M; ++r) pin16(acc[r]);
+        uint8_t* out = out_g + 16 * t;
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+            uint4 v = r < K ? x[r] : acc[r - K];
+            if (r >= K) ps[r] = sum16(v, ps[r]);
+            if constexpr (FP != 0) {  // XOR the frame's bytes only: padding past it stays 0
+                const int total = FP + HDR + (r < K ? size[r] + HEAD : gmax);
+                uint64_t klo, khi;  // bytes of this chunk below the frame's end
+                int rel = total - 16 * t;
+                asm volatile("" : "+v"(rel));  // formed here, after the encode: not hoisted into it
+                keep_words(rel, klo, khi);
+                const uint32_t mr = mm_of(r);
+                const uint64_t m2 = ((uint64_t)mr << 32) | mr;
+                const uint64_t xl = m2 & klo, xh = m2 & khi;
+                v = make_uint4(v.x ^ (uint32_t)xl, v.y ^ (uint32_t)(xl >> 32), v.z ^ (uint32_t)xh, v.w ^ (uint32_t)(xh >> 32));
+            }
+            if (act) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
+        }
     }
     // ---- line 0
     // line 0's payload dwords (lanes ln 0..15: frame bytes 4 ln .. 4 ln + 3 = datagram dword
@@ -2129,6 +2143,20 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// the one-wave send's mapping for a wire (or frame) pitch that is the 64-B multiple above the row:
+// 1 one group per wave, one pass (1088 B; tuning "wire_send_wave" 2: any pitch 592..1088);
+// 2 two groups per wave (576 B); 5 one group per wave, two passes (1104..2112 B, "wire_send_wave"
+// 2 only: at 1472 B, RS(10,13) x 100k 1400-B payloads, it ran 841 us against 782 for the body +
+// line-0 pair -- the second pass keeps 24 of 64 lanes busy; profiles/r03_wire/r03n_mtu_ab.txt); 0 none
+static int send_wave_gpw(uint64_t wire_pitch) {
+    const int sw = tuning().wire_send_wave;
+    if (!sw) return 0;
+    if (wire_pitch == 576) return 2;
+    if (wire_pitch == 1088 || (sw == 2 && wire_pitch > 576 && wire_pitch < 1088)) return 1;
+    if (sw == 2 && wire_pitch > 1088 && wire_pitch <= 2112) return 5;
+    return 0;
+}
+
 template <int K, int M, int HDR>
 hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s) {
     // body lanes per group cover chunks [TS, tn): the longest datagram the shard pitch allows;
@@ -2139,18 +2167,22 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
     // memory a read-modify-write: tools/wrskel.hip, profiles/r02zn_wrskel.txt)
     const bool line = tuning().wire_line && a.wire_pitch % 64 == 0 &&
                       a.wire_pitch == (HDR + a.pitch + 63) / 64 * 64 && a.wire_pitch / 16 >= (HDR == 13 ? 20u : 16u);
-    // groups that fill a wave exactly (k_pack_wave64): the body's chunks 4.. are 64 lanes at a
-    // 1088-B wire pitch (one group per wave) and 32 at 576 B (two)
-    const int gpw = a.wire_pitch == 1088 ? 1 : a.wire_pitch == 576 ? 2 : 0;
-    if (HDR == 13 && line && gpw && tuning().wire_send_wave) {
+    // one wave per group (k_pack_wave64): the body's chunks 4.. are 64 lanes at a 1088-B wire
+    // pitch (one pass), 32 at 576 B (two groups per wave), up to 128 in two passes above 1088 B
+    // (1472 B: 1400-B payloads)
+    const int gpw = send_wave_gpw(a.wire_pitch);
+    if (HDR == 13 && line && gpw) {
         for (uint64_t g0 = 0; g0 < a.groups; g0 += ((uint64_t)1 << 28)) {
             const uint64_t gn = std::min((uint64_t)1 << 28, a.groups - g0);
             WireArgs b = a;
             b.wire = a.wire + g0 * (uint64_t)(K + M) * a.wire_pitch;
             b.wire_len = a.wire_len + g0 * (K + M);
-            const dim3 grid((unsigned)((gn + 4 * gpw - 1) / (4 * gpw)));
+            const dim3 grid((unsigned)((gn + 4 * (gpw & 3) - 1) / (4 * (gpw & 3))));
             if (gpw == 1)
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 1>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
+                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
+            else if (gpw == 5)
+                hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
                                    a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
             else
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
@@ -2220,8 +2252,11 @@ template <int K, int M>
 hipError_t pack_frames_shape(const WireArgs& a, const FrameSend& fs, int fp, const uint32_t* tab, hipStream_t s,
                              bool* launched) {
     const uint64_t fpitch = a.wire_pitch;
-    const int gpw = fpitch == 1088 ? 1 : fpitch == 576 ? 2 : 0;
-    if (!a.checksum || !gpw || !tuning().wire_send_wave || fpitch != (fp + 13 + a.pitch + 63) / 64 * 64) return hipSuccess;
+    // frames above 1088 B take the two-pass wave whenever the one-wave send is on: the other way
+    // is two calls (datagrams, then frames), 1 577 against 851 us at 1472 B (r03n)
+    int gpw = send_wave_gpw(fpitch);
+    if (!gpw && tuning().wire_send_wave && fpitch > 1088 && fpitch <= 2112) gpw = 5;
+    if (!a.checksum || !gpw || fpitch != (fp + 13 + a.pitch + 63) / 64 * 64) return hipSuccess;
     *launched = true;
     for (uint64_t g0 = 0; g0 < a.groups; g0 += ((uint64_t)1 << 28)) {
         const uint64_t gn = std::min((uint64_t)1 << 28, a.groups - g0);
@@ -2231,14 +2266,16 @@ hipError_t pack_frames_shape(const WireArgs& a, const FrameSend& fs, int fp, con
         FrameSend f = fs;
         f.mask = fs.mask + g0 * (K + M);
         if (fs.conv_hid) f.conv_hid = fs.conv_hid + 2 * g0 * (K + M);
-        const dim3 grid((unsigned)((gn + 4 * gpw - 1) / (4 * gpw)));
-#define QFEC_PF(GPW, FP)                                                                                          \
-    hipLaunchKernelGGL((k_pack_wave64<K, M, GPW, FP>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K, \
+        const dim3 grid((unsigned)((gn + 4 * (gpw & 3) - 1) / (4 * (gpw & 3))));
+#define QFEC_PF(GPW, FP, NP)                                                                                          \
+    hipLaunchKernelGGL((k_pack_wave64<K, M, GPW, FP, NP>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K, \
                        a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, f)
-        if (gpw == 1 && fp == 4) QFEC_PF(1, 4);
-        else if (gpw == 1) QFEC_PF(1, 12);
-        else if (fp == 4) QFEC_PF(2, 4);
-        else QFEC_PF(2, 12);
+        if (gpw == 1 && fp == 4) QFEC_PF(1, 4, 1);
+        else if (gpw == 1) QFEC_PF(1, 12, 1);
+        else if (gpw == 5 && fp == 4) QFEC_PF(1, 4, 2);
+        else if (gpw == 5) QFEC_PF(1, 12, 2);
+        else if (fp == 4) QFEC_PF(2, 4, 1);
+        else QFEC_PF(2, 12, 1);
 #undef QFEC_PF
     }
     return hipGetLastError();

@@ -49,7 +49,7 @@ def oracle_frames(oracle, code, k, n, g, sizes, payload, offs, seq, checksum, ma
                              conv_hid=ch[g * n + j] if ch is not None else None) for j in range(n)]
 
 
-CASES = [(10, 13, 500, 1040, 1), (4, 6, 501, 1040, 1), (8, 12, 13, 1040, 1), (10, 13, 500, 528, 1),
+CASES = [(10, 13, 500, 1040, 1), (4, 6, 501, 1040, 1), (8, 12, 13, 1040, 1), (10, 13, 500, 528, 1), (4, 6, 130, 1408, 1),
          (4, 6, 77, 528, 1), (10, 13, 200, 1408, 1), (10, 13, 150, 1040, 0), (5, 8, 120, 1040, 1)]
 
 

@@ -241,14 +241,21 @@ def test_unpack_row_tails(k, n, checksum, pitch):
     assert ok_rows > G * k // 2
 
 
-@pytest.mark.parametrize("k,n,G,sp,wp", [(10, 13, 500, 1040, 1088), (4, 6, 500, 1040, 1088), (8, 12, 500, 1040, 1088),
-                                         (5, 8, 500, 1040, 1088), (10, 13, 13, 1040, 1088), (10, 13, 500, 528, 576),
-                                         (4, 6, 501, 528, 576), (10, 13, 13, 528, 576)])
-def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp):
+@pytest.mark.parametrize("k,n,G,sp,wp,wave", [(10, 13, 500, 1040, 1088, 1), (4, 6, 500, 1040, 1088, 1),
+                                              (8, 12, 500, 1040, 1088, 1), (5, 8, 500, 1040, 1088, 1),
+                                              (10, 13, 13, 1040, 1088, 1), (10, 13, 500, 528, 576, 1),
+                                              (4, 6, 501, 528, 576, 1), (10, 13, 13, 528, 576, 1),
+                                              (10, 13, 500, 1408, 1472, 2), (4, 6, 500, 1408, 1472, 2),
+                                              (8, 12, 501, 1408, 1472, 2), (10, 13, 13, 1408, 1472, 2),
+                                              (3, 5, 300, 1104, 1152, 2), (10, 13, 200, 2096, 2112, 2),
+                                              (10, 13, 300, 784, 832, 2), (4, 6, 301, 592, 640, 2)])
+def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp, wave):
     """Payloads with a 1088-B (1 KiB class, one group per wave) or 576-B (512-B class, two
     groups per wave) wire pitch: the send that finishes line 0 inside the wave (k_pack_wave64,
     wire_send_wave 1) writes the same datagrams and lengths as the body + k_pack_line0 pair
-    (0), and both equal the oracle's on sampled groups.  Sizes 0 .. sp - 4 (half exactly
+    (0), and both equal the oracle's on sampled groups.  wire_send_wave 2 also runs one wave per
+    group above 1088 B in two passes over the row (1472: 1400-B payloads, up to 2112) and below
+    1088 B with the lanes past the row idle.  Sizes 0 .. sp - 4 (half exactly
     sp - 16), one oversize group, G = 13 / 501 leave the last block partly (or a wave half) dead."""
     rng = np.random.default_rng(n * 7 + k + G + sp)
     m = n - k
@@ -262,8 +269,8 @@ def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp):
     code = qa.Code.vandermonde(k, m)
     full = np.concatenate([np.eye(k, dtype=np.uint8), code.rows])
     res = []
-    for wave in (1, 0):
-        qa.tune("wire_send_wave", wave)
+    for w in (wave, 0):
+        qa.tune("wire_send_wave", w)
         try:
             _, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq), True,
                                                 shard_pitch=sp, wire_pitch=wp)
@@ -284,7 +291,7 @@ def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp):
         if g == 7:
             continue
         out, ln, _ = oracle.pack_group(k, n, full, payload, offs[g * k:(g + 1) * k], sizes[g * k:(g + 1) * k],
-                                       int(seq[g, 0]), int(seq[g, 1]), 1, pitch=wp)
+                                       int(seq[g, 0]), int(seq[g, 1]), 1, shard_cap=max(2052, sp), pitch=wp)
         assert np.array_equal(ln, l1[g])
         for j in range(n):
             assert np.array_equal(out[j, :ln[j]], w1[g, j, :ln[j]]), (g, j)
