@@ -474,14 +474,17 @@ __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K]
 // while the decode record (coefficients only) is still in flight.
 // One wave per 64 16-B columns of a group: a group of `cols` columns gets
 // wpg = ceil(cols / 64) waves (B = 1400 -> 2), all in flight together, no column loop.
-template <int K, int M, int IMPL, int CT>
-__global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
+// IMPL 6: IMPL 3 compiled for 8 waves per SIMD (register caps; 7 otherwise: 106 SGPRs)
+template <int K, int M, int IMPL_, int CT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMPL_ == 6 ? 8 : 1)))
+k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ parity,
                                                           const uint8_t* __restrict__ marks,
                                                           const int32_t* __restrict__ lut,
                                                           const uint32_t* __restrict__ records) {
     // __restrict__ parameters: the LUT and records are provably not written by this
     // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
+    constexpr int IMPL = IMPL_ == 6 ? 3 : IMPL_;
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -706,8 +709,9 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
         int im = a.impl < 0 ? (KK * MM <= 64 ? (KK * MM <= 30 && lanes12 ? 4 : (lanes8 || wide8) ? 3 : 2) : 0) \
                             : a.impl;                                              \
         if (im == 4 && !lanes12_ok) im = 2;                                        \
-        const unsigned pgrid = im == 5 ? grid : im == 3 ? pgrid8 : im == 4 ? pgrid12 : pgrid16; \
-        if (im == 5) QFEC_REC_LAUNCH(KK, MM, 5);                                   \
+        const unsigned pgrid = im == 5 ? grid : (im == 3 || im == 6) ? pgrid8 : im == 4 ? pgrid12 : pgrid16; \
+        if (im == 6) QFEC_REC_LAUNCH(KK, MM, 6);                                   \
+        else if (im == 5) QFEC_REC_LAUNCH(KK, MM, 5);                              \
         else if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                              \
         else if (im == 3) QFEC_REC_LAUNCH(KK, MM, 3);                              \
         else if (im == 2) QFEC_REC_LAUNCH(KK, MM, 2);                              \

@@ -41,13 +41,15 @@ hipError_t launch_percall(const PcArgs& a, hipStream_t s);
 // the next request finds it gone.
 constexpr int kPcMaxChunks = 256;             // 16-B columns per packet row (4 KiB)
 constexpr uint64_t kPcIdleTicks = 100000;     // 1 ms at the 100 MHz wall clock
+constexpr int kPcSrvMaxCoef = 64;             // the server serves k <= 16 and k * e <= 64 (lane c: coefficient c)
+constexpr int kPcTabWords = 8 * kPcSrvMaxCoef; // coefficient c's 5 table dwords at 8 c
 struct PcBell {                               // fine-grained device memory, written by the CPU
     // the request word: number (low 32 bits, 0: none yet) | k << 32 | e << 40 | (chunks - 1) << 48,
     // stored as one 8-byte write, so the block learns the shape with the request (one round trip)
     uint64_t bell;
     uint32_t stop;                            // 1: exit now
     uint32_t pad[13];
-    uint32_t tab[kPcMaxCoef * 5];             // [e][k] perm tables
+    uint32_t tab[kPcTabWords];                // [e][k] perm tables, 8 dwords apart (5 used)
 };
 __host__ __device__ constexpr uint64_t pc_bell(uint32_t req, uint32_t k, uint32_t e, uint32_t chunks) {
     return (uint64_t)req | ((uint64_t)k << 32) | ((uint64_t)e << 40) | ((uint64_t)(chunks - 1) << 48);
@@ -55,9 +57,12 @@ __host__ __device__ constexpr uint64_t pc_bell(uint32_t req, uint32_t k, uint32_
 struct PcStatus {                             // coherent pinned host memory, written by the block
     uint32_t done;                            // the last request served
     uint32_t state;                           // (launch generation << 1) | running
-    uint32_t pad[14];
+    uint32_t pad[6];
+    // QFEC_PERCALL_TRACE=1: wall-clock ticks (100 MHz) of the last request -- seen (twice),
+    // outputs issued, system fence done
+    uint64_t ts[4];
 };
 hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,
-                                 uint32_t gen, hipStream_t s);
+                                 uint32_t gen, uint32_t trace, hipStream_t s);
 
 }  // namespace qfec

@@ -104,16 +104,20 @@ struct DevCtx {
         hipStream_t stream = nullptr;
         PcBell* bell = nullptr;      // fine-grained device memory the CPU stores into
         uint8_t* in = nullptr;       // ditto: kPcMaxCoef rows of kPcMaxChunks * 16 bytes
+        uint8_t* h_in = nullptr;     // the same in write-combined pinned host memory ("percall_in" 1)
+        uint8_t* d_in = nullptr;     //   and its device address
+        int in_mode = 0;             // where the running server reads its inputs: 0 device, 1 host
         uint8_t* h_out = nullptr;    // coherent pinned host memory, same shape
         uint8_t* d_out = nullptr;
         PcStatus* h_st = nullptr;    // coherent pinned host memory
         PcStatus* d_st = nullptr;
         uint32_t req = 0;            // the last request number stored into the bell word
-        uint32_t tab_last[kPcMaxCoef * 5];  // the tables the bell holds (tab_bytes of them)
+        uint32_t tab_last[kPcTabWords];  // the tables the bell holds (tab_bytes of them)
         size_t tab_bytes = 0;
         uint32_t gen = 0;            // the last launch's generation
         bool launched = false;
         unsigned long long calls = 0, launches = 0, relaunches = 0;
+        unsigned long long tr[5] = {0, 0, 0, 0, 0};  // QFEC_PERCALL_TRACE sums: invalidate, loads + compute, fence (ticks), host wait (ns), n
     } srv;
     int init_rc = QFEC_ENODEV;
     // qfec_encode_host: two chunk slots, each with its own stream, event, device buffers
@@ -217,6 +221,7 @@ int ensure_pc(DevCtx& c, size_t bytes) {
 
 // ---- the resident per-call server (qfec_percall.hpp)
 std::atomic<int> g_percall_resident{1};  // qfec_tune "percall_resident"
+std::atomic<int> g_percall_in{0};        // qfec_tune "percall_in": server inputs 0 in device memory, 1 in host memory
 constexpr size_t kPcSrvBytes = (size_t)kPcMaxCoef * kPcMaxChunks * 16;
 
 // true if [p, p + n) lies inside one readable, writable mapping of this process.  Fine-grained
@@ -260,6 +265,10 @@ int pc_server_setup(DevCtx& c) {
         return fail(e, "bell");
     if ((e = hipExtMallocWithFlags((void**)&s.in, kPcSrvBytes, hipDeviceMallocFinegrained)) != hipSuccess)
         return fail(e, "input rows");
+    if ((e = hipHostMalloc((void**)&s.h_in, kPcSrvBytes, hipHostMallocMapped | hipHostMallocWriteCombined)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&s.d_in, s.h_in, 0)) != hipSuccess)
+        return fail(e, "host input rows");
     if ((e = hipHostMalloc((void**)&s.h_out, kPcSrvBytes, hipHostMallocMapped | hipHostMallocCoherent)) !=
             hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0)) != hipSuccess)
@@ -303,12 +312,21 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
                    unsigned char* const* out, int sz, size_t pitch) {
     DevCtx::PcServer& s = c.srv;
     PcBell* b = s.bell;
-    for (int r = 0; r < k; ++r) memcpy(s.in + (size_t)r * pitch, in[r], (size_t)sz);
+    const int mode = g_percall_in.load();
+    if (mode != s.in_mode) {  // the running server reads the other buffer: restart it
+        (void)pc_server_stop(c);
+        s.in_mode = mode;
+    }
+    uint8_t* rows = mode ? s.h_in : s.in;
+    for (int r = 0; r < k; ++r) memcpy(rows + (size_t)r * pitch, in[r], (size_t)sz);
     // the tables go out only when they differ from the last call's (fec_encode of one parity
     // index, or a repeated loss pattern, sends none)
-    const size_t tb = (size_t)k * e * 5 * sizeof(uint32_t);
-    uint32_t t5[kPcMaxCoef * 5];
-    for (int i = 0; i < k * e; ++i) memcpy(&t5[i * 5], &tab[(size_t)i * QFEC_TAB_STRIDE], 5 * sizeof(uint32_t));
+    const size_t tb = (size_t)k * e * 8 * sizeof(uint32_t);
+    uint32_t t5[kPcTabWords];
+    for (int i = 0; i < k * e; ++i) {
+        memcpy(&t5[i * 8], &tab[(size_t)i * QFEC_TAB_STRIDE], 5 * sizeof(uint32_t));
+        t5[i * 8 + 5] = t5[i * 8 + 6] = t5[i * 8 + 7] = 0;
+    }
     if (tb != s.tab_bytes || memcmp(s.tab_last, t5, tb)) {
         memcpy(b->tab, t5, tb);
         memcpy(s.tab_last, t5, tb);
@@ -327,7 +345,8 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
         ++s.gen;
         s.launched = true;
         ++s.launches;
-        return launch_percall_server(b, s.in, s.d_out, s.d_st, prev, s.gen, s.stream);
+        static const uint32_t trace = getenv("QFEC_PERCALL_TRACE") && atoi(getenv("QFEC_PERCALL_TRACE")) ? 1u : 0u;
+        return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, trace, s.stream);
     };
     hipError_t he = hipSuccess;
     if (!pc_server_alive(s)) he = launch();
@@ -335,6 +354,13 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
     for (uint32_t it = 1; he == hipSuccess; ++it) {
         if (__atomic_load_n(&s.h_st->done, __ATOMIC_ACQUIRE) == req) {
             ++s.calls;
+            if (s.h_st->ts[0]) {  // QFEC_PERCALL_TRACE: sum the device stage times (ticks)
+                s.tr[0] += s.h_st->ts[1] - s.h_st->ts[0];
+                s.tr[1] += s.h_st->ts[2] - s.h_st->ts[1];
+                s.tr[2] += s.h_st->ts[3] - s.h_st->ts[2];
+                s.tr[3] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+                ++s.tr[4];
+            }
             for (int j = 0; j < e; ++j) memcpy(out[j], s.h_out + (size_t)j * pitch, (size_t)sz);
             return QFEC_OK;
         }
@@ -358,6 +384,11 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
 
 void pc_server_stop_all() {
     for (DevCtx& c : g_ctx) {
+        if (c.srv.tr[4])  // QFEC_PERCALL_TRACE
+            fprintf(stderr, "[qfec] per-call server, device %d, %llu traced calls: cache invalidate %.2f us, "
+                    "loads + compute -> outputs issued %.2f us, system fence %.2f us, host request -> completion "
+                    "seen %.2f us\n", c.device, c.srv.tr[4], c.srv.tr[0] * 0.01 / c.srv.tr[4],
+                    c.srv.tr[1] * 0.01 / c.srv.tr[4], c.srv.tr[2] * 0.01 / c.srv.tr[4], c.srv.tr[3] * 1e-3 / c.srv.tr[4]);
         if (c.srv.usable <= 0 || !c.srv.launched) continue;
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -813,7 +844,7 @@ int qfec_get_kernel_variant(void) { return g_variant.load(); }
 // experiment knobs, for A/B timing in one process (tools/ab.py); not needed in production
 int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
-    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 5) { tuning().recon_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 6) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "host_chunk") && value >= 0) { tuning().host_chunk = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
@@ -831,6 +862,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
     if (!strcmp(key, "percall_spin") && (value == 0 || value == 1)) { g_percall_spin = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_in") && (value == 0 || value == 1)) { g_percall_in = value; return QFEC_OK; }
     if (!strcmp(key, "percall_resident") && (value == 0 || value == 1)) {
         g_percall_resident = value;
         if (!value)
@@ -2133,7 +2165,8 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (!dev && k * e <= kPcMaxCoef && g_percall_fast.load() && !is_device_ptr(out[0])) {
         // the resident server (packets of up to 4 KiB)
-        if (pitch <= (size_t)kPcMaxChunks * 16 && g_percall_resident.load() && pc_server_setup(*ctx) == QFEC_OK)
+        if (pitch <= (size_t)kPcMaxChunks * 16 && k <= 16 && k * e <= kPcSrvMaxCoef && g_percall_resident.load() &&
+            pc_server_setup(*ctx) == QFEC_OK)
             return pc_server_call(*ctx, tab, k, e, in, out, sz, pitch);
         // host packets: CPU staging into mapped pinned memory, one launch, one synchronise
         if ((rc = ensure_pc(*ctx, (size_t)(k + e) * pitch))) return rc;

@@ -212,15 +212,17 @@ def test_two_ranks_share_gpu_match_single(oracle):
 
 @pytest.mark.parametrize("fast,spin,resident", [(1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 1, 0)])
 @pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 37), (3, 5, 2052), (16, 20, 1400), (3, 5, 4096),
-                                    (3, 5, 8200), (1, 161, 64), (160, 161, 100)])
+                                    (3, 5, 8200), (1, 161, 64), (160, 161, 100), (13, 18, 1028), (17, 19, 200)])
 def test_per_packet_paths_vs_oracle(oracle, fast, spin, resident, k, n, sz):
     """fec_encode / fec_decode on host packets through the resident server (percall_resident 1:
-    rows and tables stored into device memory, a request word polled by one resident block),
+    rows and tables stored into device memory, a request word polled by one resident wave),
     the per-call kernel (percall_fast 1: mapped pinned staging, tables in the kernel arguments,
     one launch; percall_spin 1: the caller waits on the kernel's completion word, 0: on the
     stream) and the staged DMA path (percall_fast 0), against the oracle's fec.c restatement.
     sz 4096 is the server's largest packet; sz 8200 needs a multi-block launch, which is always
-    waited for on the stream; (1, 161) and (160, 161) are the 160-coefficient limit's two ends."""
+    waited for on the stream; (1, 161) and (160, 161) are the 160-coefficient limit's two ends;
+    the server takes k <= 16 and k * e <= 64 ((16, 20) decodes 64 coefficients, (13, 18) 65 and
+    (17, 19) k = 17 go to the one-launch kernel)."""
     rng = np.random.default_rng(k * 100 + sz)
     fp = qa.FecParms(k, n)
     full = fp.matrix
@@ -250,7 +252,9 @@ def test_per_packet_paths_vs_oracle(oracle, fast, spin, resident, k, n, sz):
         after = qa.percall_stats()
         served = after["calls"] - before["calls"]
         if fast and resident and sz <= 4096 and after["usable"] > 0:
-            assert served == (n - k) * 2 + (1 if min(n - k, k) else 0), served  # every encode + the decode
+            lost = min(n - k, k)
+            want = (n - k) * 2 * (k <= 16) + (1 if lost and k <= 16 and k * lost <= 64 else 0)
+            assert served == want, served  # every encode (checker + decode input) + the decode
         else:
             assert served == 0
     finally:
