@@ -66,134 +66,154 @@ __device__ __forceinline__ void st_rel_sys(uint32_t* p, uint32_t v) {
 }
 
 // ---- the resident server (qfec_percall.hpp)
-// Serves calls with k <= 16 and k * e <= 64 (kPcSrvMaxCoef; others take k_percall): lane c holds
-// coefficient c's perm table (5 dwords; v_readlane with the wave-uniform coefficient index
-// gives it to the MAC as scalars, no LDS round trip per coefficient), and every input byte the
-// call needs is in registers before the first multiply.  The inputs and tables are read past the
-// caches (system-scope loads), so no cache invalidation is needed; they live in fine-grained
-// memory whose reads each go to memory, so only what the call needs is read -- KB >= k rows
-// (KB - k < 6 rows re-read row k - 1), only lanes inside the packet -- and all of it is issued
-// before any of it is used (one enclosing branch per group of loads: a branch per load makes the
+// Serves calls with k <= 16 and k * e <= 64 (kPcSrvMaxCoef; others take k_percall).  One block of
+// four waves, lane = one 8-byte column of the packets (a 1 028-B packet is 129 columns): the
+// multiply is VALU work that one wave would do alone (measured: 3.8 us of a call with 16-B lanes
+// in one wave, the 65th column costing a whole second pass), so it is spread over the four SIMDs.
+// Lane c of every wave holds coefficient c's perm table (5 dwords; v_readlane with the
+// wave-uniform coefficient index gives it to the MAC as scalars, no LDS round trip per
+// coefficient).  Every input byte the call needs is in registers before the first multiply: KB >=
+// k rows (KB - k < 6 rows re-read row k - 1), only lanes inside the packet, all loads issued
+// before any is used (one enclosing branch per group of loads: a branch per load makes the
 // compiler wait for each load before it issues the next).
 template <int NQ, int KB>
-__device__ __forceinline__ void pc_wave_serve(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
-                                              uint32_t e, uint32_t chunks, uint32_t col0, uint32_t lane) {
-    const uint32_t pitch = chunks * 16u;
-    uint4 x[NQ][KB];
+__device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
+                                               uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t,
+                                               uint64_t& ts_loaded) {
+    const uint32_t lane = t & 63u;
+    uint2 x[NQ][KB];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
-        const uint32_t col = col0 + lane + 64u * q;
+        const uint32_t col = t + 256u * q;
 #pragma unroll
-        for (int i = 0; i < KB; ++i) x[q][i] = make_uint4(0, 0, 0, 0);
-        if (col < chunks) {
+        for (int i = 0; i < KB; ++i) x[q][i] = make_uint2(0, 0);
+        if (col < cols) {
 #pragma unroll
-            for (int i = 0; i < KB; ++i) x[q][i] = ld_sys16(in + (uint64_t)min((uint32_t)i, k - 1) * pitch + (uint64_t)col * 16u);
+            for (int i = 0; i < KB; ++i)
+                x[q][i] = *reinterpret_cast<const uint2*>(in + (uint64_t)min((uint32_t)i, k - 1) * pitch + (uint64_t)col * 8u);
         }
     }
-    uint4 ta = make_uint4(0, 0, 0, 0), tb = make_uint4(0, 0, 0, 0);  // coefficient `lane`: dwords 0-3, 4
+    uint4 ta = make_uint4(0, 0, 0, 0);  // coefficient `lane`: table dwords 0-3, then 4
+    uint32_t tb = 0;
     if (lane < k * e) {
-        ta = ld_sys16(bell->tab + 8u * lane);
-        tb = ld_sys16(bell->tab + 8u * lane + 4u);
+        ta = *reinterpret_cast<const uint4*>(bell->tab + 8u * lane);
+        tb = bell->tab[8u * lane + 4u];
     }
+    if (ts_loaded) {  // QFEC_PERCALL_TRACE: when every load has landed
+        __builtin_amdgcn_s_waitcnt(0);
+        ts_loaded = wall_clock64();
+    }
+    if ((t & ~63u) >= cols) return;  // a wave with no column (wave-uniform)
     for (uint32_t j0 = 0; j0 < e; j0 += 4) {
         const uint32_t ej = min(4u, e - j0);
-        uint4 acc[NQ][4];
+        uint2 acc[NQ][4];
 #pragma unroll
         for (int q = 0; q < NQ; ++q)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[q][j] = make_uint4(0, 0, 0, 0);
+            for (int j = 0; j < 4; ++j) acc[q][j] = make_uint2(0, 0);
 #pragma unroll
         for (int i = 0; i < KB; ++i) {
             if ((uint32_t)i >= k) continue;
-            Sel sl[NQ][4];
+            Sel sl[NQ][2];
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) sel16(sl[q], x[q][i]);
+            for (int q = 0; q < NQ; ++q) {
+                sl[q][0] = gf_sel(x[q][i].x);
+                sl[q][1] = gf_sel(x[q][i].y);
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if ((uint32_t)j >= ej) continue;
                 const int c = (int)((j0 + j) * k + i);  // wave-uniform
-                const uint32_t t[5] = {(uint32_t)__builtin_amdgcn_readlane((int)ta.x, c),
-                                       (uint32_t)__builtin_amdgcn_readlane((int)ta.y, c),
-                                       (uint32_t)__builtin_amdgcn_readlane((int)ta.z, c),
-                                       (uint32_t)__builtin_amdgcn_readlane((int)ta.w, c),
-                                       (uint32_t)__builtin_amdgcn_readlane((int)tb.x, c)};
+                const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)ta.x, c),
+                               t1 = (uint32_t)__builtin_amdgcn_readlane((int)ta.y, c),
+                               t2 = (uint32_t)__builtin_amdgcn_readlane((int)ta.z, c),
+                               t3 = (uint32_t)__builtin_amdgcn_readlane((int)ta.w, c),
+                               t4 = (uint32_t)__builtin_amdgcn_readlane((int)tb, c);
 #pragma unroll
-                for (int q = 0; q < NQ; ++q) gf_mac16(acc[q][j], sl[q], t);
+                for (int q = 0; q < NQ; ++q) {
+                    acc[q][j].x = xor3(acc[q][j].x, pp0(sl[q][0], t0, t1), pp1(sl[q][0], t2, t3)) ^ pp2(sl[q][0], t4);
+                    acc[q][j].y = xor3(acc[q][j].y, pp0(sl[q][1], t0, t1), pp1(sl[q][1], t2, t3)) ^ pp2(sl[q][1], t4);
+                }
             }
         }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            const uint32_t col = col0 + lane + 64u * q;
-            if (col < chunks) {
+            const uint32_t col = t + 256u * q;
+            if (col < cols) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     if ((uint32_t)j < ej)
-                        *reinterpret_cast<uint4*>(out + (uint64_t)(j0 + j) * pitch + (uint64_t)col * 16u) = acc[q][j];
+                        *reinterpret_cast<uint2*>(out + (uint64_t)(j0 + j) * pitch + (uint64_t)col * 8u) = acc[q][j];
             }
         }
     }
 }
 
 template <int NQ>
-__device__ __forceinline__ void pc_wave_serve_k(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
-                                                uint32_t e, uint32_t chunks, uint32_t col0, uint32_t lane) {
-    if (k <= 4) pc_wave_serve<NQ, 4>(bell, in, out, k, e, chunks, col0, lane);
-    else if (k <= 10) pc_wave_serve<NQ, 10>(bell, in, out, k, e, chunks, col0, lane);
-    else pc_wave_serve<NQ, 16>(bell, in, out, k, e, chunks, col0, lane);
+__device__ __forceinline__ void pc_block_serve_k(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
+                                                 uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t, uint64_t& ts) {
+    if (k <= 4) pc_block_serve<NQ, 4>(bell, in, out, k, e, cols, pitch, t, ts);
+    else if (k <= 10) pc_block_serve<NQ, 10>(bell, in, out, k, e, cols, pitch, t, ts);
+    else pc_block_serve<NQ, 16>(bell, in, out, k, e, cols, pitch, t, ts);
 }
 
-// One wave, lane = 16-B columns lane, lane + 64, ... of the packets.  The wave polls the 8-byte
-// request word (system-scope loads that bypass the caches), which carries the call's shape.
-// One wave, not a block of four: one system fence per call and no workgroup barriers.  Every
-// iteration ends in the same place for every lane, and the loop exits on idle or stop, so the
-// grid always drains.
-__global__ void __launch_bounds__(64) k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st,
-                                                       uint32_t served, uint32_t gen, uint32_t trace) {
-    const uint32_t lane = threadIdx.x;
-    if (lane == 0) st_rel_sys(&st->state, (gen << 1) | 1u);
+// Lane 0 polls the 8-byte request word (system-scope loads that bypass the caches), which carries
+// the call's shape, and after it a system-scope acquire fence invalidates the caches, so the block
+// then reads what the CPU wrote before the word.  Every iteration ends in the same place for
+// every lane, and the loop exits on idle or stop, so the grid always drains.
+__global__ void __launch_bounds__(256) k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st,
+                                                        uint32_t served, uint32_t gen, uint32_t trace) {
+    __shared__ uint64_t s_bell;
+    __shared__ uint32_t s_quit;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) st_rel_sys(&st->state, (gen << 1) | 1u);
     uint64_t t0 = wall_clock64();
     for (;;) {
-        uint64_t b = 0;
-        bool quit = false;
-        for (uint32_t it = 1;; ++it) {  // one load per poll; `stop` and the idle clock every 16th
-            const uint64_t v = ld_sys64(&bell->bell);  // every lane loads the same word: make it uniform
-            b = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
-            if ((uint32_t)b != served) break;
-            if ((it & 15u) == 0 && (ld_sys(&bell->stop) || wall_clock64() - t0 > kPcIdleTicks)) {
-                quit = true;
-                break;
+        if (t == 0) {
+            uint64_t b = 0;
+            uint32_t quit = 0;
+            for (uint32_t it = 1;; ++it) {  // one load per poll; `stop` and the idle clock every 16th
+                b = ld_sys64(&bell->bell);
+                if ((uint32_t)b != served) break;
+                if ((it & 15u) == 0 && (ld_sys(&bell->stop) || wall_clock64() - t0 > kPcIdleTicks)) {
+                    quit = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
-            __builtin_amdgcn_s_sleep(1);
+            if (!quit) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+            s_bell = b;
+            s_quit = quit;
         }
-        if (quit) break;
+        __syncthreads();
+        if (s_quit) break;
         const uint64_t ts0 = trace ? wall_clock64() : 0;
+        const uint64_t b = s_bell;
         const uint32_t r = (uint32_t)b, k = (uint32_t)(b >> 32) & 0xFFu, e = (uint32_t)(b >> 40) & 0xFFu,
-                       chunks = (uint32_t)(b >> 48) + 1u;
-        if (chunks <= 64) {
-            pc_wave_serve_k<1>(bell, in, out, k, e, chunks, 0, lane);
-        } else {  // 128 columns at a time (2 KiB packets in one round trip)
-            for (uint32_t c0 = 0; c0 < chunks; c0 += 128) pc_wave_serve_k<2>(bell, in, out, k, e, chunks, c0, lane);
-        }
+                       chunks = (uint32_t)(b >> 48) + 1u, pitch = chunks * 16u, cols = chunks * 2u;
+        uint64_t ts1 = trace;
+        if (cols <= 256) pc_block_serve_k<1>(bell, in, out, k, e, cols, pitch, t, ts1);
+        else pc_block_serve_k<2>(bell, in, out, k, e, cols, pitch, t, ts1);
         const uint64_t ts2 = trace ? wall_clock64() : 0;
         __threadfence_system();  // every lane's outputs reach the host before the completion word
-        if (trace && lane == 0) {
+        __syncthreads();         // (and s_bell is not rewritten before every lane has read it)
+        if (trace && t == 0) {
             st->ts[0] = ts0;
-            st->ts[1] = ts0;
+            st->ts[1] = ts1;
             st->ts[2] = ts2;
             st->ts[3] = wall_clock64();
             __threadfence_system();
         }
-        if (lane == 0) st_rel_sys(&st->done, r);
+        if (t == 0) st_rel_sys(&st->done, r);
         served = r;
         t0 = wall_clock64();
     }
-    if (lane == 0) st_rel_sys(&st->state, gen << 1);  // this generation has exited
+    if (t == 0) st_rel_sys(&st->state, gen << 1);  // this generation has exited
 }
 
 hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,
                                  uint32_t gen, uint32_t trace, hipStream_t s) {
-    hipLaunchKernelGGL(k_percall_server, dim3(1), dim3(64), 0, s, bell, in, out, st, served, gen, trace);
+    hipLaunchKernelGGL(k_percall_server, dim3(1), dim3(256), 0, s, bell, in, out, st, served, gen, trace);
     return hipGetLastError();
 }
 

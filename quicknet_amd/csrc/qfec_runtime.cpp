@@ -385,8 +385,8 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
 void pc_server_stop_all() {
     for (DevCtx& c : g_ctx) {
         if (c.srv.tr[4])  // QFEC_PERCALL_TRACE
-            fprintf(stderr, "[qfec] per-call server, device %d, %llu traced calls: cache invalidate %.2f us, "
-                    "loads + compute -> outputs issued %.2f us, system fence %.2f us, host request -> completion "
+            fprintf(stderr, "[qfec] per-call server, device %d, %llu traced calls: seen -> inputs and tables in %.2f us, "
+                    "compute -> outputs issued %.2f us, system fence %.2f us, host request -> completion "
                     "seen %.2f us\n", c.device, c.srv.tr[4], c.srv.tr[0] * 0.01 / c.srv.tr[4],
                     c.srv.tr[1] * 0.01 / c.srv.tr[4], c.srv.tr[2] * 0.01 / c.srv.tr[4], c.srv.tr[3] * 1e-3 / c.srv.tr[4]);
         if (c.srv.usable <= 0 || !c.srv.launched) continue;
