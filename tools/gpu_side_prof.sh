@@ -12,7 +12,7 @@ echo "== side legs"
 timeout -k 10 200 python tools/side_legs.py --steps 100 > $OUT/side.json 2> $OUT/side.err || { tail -20 $OUT/side.err; exit 2; }
 tail -c 3000 $OUT/side.json
 echo "== rocprof kernel trace"
-(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof -o run -- python3 $R/tools/side_legs.py --steps 100 > $R/$OUT/side_prof.json 2> $R/$OUT/side_prof.err) || { tail -20 $OUT/side_prof.err; exit 3; }
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o run -- python3 $R/tools/side_legs.py --steps 100 > $R/$OUT/side_prof.json 2> $R/$OUT/side_prof.err) || { tail -20 $OUT/side_prof.err; exit 3; }
 find $OUT/prof -name "*kernel_stats.csv" | head -3
 f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); head -12 "$f" | cut -c1-200
 echo "== PMC"
