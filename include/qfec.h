@@ -243,9 +243,11 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "wire_line"        1 the fused send writes whole 64-B lines when the wire pitch is the 64-B
  *                      multiple above 13 + shard pitch (body + k_pack_line0) | 0 body + k_pack_head
  *   "wire_send_wave"   1 at a 1088-B (576-B) wire pitch one wave holds one (two) groups and writes
- *                      their rows' first lines itself (k_pack_wave64) | 2 also one wave per group at
- *                      592..1072 B, and in two passes at 1104..2112 B (e.g. 1472 for 1400-B payloads;
- *                      A/B: slower there) | 0 body + k_pack_line0
+ *                      their rows' first lines itself (k_pack_wave64); at 1104..1600 B (e.g. 1472 for
+ *                      1400-B payloads) the same on 8-byte lanes in three passes | 2 also one wave per
+ *                      group at 592..1072 B, and on 16-B lanes in two passes at 1104..2112 B (A/B:
+ *                      slower) | 3 8-B lanes at 592..1600 B | 4 (A/B) 8-B lanes at 5 waves/SIMD above
+ *                      1088 B | 0 body + k_pack_line0
  *   "wire_rx_tail"     1 (k_unpack_fused) tail dwords ride on the last 16-B pass | 0 their own pass
  *   "frame_rows"       2 framing kernels run two rows per wave, loads first, frames built in LDS and
  *                      stored flat (rows <= 2 KiB) | 3 the same, stored directly | 1 | 4

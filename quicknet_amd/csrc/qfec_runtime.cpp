@@ -849,7 +849,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
     if (!strcmp(key, "wire_chunk") && value >= 0) { tuning().wire_chunk = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_send_wave") && value >= 0 && value <= 2) { tuning().wire_send_wave = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_send_wave") && value >= 0 && value <= 4) { tuning().wire_send_wave = value; return QFEC_OK; }
     if (!strcmp(key, "wire_line") && (value == 0 || value == 1)) { tuning().wire_line = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_tail") && (value == 0 || value == 1)) { tuning().wire_rx_tail = value; return QFEC_OK; }
     if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }

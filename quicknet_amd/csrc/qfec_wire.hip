@@ -380,6 +380,47 @@ __device__ __forceinline__ void encode_cols(const uint4 (&x)[K], uint4 (&acc)[M]
     }
 }
 
+// the same over 8-byte columns (k_pack_wave64 with 8-B lanes)
+template <int K, int M>
+__device__ __forceinline__ void encode_cols8(const uint2 (&x)[K], uint2 (&acc)[M], const uint32_t* __restrict__ tab) {
+#pragma unroll
+    for (int r = 0; r < M; ++r) acc[r] = make_uint2(0, 0);
+#pragma unroll
+    for (int c = 0; c + 1 < K; c += 2) {
+        const Sel a0 = gf_sel(x[c].x), a1 = gf_sel(x[c].y), b0 = gf_sel(x[c + 1].x), b1 = gf_sel(x[c + 1].y);
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            const uint32_t* ta = tab + (r * K + c) * QFEC_TAB_STRIDE;
+            const uint32_t* tb = tab + (r * K + c + 1) * QFEC_TAB_STRIDE;
+            acc[r].x = mac2(acc[r].x, a0, b0, ta, tb);
+            acc[r].y = mac2(acc[r].y, a1, b1, ta, tb);
+        }
+    }
+    if (K & 1) {
+        const Sel a0 = gf_sel(x[K - 1].x), a1 = gf_sel(x[K - 1].y);
+#pragma unroll
+        for (int r = 0; r < M; ++r) {
+            const uint32_t* t = tab + (r * K + K - 1) * QFEC_TAB_STRIDE;
+            acc[r].x ^= gf_mul4(a0, t[0], t[1], t[2], t[3], t[4]);
+            acc[r].y ^= gf_mul4(a1, t[0], t[1], t[2], t[3], t[4]);
+        }
+    }
+}
+
+__device__ __forceinline__ uint2 ldu8(const uint8_t* p) {
+    uint2 v;
+    __builtin_memcpy(&v, p, 8);
+    return v;
+}
+__device__ __forceinline__ uint2 mask8(uint2 v, int lo, int hi) {
+    v.x &= byte_mask(lo, hi, 0);
+    v.y &= byte_mask(lo, hi, 1);
+    return v;
+}
+__device__ __forceinline__ uint32_t sum8(const uint2& v, uint32_t acc) {
+    return __builtin_amdgcn_sad_u8(v.y, 0u, __builtin_amdgcn_sad_u8(v.x, 0u, acc));
+}
+
 // sum over each aligned 16-lane row, result in every lane of the row (DPP, no LDS)
 __device__ __forceinline__ uint32_t row16_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
@@ -761,8 +802,11 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
 // 1472-B pitch of 1400-B (MTU-size) payloads: pass 0 chunks 4..67, pass 1 chunks 68.. on the
 // first wire_pitch / 16 - 68 lanes.  Row sums accumulate over the passes, so line 0 is
 // unchanged.
-template <int K, int M, int GPW, int FP = 0, int NP = 1>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? FRAME_WAVES : 4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
+//
+// LW 8 (tuning "wire_send_wave" 3): 8-byte lanes, NP passes over the 8-B chunks 8 .. wire_pitch
+// / 8 - 1 (1088: two full passes; 1472: 64 + 64 + 48 lanes), fewer registers per pass.
+template <int K, int M, int GPW, int FP = 0, int NP = 1, int LW = 16, int WV = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WV ? WV : LW == 8 ? (NP >= 3 ? 4 : 6) : FP ? FRAME_WAVES : 4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
                                                      const int64_t* __restrict__ offsets,
                                                      const int32_t* __restrict__ sizes,
                                                      const uint32_t* __restrict__ seq,
@@ -772,6 +816,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? F
     constexpr int FD = FP / 4;                                      // prefix dwords of line 0
     static_assert(FP == 0 || FP == 4 || FP == 12, "frame prefix");
     static_assert(NP == 1 || GPW == 1, "passes");
+    static_assert(LW == 16 || (LW == 8 && GPW == 1), "lane width");
     const int lane = threadIdx.x & 63;
     const int ln = GPW == 1 ? lane : lane % LPG;  // lane within its group: chunk 4 + ln (+ 64 per pass)
     const uint64_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));  // wave-uniform
@@ -816,6 +861,55 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? F
     uint32_t ps[N];  // per-lane byte sums of each row's chunks (payload / check bytes)
 #pragma unroll
     for (int r = 0; r < N; ++r) ps[r] = 0;
+    if constexpr (LW == 8) {
+        const int tend8 = (int)(a.wire_pitch / 8);
+#pragma unroll
+        for (int pp = 0; pp < NP; ++pp) {
+            const int t = 8 + ln + 64 * pp;
+            const bool act = ok && t < tend8;
+            const int p = 8 * t - FP - HDR - HEAD;  // payload offset of this chunk's first byte (>= 35)
+            uint2 x[K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) x[i] = make_uint2(0, 0);
+            if (act) {
+#pragma unroll
+                for (int i = 0; i < K; ++i) x[i] = ldu8(payload + off[i] + min(p, size[i]));
+#pragma unroll
+                for (int i = 0; i < K; ++i) x[i] = mask8(x[i], 0, size[i] - p);
+            }
+#pragma unroll
+            for (int i = 0; i < K; ++i) ps[i] = sum8(x[i], ps[i]);
+            uint2 acc[M];
+            encode_cols8<K, M>(x, acc, tab);
+#pragma unroll
+            for (int r = 0; r < M; ++r) asm volatile("" : "+v"(acc[r].x), "+v"(acc[r].y));
+            uint8_t* out = out_g + 8 * t;
+#pragma unroll
+            for (int r = 0; r < N; ++r) {
+                uint2 v = r < K ? x[r] : acc[r - K];
+                if (r >= K) ps[r] = sum8(v, ps[r]);
+                if constexpr (FP != 0) {  // XOR the frame's bytes only: padding past it stays 0
+                    const int total = FP + HDR + (r < K ? size[r] + HEAD : gmax);
+                    uint64_t klo, khi;
+                    int rel = total - 8 * t;
+                    asm volatile("" : "+v"(rel));
+                    keep_words(rel, klo, khi);
+                    const uint32_t mr = mm_of(r);
+                    const uint64_t xl = (((uint64_t)mr << 32) | mr) & klo;
+                    v = make_uint2(v.x ^ (uint32_t)xl, v.y ^ (uint32_t)(xl >> 32));
+                }
+                if (act) {
+                    uint2* dst = reinterpret_cast<uint2*>(out + (uint64_t)r * a.wire_pitch);
+                    if (a.store_nt & 1) {
+                        const u32x2 w2 = {v.x, v.y};
+                        __builtin_nontemporal_store(w2, reinterpret_cast<u32x2*>(dst));
+                    } else {
+                        *dst = v;
+                    }
+                }
+            }
+        }
+    } else {
 #pragma unroll
     for (int pp = 0; pp < NP; ++pp) {
         const int t = 4 + ln + 64 * pp;
@@ -854,6 +948,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FP ? F
             }
             if (act) stw(out + (uint64_t)r * a.wire_pitch, v, a.store_nt & 1);
         }
+    }
     }
     // ---- line 0
     // line 0's payload dwords (lanes ln 0..15: frame bytes 4 ln .. 4 ln + 3 = datagram dword
@@ -2151,6 +2246,12 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s) {
 static int send_wave_gpw(uint64_t wire_pitch) {
     const int sw = tuning().wire_send_wave;
     if (!sw) return 0;
+    if (sw == 4 && wire_pitch > 1088 && wire_pitch <= 1600) return 11;  // A/B: 8-B lanes at 5 waves/SIMD
+    if (sw == 3 && wire_pitch > 576 && wire_pitch <= 1600)  // 8-B lanes: 2 passes to 1088 B, 3 to 1600
+        return wire_pitch <= 1088 ? 9 : 10;
+    // the default above 1088 B: 8-B lanes in three passes (1472 B, RS(10,13) x 100k: 737 against
+    // 781 us for the body + line-0 pair; at 1088 B the 16-B lanes stay: 497 against 545 us)
+    if (wire_pitch > 1088 && wire_pitch <= 1600) return 10;
     if (wire_pitch == 576) return 2;
     if (wire_pitch == 1088 || (sw == 2 && wire_pitch > 576 && wire_pitch < 1088)) return 1;
     if (sw == 2 && wire_pitch > 1088 && wire_pitch <= 2112) return 5;
@@ -2177,13 +2278,22 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
             WireArgs b = a;
             b.wire = a.wire + g0 * (uint64_t)(K + M) * a.wire_pitch;
             b.wire_len = a.wire_len + g0 * (K + M);
-            const dim3 grid((unsigned)((gn + 4 * (gpw & 3) - 1) / (4 * (gpw & 3))));
+            const dim3 grid((unsigned)((gn + 4 * (gpw == 2 ? 2 : 1) - 1) / (4 * (gpw == 2 ? 2 : 1))));
             if (gpw == 1)
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 1>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
                                    a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
             else if (gpw == 5)
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
                                    a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
+            else if (gpw == 9)
+                hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 2, 8>), grid, dim3(256), 0, s, b, a.payload,
+                                   a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
+            else if (gpw == 10)
+                hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 3, 8>), grid, dim3(256), 0, s, b, a.payload,
+                                   a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
+            else if (gpw == 11)
+                hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 3, 8, 5>), grid, dim3(256), 0, s, b, a.payload,
+                                   a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
             else
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
                                    a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
@@ -2266,17 +2376,26 @@ hipError_t pack_frames_shape(const WireArgs& a, const FrameSend& fs, int fp, con
         FrameSend f = fs;
         f.mask = fs.mask + g0 * (K + M);
         if (fs.conv_hid) f.conv_hid = fs.conv_hid + 2 * g0 * (K + M);
-        const dim3 grid((unsigned)((gn + 4 * (gpw & 3) - 1) / (4 * (gpw & 3))));
+        const dim3 grid((unsigned)((gn + 4 * (gpw == 2 ? 2 : 1) - 1) / (4 * (gpw == 2 ? 2 : 1))));
 #define QFEC_PF(GPW, FP, NP)                                                                                          \
     hipLaunchKernelGGL((k_pack_wave64<K, M, GPW, FP, NP>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K, \
                        a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, f)
-        if (gpw == 1 && fp == 4) QFEC_PF(1, 4, 1);
+#define QFEC_PF8(FP, NP)                                                                                          \
+    hipLaunchKernelGGL((k_pack_wave64<K, M, 1, FP, NP, 8>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K, \
+                       a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, f)
+        if (gpw == 11) gpw = 10;  // (the 5-wave A/B build is for datagrams only)
+        if (gpw == 9 && fp == 4) QFEC_PF8(4, 2);
+        else if (gpw == 9) QFEC_PF8(12, 2);
+        else if (gpw == 10 && fp == 4) QFEC_PF8(4, 3);
+        else if (gpw == 10) QFEC_PF8(12, 3);
+        else if (gpw == 1 && fp == 4) QFEC_PF(1, 4, 1);
         else if (gpw == 1) QFEC_PF(1, 12, 1);
         else if (gpw == 5 && fp == 4) QFEC_PF(1, 4, 2);
         else if (gpw == 5) QFEC_PF(1, 12, 2);
         else if (fp == 4) QFEC_PF(2, 4, 1);
         else QFEC_PF(2, 12, 1);
 #undef QFEC_PF
+#undef QFEC_PF8
     }
     return hipGetLastError();
 }

@@ -248,14 +248,20 @@ def test_unpack_row_tails(k, n, checksum, pitch):
                                               (10, 13, 500, 1408, 1472, 2), (4, 6, 500, 1408, 1472, 2),
                                               (8, 12, 501, 1408, 1472, 2), (10, 13, 13, 1408, 1472, 2),
                                               (3, 5, 300, 1104, 1152, 2), (10, 13, 200, 2096, 2112, 2),
-                                              (10, 13, 300, 784, 832, 2), (4, 6, 301, 592, 640, 2)])
+                                              (10, 13, 300, 784, 832, 2), (4, 6, 301, 592, 640, 2),
+                                              (10, 13, 500, 1040, 1088, 3), (4, 6, 501, 1040, 1088, 3),
+                                              (10, 13, 13, 1040, 1088, 3), (10, 13, 500, 1408, 1472, 3),
+                                              (8, 12, 501, 1408, 1472, 3), (3, 5, 300, 1536, 1600, 3),
+                                              (10, 13, 300, 784, 832, 3), (10, 13, 500, 1408, 1472, 1),
+                                              (4, 6, 77, 1408, 1472, 4)])
 def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp, wave):
     """Payloads with a 1088-B (1 KiB class, one group per wave) or 576-B (512-B class, two
     groups per wave) wire pitch: the send that finishes line 0 inside the wave (k_pack_wave64,
     wire_send_wave 1) writes the same datagrams and lengths as the body + k_pack_line0 pair
     (0), and both equal the oracle's on sampled groups.  wire_send_wave 2 also runs one wave per
     group above 1088 B in two passes over the row (1472: 1400-B payloads, up to 2112) and below
-    1088 B with the lanes past the row idle.  Sizes 0 .. sp - 4 (half exactly
+    1088 B with the lanes past the row idle; 3 runs it on 8-byte lanes (two passes at 1088 B,
+    three at 1472 and 1600), which 1 (the default) does above 1088 B; 4 is that body at 5 waves/SIMD.  Sizes 0 .. sp - 4 (half exactly
     sp - 16), one oversize group, G = 13 / 501 leave the last block partly (or a wave half) dead."""
     rng = np.random.default_rng(n * 7 + k + G + sp)
     m = n - k

@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--session", action="store_true")
     ap.add_argument("--payload", type=int, default=1024)
+    ap.add_argument("--tune", default="", help="qfec_tune settings, e.g. wire_send_wave=3")
     a = ap.parse_args()
+    for kv in filter(None, a.tune.split(",")):
+        kk, vv = kv.split("=")
+        qa.tune(kk, int(vv))
     k, n, S, G = 10, 13, a.payload, a.groups
     m = n - k
     P = 12 if a.session else 4
