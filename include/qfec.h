@@ -256,9 +256,12 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged
  *   "percall_spin"     1 a per-call launch of one block is waited for by spinning on the completion
  *                      word the kernel stores in coherent pinned memory | 0 hipStreamSynchronize
- *   "percall_resident" 1 fec_encode / fec_decode of packets up to 4 KiB go to a resident one-block
- *                      server that polls a request word in device memory and exits by itself after
- *                      1 ms without a request | 0 one launch per call (setting 0 stops the servers) */
+ *   "percall_resident" 1 fec_encode / fec_decode of packets up to 4 KiB with k <= 16 and k * e <= 64
+ *                      go to a resident one-block server that polls a request word in device memory
+ *                      and exits by itself after 1 ms without a request | 0 one launch per call
+ *                      (setting 0 stops the servers)
+ *   "percall_in"       0 the server's input rows in device memory | 1 in write-combined pinned host
+ *                      memory (A/B: 0.9 us slower per call) */
 int qfec_tune(const char *key, int value);
 
 /* The resident per-call server of the current device (qfec_tune "percall_resident"): out[0] calls

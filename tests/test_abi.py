@@ -172,3 +172,22 @@ def test_net_layer_fec_off_host_side():
     assert rx.unpack_input(r, b"\xed" * 5) == 1   # an FEC tag but under 11 bytes: plain too
     assert rx.flush_unpack() == [(r, b"abc", 0), (r, b"\xed" * 4, 0)]
     assert rx.stats()["delivered"] == 2
+
+
+def test_tune_keys_documented_and_accepted():
+    """Every qfec_tune key that include/qfec.h documents is accepted with its documented first
+    value (host state only: no device is touched), and an unknown key or value is refused."""
+    text = open(os.path.join(ROOT, "include", "qfec.h")).read()
+    block = text[text.index("int qfec_tune(") - 6000:text.index("int qfec_tune(")]
+    keys = re.findall(r'^ \*   "(\w+)"\s+(-?\d+)?', block, re.M)
+    assert len(keys) >= 20, keys
+    L = lib()
+    for key, first in keys:
+        value = int(first) if first else 0
+        assert L.qfec_tune(key.encode(), value) == 0, (key, value)
+    assert L.qfec_tune(b"no_such_knob", 1) != 0
+    assert L.qfec_tune(b"percall_in", 7) != 0
+    assert L.qfec_tune(b"recon_impl", 99) != 0
+    # back to the defaults the rest of this process expects
+    for key, value in (("recon_impl", -1), ("wire_store_nt", 3), ("percall_resident", 1), ("percall_in", 0)):
+        assert L.qfec_tune(key.encode(), value) == 0
