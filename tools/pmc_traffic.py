@@ -23,8 +23,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"encode": "k_encode_perm<{k}, {m}>", "reconstruct": "k_reconstruct_perm<{k}, {m},", "probe": "k_probe_xor"}
 # --workload wire: bench.py's `wire` leg (tools/side_legs.py), RS(10,13) 1 KiB payloads
-WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0, 1>", "unpack": "k_unpack_v2<10, 3, 4, true, 0>",
-                "pack_frames": "k_pack_wave64<10, 3, 1, 4, 1>", "unpack_frames": "k_unpack_v2<10, 3, 4, true, 4>"}
+WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0, 1, 16, 0>", "unpack": "k_unpack_v2<10, 3, 4, true, 0>",
+                "pack_frames": "k_pack_wave64<10, 3, 1, 4, 1, 16, 0>", "unpack_frames": "k_unpack_v2<10, 3, 4, true, 4>"}
 
 
 def run_pass(counter, out, bench_args, k, m, kernels=KERNELS, script="bench.py"):
