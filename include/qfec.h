@@ -237,7 +237,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "host_chunk"       groups per staged host chunk (0: ~32 MiB)
  *   "wire_fused"       1 fused datagram send where a (k, m) instance exists | 0 staged build -> encode -> emit
  *   "wire_fused_rx"    1 fused datagram receive | 0 staged parse -> reconstruct -> check
- *   "wire_rx_split"    1 k_unpack_v2, lanes by pitch | 2 16-B | 3 8-B | 0 the round-1 k_unpack_fused
+ *   "wire_rx_split"    1 k_unpack_v2, lanes by pitch | 2 16-B | 3 8-B | 4 16-B with a remainder of up
+ *                      to 512 B riding on the last pass (2 tail dwords) | 0 the round-1 k_unpack_fused
  *   "wire_store_nt"    0-3 non-temporal datagram stores (bit 0 body, bit 1 head)
  *   "wire_chunk"       groups per fused send launch pair (0: as many as fit)
  *   "wire_line"        1 the fused send writes whole 64-B lines when the wire pitch is the 64-B

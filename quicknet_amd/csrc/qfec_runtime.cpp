@@ -859,7 +859,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "recon_full_lines") && value >= 0 && value <= 2) { tuning().recon_full_lines = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_lds") && value >= 0 && value <= 2) { tuning().wire_rx_lds = value; return QFEC_OK; }
     if (!strcmp(key, "frame_rows") && value >= 1 && value <= 4) { tuning().frame_rows = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 3) { tuning().wire_rx_split = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 4) { tuning().wire_rx_split = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
     if (!strcmp(key, "percall_spin") && (value == 0 || value == 1)) { g_percall_spin = value; return QFEC_OK; }
     if (!strcmp(key, "percall_in") && (value == 0 || value == 1)) { g_percall_in = value; return QFEC_OK; }

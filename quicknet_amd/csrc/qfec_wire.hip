@@ -1625,7 +1625,10 @@ extern __shared__ uint4 rx_stage[];
 // the datagram checksum does not), and rows whose FEC header is rejected get their checksum
 // from a last per-row pass, so fr.status is RecvPacket's verdict for every row: 0 ok, 1 short,
 // 2 checksum, 3 cmd, 4 too long (as qfec_unframe_udp).
-template <int K, int M, int NVA, bool LDSW = false, int FP = 0>
+// TT: tail dwords per lane a row's remainder after the full passes may ride on the last one
+// (1: up to 256 bytes; 2, tuning "wire_rx_split" 4: up to 512, e.g. 1 408 = 1 024 + 384 in one pass
+// on 16-B lanes)
+template <int K, int M, int NVA, bool LDSW = false, int FP = 0, int TT = 1>
 __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const uint8_t* __restrict__ wire,
                                                    const int32_t* __restrict__ wire_len,
                                                    const int32_t* __restrict__ lut,
@@ -1694,7 +1697,7 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
     // passes: full passes of A bytes; a remainder of <= 256 bytes rides on the last one as
     // one tail dword per lane, a longer one is a partial pass of its own
     const int P = pitch / A, rem = pitch % A;
-    const bool fuse_tail = P > 0 && rem > 0 && rem <= 256;
+    const bool fuse_tail = P > 0 && rem > 0 && rem <= 256 * TT;
     const int passes = P + ((rem > 0 && !fuse_tail) ? 1 : 0);
     uint32_t bad = 0, verified = 0, fbad = 0;
     RxP<K, M> pl;
@@ -1762,8 +1765,8 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
         for (int q = 0; q < passes; ++q) {
             const int base = A * q;
             if (fuse_tail && q == passes - 1) {
-                RxSl<NVA, 1> sl{base + 4 * NVA * lane, base + A, lane, true, pitch};
-                rx2_pass<K, M, NVA, 1, FP>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, base + A, pitch, v_w0,
+                RxSl<NVA, TT> sl{base + 4 * NVA * lane, base + A, lane, true, pitch};
+                rx2_pass<K, M, NVA, TT, FP>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, base + A, pitch, v_w0,
                                               dsum, xsum, psl);
             } else {
                 RxSl<NVA, 0> sl{base + 4 * NVA * lane, 0, lane, base + 4 * NVA * lane < pitch, pitch};
@@ -2458,7 +2461,11 @@ hipError_t unpack_v2_launch(const WireArgs& a, const int32_t* lut, const uint32_
                                lut, records, rec_hdr, a.shards, fr);
         return hipGetLastError();
     }
-    if (nva == 4)
+    const uint32_t rem16 = (uint32_t)(a.pitch % 1024);
+    if (nva == 4 && tuning().wire_rx_split == 4 && a.pitch > 1024 && rem16 > 256 && rem16 <= 512)
+        hipLaunchKernelGGL((k_unpack_v2<K, M, 4, false, FP, 2>), grid, block, 0, s, a, w, wl, lut, records, rec_hdr,
+                           a.shards, fr);
+    else if (nva == 4)
         hipLaunchKernelGGL((k_unpack_v2<K, M, 4, false, FP>), grid, block, 0, s, a, w, wl, lut, records, rec_hdr,
                            a.shards, fr);
     else
@@ -2485,7 +2492,7 @@ hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint
     // 3: 8-B lanes.  RS(10,13) x 100k, A/B on one box (r02n): 1 KiB payloads 520 us on 16-B
     // lanes / 566 on 8-B; 1400 B 690 on 8-B / 725 on 16-B; 512 B 337 on 8-B / 411 on 16-B
     const int rx = tuning().wire_rx_split;
-    const int nva = rx == 2 ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
+    const int nva = (rx == 2 || rx == 4) ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
     QFEC_UNPACK_CASE(10, 3)
     QFEC_UNPACK_CASE(4, 1)
     QFEC_UNPACK_CASE(4, 2)
@@ -2507,7 +2514,7 @@ hipError_t launch_unpack_frames(const WireArgs& a, const FrameRecv& fr, int fp, 
     *launched = false;
     if (!a.groups) return hipSuccess;
     const int rx = tuning().wire_rx_split;
-    const int nva = rx == 2 ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
+    const int nva = (rx == 2 || rx == 4) ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
 #define QFEC_UFC(KK, MM)                                                               \
     if (a.k == KK && a.m == MM) {                                                      \
         *launched = true;                                                              \

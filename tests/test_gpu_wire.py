@@ -183,10 +183,12 @@ def test_pack_oversize_group(wire_fused):
 
 @pytest.mark.parametrize("k,n,checksum,pitch", [(10, 13, 1, 1040), (10, 13, 0, 1040), (4, 6, 1, 1040), (8, 12, 1, 1040),
                                                 (5, 8, 1, 1056), (8, 12, 1, 1056), (4, 6, 1, 1088), (4, 5, 0, 1088),
-                                                (10, 13, 1, 528), (7, 8, 1, 544), (3, 5, 1, 1280)])
+                                                (10, 13, 1, 528), (7, 8, 1, 544), (3, 5, 1, 1280), (10, 13, 1, 1408),
+                                                (4, 6, 0, 1408), (5, 8, 1, 1536), (10, 13, 1, 1296)])
 def test_unpack_row_tails(k, n, checksum, pitch):
     """Shard pitches whose last pass leaves a short row tail (1040 = 1024 + 16, 1056, 1088, 528,
-    544, 1280; k_unpack_v2 runs it as tail dwords on the last pass): every data packet of a
+    544, 1280; k_unpack_v2 runs it as tail dwords on the last pass; 1408, 1536, 1296 with two tail
+    dwords under wire_rx_split 4): every data packet of a
     recoverable group comes back exactly, on 16-B lanes with and without the LDS-staged flat row
     stores (wire_rx_lds) and on 8-B lanes (all give the same shard rows, verdicts and sizes).  Losses up to m + 1 per group, some datagrams corrupted
     inside the row tail, half the rows full to the pitch's limit."""
@@ -214,7 +216,9 @@ def test_unpack_row_tails(k, n, checksum, pitch):
                 w[g, j, wl[g, j] - 1] ^= 0x10  # a byte inside the row tail
     rx_len = np.where(drop, 0, wl).astype(np.int32)
     outs = []
-    for split, lds in ((2, 1), (2, 0), (3, 1)):  # 16-B lanes with / without LDS-staged rows, 8-B lanes
+    # 16-B lanes with / without LDS-staged rows, 8-B lanes, 16-B lanes with a remainder of up to
+    # 512 B on the last pass (1408 = 1024 + 384, 1536, 1296)
+    for split, lds in ((2, 1), (2, 0), (3, 1), (4, 0)):
         qa.tune("wire_rx_split", split)
         qa.tune("wire_rx_lds", lds)
         try:
