@@ -23,8 +23,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"encode": "k_encode_perm<{k}, {m}>", "reconstruct": "k_reconstruct_perm<{k}, {m},", "probe": "k_probe_xor"}
 # --workload wire: bench.py's `wire` leg (tools/side_legs.py), RS(10,13) 1 KiB payloads
-WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0, 1, 16, 0>", "unpack": "k_unpack_v2<10, 3, 4, true, 0>",
-                "pack_frames": "k_pack_wave64<10, 3, 1, 4, 1, 16, 0>", "unpack_frames": "k_unpack_v2<10, 3, 4, true, 4>"}
+WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0, 1, 16, 0>", "unpack": "k_unpack_v2<10, 3, 4, true, 0, 1>",
+                "pack_frames": "k_pack_wave64<10, 3, 1, 4, 1, 16, 0>", "unpack_frames": "k_unpack_v2<10, 3, 4, true, 4, 1>"}
 
 
 def run_pass(counter, out, bench_args, k, m, kernels=KERNELS, script="bench.py"):
@@ -117,6 +117,10 @@ def wire_main(a):
         w = sum(write[key]) / len(write[key])
         res[key] = {"fetch_kib_raw": f, "write_kib_raw": w, "read_bytes": 2 * f * 1024, "write_bytes": w * 1024,
                     "bytes_per_launch": 2 * f * 1024 + w * 1024, "launches": len(fetch[key])}
+    missing = [k2 for k2 in WIRE_KERNELS if k2 not in res]
+    if missing:  # a kernel renamed (template arguments) without this table following
+        print(f"no PMC rows for {missing}: kernel names {[WIRE_KERNELS[k2] for k2 in missing]} not found", file=sys.stderr)
+        return 1
     doc = {}
     if os.path.exists(a.json):
         with open(a.json) as fh:
@@ -136,4 +140,4 @@ def wire_main(a):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
