@@ -12,8 +12,10 @@ R=$GRAFT_REPO_ROOT
 echo "== pytest -m gpu" && timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 2; }
 tail -1 $OUT/pytest_gpu.log
 echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 3; }
-echo "== PMC traffic" && timeout -k 10 900 python tools/pmc_traffic.py --out $OUT/pmc --json $OUT/traffic.json --tag $TAG > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 6; }
-cp $OUT/traffic.json profiles/traffic.json  # bench.py reads roofline.traffic from here
+# bench.py reads roofline.traffic from profiles/traffic.json: the headline entry is updated in
+# place (the wire leg's entry, from tools/gpu_side_prof.sh, stays), and a copy comes back in $OUT
+echo "== PMC traffic" && timeout -k 10 900 python tools/pmc_traffic.py --out $OUT/pmc --json profiles/traffic.json --tag $TAG > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 6; }
+cp profiles/traffic.json $OUT/traffic.json
 echo "== bench" && timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 4; }
 cat $OUT/bench.json
 # only the timed step's launches (and config 4's) under the profiler, so each kernel's average is
