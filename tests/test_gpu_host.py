@@ -308,6 +308,53 @@ def test_per_packet_spin_back_to_back(oracle, resident):
         qa.tune("percall_resident", 1)
 
 
+def test_per_packet_threads(oracle):
+    """fec_encode / fec_decode from four host threads at once (ctypes drops the GIL, so the calls
+    really overlap), each on its own handle and fresh packets: every call is served by the one
+    resident server of the device, one request at a time, and every output is the oracle's."""
+    import threading
+    k, n, sz = 10, 13, 1028
+    fps = [qa.FecParms(k, n) for _ in range(4)]
+    expect = _encode_checker(oracle, fps[0], k, n)
+    full = fps[0].matrix
+    errors = []
+    qa.tune("percall_resident", 1)
+    before = qa.percall_stats()
+
+    def worker(t):
+        rng = np.random.default_rng(900 + t)
+        fp = fps[t]
+        try:
+            for call in range(150):
+                data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+                idx = k + call % (n - k)
+                dst = np.zeros(sz, np.uint8)
+                fp.encode(data, dst, idx, sz)
+                if not np.array_equal(dst, expect(data, idx)):
+                    errors.append(("encode", t, call))
+                if call % 10 == 0:  # a decode with the first 3 data packets lost
+                    coded = np.concatenate([data, np.zeros((n - k, sz), np.uint8)])
+                    for j in range(k, n):
+                        coded[j] = expect(data, j)
+                    keep = list(range(3, n))
+                    rc, pk, ix = fp.decode(coded[keep], keep, sz)
+                    if rc != 0 or not np.array_equal(pk, data):
+                        errors.append(("decode", t, call))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(("raised", t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+    st = qa.percall_stats()
+    if st["usable"] > 0:
+        assert st["calls"] - before["calls"] == 4 * (150 + 15)
+    assert full is not None
+
+
 def test_percall_server_idle_exit_and_relaunch(oracle):
     """The resident server exits by itself 1 ms after its last request (so no block outlives an
     idle caller, and a device synchronise never waits on it for long), a call after an idle gap
