@@ -191,3 +191,45 @@ def test_tune_keys_documented_and_accepted():
     # back to the defaults the rest of this process expects
     for key, value in (("recon_impl", -1), ("wire_store_nt", 3), ("percall_resident", 1), ("percall_in", 0)):
         assert L.qfec_tune(key.encode(), value) == 0
+
+
+def test_fec_decode_shuffle_and_pattern_cache(oracle):
+    """fec_decode's host part on CPU (sz = 0: no bytes move, so no device is touched): the
+    shuffle's permutation of pkt[] and index[], and the return code for valid, conflicting,
+    invalid and duplicate index lists, equal the oracle's restatement of fec.c:738-862 over
+    6 000 random calls -- more distinct loss patterns than the per-handle decode cache holds
+    (4 096), so the cache is cleared and refilled on the way, and every repeat of a pattern
+    is served from it."""
+    L = lib()
+    k, n = 10, 20
+    h = C.c_void_p(L.fec_new(k, n))
+    full = np.zeros((n, k), np.uint8)
+    assert L.qfec_fec_matrix(h, full.ctypes.data_as(C.c_void_p)) == 0
+    rng = np.random.default_rng(77)
+    bufs = np.zeros((n, 4), np.uint8)
+    base = bufs.ctypes.data
+    prev = None
+    for call in range(6000):
+        if call % 7 == 0 and prev is not None:  # a repeat: served from the cache
+            idx = list(prev)
+        elif call % 50 == 49:  # now and then an invalid or conflicting list
+            idx = list(rng.choice(n, k, replace=False))
+            if call % 100 == 49:
+                idx[int(rng.integers(0, k))] = n + 3  # invalid index
+            else:
+                idx[1] = idx[0] if idx[0] < k else int(rng.integers(0, k))  # duplicate / conflict
+        else:
+            idx = sorted(rng.choice(n, k, replace=False)) if call % 3 else list(rng.choice(n, k, replace=False))
+        idx = [int(x) for x in idx]
+        prev = idx
+        ptrs = (C.c_void_p * k)(*[base + 4 * i for i in range(k)])
+        ia = (C.c_int * k)(*idx)
+        rc = L.fec_decode(h, ptrs, ia, 0)
+        rc2, _, ix2 = oracle.fec_decode(k, n, full, bufs[:k], idx)
+        assert rc == rc2, (call, idx, rc, rc2)
+        if rc == 0:
+            assert list(ia) == list(ix2), (call, idx)
+            # the pointers moved with their indices: slot s holds the buffer the caller gave for index[s]
+            where = {v: i for i, v in enumerate(idx)}
+            assert [((p - base) // 4) for p in ptrs] == [where[v] for v in ia], (call, idx)
+    L.fec_free(h)
