@@ -475,6 +475,8 @@ __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K]
 // One wave per 64 16-B columns of a group: a group of `cols` columns gets
 // wpg = ceil(cols / 64) waves (B = 1400 -> 2), all in flight together, no column loop.
 // IMPL 6: IMPL 3 compiled for 8 waves per SIMD (register caps; 7 otherwise: 106 SGPRs)
+// IMPL 8: IMPL 3 launched with one group per block (blocks of wpg8 waves), so a group's slab
+// waves share a CU and its scalar data (marks, LUT entry, record header, tables)
 template <int K, int M, int IMPL_, int CT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMPL_ == 6 ? 8 : 1)))
 k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
@@ -484,10 +486,10 @@ k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint32_t* __restrict__ records) {
     // __restrict__ parameters: the LUT and records are provably not written by this
     // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
-    constexpr int IMPL = IMPL_ == 6 ? 3 : IMPL_;
+    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8) ? 3 : IMPL_;
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (IMPL_ == 8 ? a.wpg8 : 4u) + (threadIdx.x >> 6));
     const uint32_t wpg = IMPL == 5 ? 1u : IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
@@ -693,11 +695,12 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 
 #define QFEC_REC_LAUNCH(KK, MM, AR)                                                                        \
     do {                                                                                                   \
+        const dim3 blk(AR == 8 ? 64u * a.wpg8 : 256u), grd(AR == 8 ? (unsigned)a.groups : pgrid);          \
         if (AR >= 2 && a.compact && a.t256)                                                                \
-            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, (AR >= 2) * 1>), dim3(pgrid), dim3(256), 0, stream, a, \
+            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, (AR >= 2) * 1>), grd, blk, 0, stream, a,   \
                                a.data, a.parity, a.marks, a.lut, a.records);                               \
         else                                                                                               \
-            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, 0>), dim3(pgrid), dim3(256), 0, stream, a, \
+            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, 0>), grd, blk, 0, stream, a,               \
                                a.data, a.parity, a.marks, a.lut, a.records);                               \
     } while (0)
 
@@ -710,7 +713,12 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
                             : a.impl;                                              \
         if (im == 4 && !lanes12_ok) im = 2;                                        \
         const unsigned pgrid = im == 5 ? grid : (im == 3 || im == 6) ? pgrid8 : im == 4 ? pgrid12 : pgrid16; \
-        if (im == 6) QFEC_REC_LAUNCH(KK, MM, 6);                                   \
+        /* 8-B lanes run one group per block where a group is at most 4 waves: its slab */ \
+        /* waves share a CU (RS(16,4) B=1400: 1 218 against 1 224 us, r03blk)            */ \
+        if (im == 3 && a.impl < 0) im = 8;                                         \
+        if (im == 8 && (a.wpg8 < 1 || a.wpg8 > 4)) im = 3;                         \
+        if (im == 8) QFEC_REC_LAUNCH(KK, MM, 8);                                   \
+        else if (im == 6) QFEC_REC_LAUNCH(KK, MM, 6);                              \
         else if (im == 5) QFEC_REC_LAUNCH(KK, MM, 5);                              \
         else if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                              \
         else if (im == 3) QFEC_REC_LAUNCH(KK, MM, 3);                              \
