@@ -798,26 +798,38 @@ def per_call_leg(reps=2000, ref_lib=None, batched=True):
     rng = np.random.default_rng(11)
     data = rng.integers(0, 256, (n, sz), dtype=np.uint8)
     idx_t = [0, 1, 2, 4, 5, 7, 8, 10, 11, 12]  # data 3, 6, 9 lost; the first k valid rows
-    out = {"shape": "RS(10,3), sz 1028 B per packet"}
+    # 64 distinct groups of inputs, cycled, so every group's first fec_encode meets new inputs
+    # (libqfec keeps the last group's rows per handle: repeating one group would time its cache)
+    groups = rng.integers(0, 256, (64, k, sz), dtype=np.uint8)
+    out = {"shape": "RS(10,3), sz 1028 B per packet; encode inputs cycle over 64 distinct groups"}
 
     def run(lib, tag):
         h = C.c_void_p(lib.fec_new(k, n))
-        src = (C.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
+        srcs = [(C.c_void_p * k)(*[groups[g, i].ctypes.data for i in range(k)]) for g in range(64)]
         dst = np.zeros(sz, np.uint8)
+        dptr = C.c_void_p(dst.ctypes.data)
         pk_t = (C.c_void_p * k)(*[data[i].ctypes.data for i in idx_t])
         pk = (C.c_void_p * k)()
         ix = (C.c_int * k)()
         ix_t = (C.c_int * k)(*idx_t)
+        it = [0]
 
-        def enc():
-            lib.fec_encode(h, src, C.c_void_p(dst.ctypes.data), k, sz)
+        def enc():  # one check packet of a new group
+            lib.fec_encode(h, srcs[it[0] & 63], dptr, k, sz)
+            it[0] += 1
+
+        def grp():  # all n - k check packets of a new group, as get_fec_encoded_pkt asks for them
+            s_ = srcs[it[0] & 63]
+            for idx in range(k, n):
+                lib.fec_encode(h, s_, dptr, idx, sz)
+            it[0] += 1
 
         def dec():
             C.memmove(pk, pk_t, C.sizeof(pk))
             C.memmove(ix, ix_t, C.sizeof(ix))
             lib.fec_decode(h, pk, ix, sz)
 
-        for f, name in ((enc, "fec_encode_us"), (dec, "fec_decode_us")):
+        for f, name in ((enc, "fec_encode_us"), (grp, "fec_encode_group_us"), (dec, "fec_decode_us")):
             for _ in range(50):
                 f()
             t0 = time.perf_counter()
@@ -830,8 +842,13 @@ def per_call_leg(reps=2000, ref_lib=None, batched=True):
         run(ref_lib, "ref_cpu_")
         return out
     st0 = qa.percall_stats()
+    c0 = qa.percall_counters()
     run(qa.lib(), "gpu_")
     st = qa.percall_stats()
+    c1 = qa.percall_counters()
+    out["gpu_group_cache"] = {"hits": c1["group_hits"] - c0["group_hits"],
+                              "misses": c1["group_misses"] - c0["group_misses"]}
+    out["percall_idle_us"] = c1["idle_us"]
     out["gpu_path"] = ("resident server (percall_resident 1, qfec_percall.hpp)" if st["calls"] > st0["calls"]
                        else "one launch per call (qfec_percall.hpp k_percall)")
     out["gpu_server_launches"] = st["launches"] - st0["launches"]
@@ -1072,14 +1089,21 @@ def main(argv=None):
                     ref3 = 3 * cpu["per_call"]["ref_cpu_fec_encode_us"]
                     beat = [b["groups"] for b in per_call["batched_encode_host"] if b["us_per_group"] < ref3]
                     per_call["batch_beats_reference_encode_at_groups"] = beat[0] if beat else None
+                if isinstance(per_call, dict) and "gpu_fec_encode_group_us" in per_call:
+                    # the unchanged caller's group of n - k fec_encode calls, GPU over CPU reference
+                    ref_g = cpu["per_call"].get("ref_cpu_fec_encode_group_us")
+                    if ref_g:
+                        per_call["group_vs_reference"] = round(per_call["gpu_fec_encode_group_us"] / ref_g, 3)
         except Exception as exc:
             cpu["per_call"] = {"error": repr(exc)}
         if host_sample is not None:  # the checker role: config 5's output against the reference rs.c
             try:
                 host_mixed["reference_check"] = cpu_check_host_sample(host_sample)
                 ok = ok and bool(host_mixed["reference_check"].get("match"))
-            except Exception as exc:
+            except Exception as exc:  # a checker that could not run verifies nothing
                 host_mixed["reference_check"] = {"error": repr(exc)}
+                host_mixed["verified"] = False
+                ok = False
         # the reference's datagram pipeline (FecCodecBuf.cpp + system/fec.c, oracle/_ref),
         # RS(10,13) 1 KiB payloads, send + receive, 1 thread: the CPU side of DESIGN 3.5
         ref_wire = os.path.join(ROOT, "oracle", "_ref", "ref_wire_bench")

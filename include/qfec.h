@@ -171,7 +171,8 @@ int qfec_unpack_datagrams(qfec_code *code, const unsigned char *d_wire, long lon
  * qfec_unframe_udp reverses it (ProtocolUdp::RecvPacket, ProtocolBasic.cpp:152-210):
  * d_status[r] = 0 ok, 1 short, 2 bad checksum, 3 bad cmd, 4 too long; d_out row = the data,
  * d_out_len = len - 4 (- 8 with session = 1); d_info [rows][4] = xor mask, c, cmd & 0x1f,
- * protocol (nullable); d_conv_hid receives the Session prefix when session = 1 (nullable).
+ * protocol (nullable); d_conv_hid receives the Session prefix when session = 1 (nullable; its
+ * entries are meaningful only for rows whose d_status is 0).
  * Pitches multiples of 16, rows 16-B aligned. */
 int qfec_frame_udp(const unsigned char *d_in, long long in_pitch, const int *d_len, long long rows,
                    const unsigned char *d_mask, const unsigned int *d_conv_hid, int gmask, int cmd, int protocol,
@@ -195,8 +196,10 @@ int qfec_unframe_udp(const unsigned char *d_in, long long in_pitch, const int *d
  * every row, rows RecvPacket rejects counting as not received, then qfec_unpack_datagrams over
  * the datagrams inside: the same d_marks / d_rx_size / d_status / d_psize / d_shards as that
  * call.  d_frame_status [G*n] (nullable) = RecvPacket's verdict per row (0 ok, 1 short,
- * 2 checksum, 3 cmd, 4 too long, as qfec_unframe_udp); d_conv_hid receives the Session prefix
- * of rows with status 0 when session = 1 (nullable).  One pass for the templated (k, m). */
+ * 2 checksum, 3 cmd, 4 too long, as qfec_unframe_udp; a row with both a bad checksum and a bad
+ * cmd is 2, RecvPacket's order); d_conv_hid receives the Session prefix when session = 1
+ * (nullable): its entries are meaningful only for rows whose d_frame_status is 0, the others are
+ * unspecified.  One pass for the templated (k, m). */
 int qfec_pack_frames(qfec_code *code, const unsigned char *d_payload, const long long *d_offsets,
                      const int *d_sizes, const unsigned int *d_seq, long long groups, int checksum,
                      unsigned char *d_shards, long long shard_pitch, const unsigned char *d_mask,
@@ -262,7 +265,19 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *                      and exits by itself after 1 ms without a request | 0 one launch per call
  *                      (setting 0 stops the servers)
  *   "percall_in"       0 the server's input rows in device memory | 1 in write-combined pinned host
- *                      memory (A/B: 0.9 us slower per call) */
+ *                      memory (A/B: 0.9 us slower per call)
+ *   "percall_idle_us"  how long the resident server's block stays on the device after its last
+ *                      request, 0 .. 1 000 000 us (default 1 000); 0 = it exits right after each
+ *                      call (every call then pays a launch).  A hipDeviceSynchronize issued while it
+ *                      is resident waits for it: at most this long after the last call.
+ *   "percall_timeout_us" how long a call spins for the server before it stops the block and waits
+ *                      for it (the block serves the pending request first), or, if the request was
+ *                      never taken, runs it through one launch (default 2 000 000)
+ *   "percall_group"    1 fec_encode of a parity index computes the group's n - k rows in one request
+ *                      and serves the group's other indices from a per-handle copy while src[], sz and
+ *                      every input byte are unchanged | 0 one request per index
+ *   "percall_fault"    (tests) 1 requests are never handed to a server, so every call takes the
+ *                      timeout branch */
 int qfec_tune(const char *key, int value);
 
 /* The resident per-call server of the current device (qfec_tune "percall_resident"): out[0] calls
@@ -271,6 +286,11 @@ int qfec_tune(const char *key, int value);
  * out[4] 1 set up | -1 unavailable on this device (device memory not CPU-mapped) | 0 not yet used.
  * Returns QFEC_OK, or an error without a device. */
 int qfec_percall_stats(unsigned long long out[5]);
+/* The same counters and more, as many as `n` asks for (returns how many were written, or an error):
+ * [0..4] as qfec_percall_stats, [5] requests the server did not serve within percall_timeout_us
+ * (each then waited for the stopped server, or ran through one launch), [6] / [7] fec_encode calls
+ * served from / computing the group cache (all handles), [8] the current percall_idle_us. */
+int qfec_percall_counters(unsigned long long *out, int n);
 
 int qfec_set_kernel_variant(int variant);
 int qfec_get_kernel_variant(void);

@@ -13,8 +13,13 @@
  *     first e non-erased parity rows in ascending order; parity is never regenerated,
  *     returns -1 when any group is under-determined                (rs.c:598-643)
  *   - a zero coefficient in column 0 leaves the output's previous bytes in place
- *     (mul() memsets 0 bytes, rs.c:116-117); the public `parity` matrix may be edited
- *     between calls and is re-read on every call
+ *     (mul() memsets 0 bytes, rs.c:116-117)
+ *   - the public matrices may be edited between calls and are re-read on every call, each
+ *     where rs.c reads it: encode multiplies by `parity` (rs.c:583); reconstruct builds its
+ *     k x k sub-matrix from the rows of `m` (data rows included, rs.c:505, 536-548), so the
+ *     two are independent copies, as in rs.c (:431-442).  A sub-matrix that an edit made
+ *     singular is decoded with invert_mat's partially eliminated state and does not change
+ *     the return value: rs.c ignores invert_mat's result (rs.c:556)
  *   - reed_solomon_new() errors: 1 bad shape, 2..5 allocation     (rs.c:404-476)
  */
 #ifndef QFEC_RS_H
@@ -29,8 +34,8 @@ typedef struct _reed_solomon {
     int data_shards;
     int parity_shards;
     int shards;
-    unsigned char *m;      /* n x k: identity on top, parity rows below */
-    unsigned char *parity; /* m x k parity rows                        */
+    unsigned char *m;      /* n x k: identity on top, parity rows below (reconstruct reads it) */
+    unsigned char *parity; /* m x k parity rows (encode reads it)                             */
 } reed_solomon;
 
 #ifdef __cplusplus

@@ -286,6 +286,94 @@ def gen_reconstruct_large(rs):
     np.savez_compressed(os.path.join(OUT, "reconstruct_large.npz"), **out)
 
 
+# reed_solomon handles whose public matrices the caller edits (rs.h:7-13 exposes both):
+# encode reads rs->parity (rs.c:583), reconstruct builds its sub-matrix from rs->m, data rows
+# included (rs.c:505, 536-548), and ignores invert_mat's failure (rs.c:556).
+#   name: (k, m, B, groups or None = every mask, edits of parity, edits of m, stored in full?)
+# an edit is (row, col, value); a row edit (row, None, values) replaces the whole row
+RS_EDITS = {
+    # (i) parity edited (a zero in column 0 among them): encode, then reconstruct from the
+    # untouched m over the parity that encode produced
+    "p42": (4, 2, 16, None, [(0, 0, 0), (1, 3, 0x77), (0, 2, 0x11)], [], True),
+    # (ii) rows of m edited: a data row and a parity row (column 0 zeroed)
+    "m42": (4, 2, 16, None, [], [(1, None, [3, 1, 0, 9]), (5, None, [0, 0xC4, 0x21, 0x90])], True),
+    # (iii) singular sub-matrices: parity row 0 == data row 0, parity row 1 all zero
+    "s42": (4, 2, 16, None, [], [(4, None, [1, 0, 0, 0]), (5, None, [0, 0, 0, 0])], True),
+    "s103": (10, 3, 8, None, [(2, 0, 0)], [(4, None, list(range(1, 11))), (11, None, [0, 0, 0, 0, 0, 0, 0, 1, 0, 0]),
+                                           (12, None, [0] * 10)], False),
+    # bench block sizes, where the wide-lane kernel bodies run
+    "m103w": (10, 3, 1024, 300, [], [(4, None, [7, 0, 3, 1, 0x99, 2, 5, 0, 1, 0xFE]), (11, 0, 0),
+                                    (12, None, [0, 0, 0, 0, 0, 0, 0, 1, 0, 0])], False),
+    "m164w": (16, 4, 1400, 200, [(3, 0, 0)], [(0, None, [(5 * i + 1) & 255 for i in range(16)]),
+                                             (16, None, [(11 * i + 7) & 255 for i in range(16)]),
+                                             (18, None, [0] * 16), (19, 0, 0)], False),
+}
+
+
+def _apply_edits(arr, k, edits):
+    for r, c, v in edits:
+        if c is None:
+            for i, x in enumerate(v):
+                arr[r * k + i] = x
+        else:
+            arr[r * k + c] = v
+
+
+def gen_rs_edits(rs):
+    """reed_solomon_encode / reconstruct on handles whose public `parity` / `m` were edited,
+    including edits that make some erasure pattern's sub-matrix singular (rs.c then decodes
+    with invert_mat's partial state and keeps err unchanged).  Erased data buffers are
+    pre-filled with 0x5A; parity is random ('incons') unless the case encodes first."""
+    out = {}
+    for name, (k, m, B, sample, pedits, medits, store) in RS_EDITS.items():
+        n = k + m
+        if sample is None:
+            gmarks = all_masks(n)
+        else:
+            gen = np.random.default_rng(0xED17 + 7 * k + B)
+            gmarks = np.zeros((sample, n), np.uint8)
+            for g in range(sample):
+                gmarks[g, gen.choice(n, size=int(gen.integers(1, m + 2)), replace=False)] = 1
+        G = gmarks.shape[0]
+        seed = 0xED170000 + 131 * k + m + B
+        data0 = synth_bytes(seed, G * k * B).reshape(G * k, B)
+        h = rs.reed_solomon_new(k, m)
+        _apply_edits(h.contents.parity, k, pedits)
+        _apply_edits(h.contents.m, k, medits)
+        pm = np.ctypeslib.as_array(h.contents.parity, shape=(m * k,)).copy().reshape(m, k)
+        full = np.ctypeslib.as_array(h.contents.m, shape=(n * k,)).copy().reshape(n, k)
+        if pedits:  # encode with the edited parity rows over 0x5A (stale bytes show)
+            par = np.full((G * m, B), 0x5A, dtype=np.uint8)
+            ptrs = (C.c_void_p * (G * n))(*([ptr(data0, i * B) for i in range(G * k)] +
+                                             [ptr(par, i * B) for i in range(G * m)]))
+            rs.reed_solomon_encode(h, ptrs, G * n, B)
+            enc = par.copy()
+        else:
+            par = synth_bytes(seed ^ 0xFFFF, G * m * B).reshape(G * m, B)
+            enc = None
+        marks = np.concatenate([gmarks[:, :k].reshape(-1), gmarks[:, k:].reshape(-1)]).astype(np.uint8)
+        d = data0.copy()
+        d[marks[:G * k] == 1] = 0x5A
+        p = par.copy()
+        ptrs = (C.c_void_p * (G * n))(*([ptr(d, i * B) for i in range(G * k)] + [ptr(p, i * B) for i in range(G * m)]))
+        rc = rs.reed_solomon_reconstruct(h, ptrs, C.c_void_p(ptr(marks)), G * n, B)
+        rs.reed_solomon_release(h)
+        assert np.array_equal(p, par)
+        out[f"seed_{name}"] = np.array([seed], dtype=np.uint64)
+        out[f"shape_{name}"] = np.array([k, m, B], dtype=np.int32)
+        out[f"marks_{name}"] = gmarks
+        out[f"parity_{name}"] = pm
+        out[f"m_{name}"] = full
+        out[f"rc_{name}"] = np.array([rc], dtype=np.int32)
+        if enc is not None:  # whole for the small cases, else a digest (tests re-encode and compare)
+            out[f"enc_{name}"] = enc if store else np.frombuffer(hashlib.sha256(enc.tobytes()).digest(), np.uint8)
+        if store:
+            out[f"out_{name}"] = d
+        else:
+            out[f"out_{name}"] = np.frombuffer(hashlib.sha256(d.tobytes()).digest(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(OUT, "rs_edits.npz"), **out)
+
+
 def gen_fec_decode(fec):
     """fec.c fec_decode on k received packets: NetFecCodec order (first k valid in group
     order), random arrival order (exercises shuffle, fec.c:738-771), and error cases
@@ -451,7 +539,7 @@ def main():
     rs, fec = load_ref()
     gens = {"matrices": lambda: gen_matrices(rs, fec), "encode": lambda: gen_encode(rs, fec),
             "reconstruct": lambda: gen_reconstruct(rs), "reconstruct_large": lambda: gen_reconstruct_large(rs),
-            "fec_decode": lambda: gen_fec_decode(fec), "wire": gen_wire}
+            "fec_decode": lambda: gen_fec_decode(fec), "wire": gen_wire, "rs_edits": lambda: gen_rs_edits(rs)}
     for name in (sys.argv[1:] or list(gens)):
         gens[name]()
     manifest = {

@@ -34,6 +34,7 @@ class Oracle:
         L.orc_rs_encode_contig.argtypes = [i, i, vp, vp, vp, ll, i, ll]
         L.orc_fec_encode_contig.argtypes = [i, i, vp, vp, vp, ll, i, ll]
         L.orc_rs_reconstruct_contig.argtypes = [i, i, vp, vp, vp, vp, ll, i, ll]
+        L.orc_rs_reconstruct_full_contig.argtypes = [i, i, vp, vp, vp, vp, ll, i, ll]
         L.orc_fec_reconstruct_contig.argtypes = [i, i, vp, vp, vp, vp, ll, i, ll]
         L.orc_fec_reconstruct_contig.restype = ll
         L.orc_fec_decode.argtypes = [i, i, vp, C.POINTER(vp), C.POINTER(C.c_int), i]
@@ -68,6 +69,11 @@ class Oracle:
         rc = self.L.orc_invert(_p(a), a.shape[0])
         return None if rc else a
 
+    def invert_partial(self, mat):
+        """invert_mat as rs.c uses it: (rc, matrix as left), the partial state when singular."""
+        a = np.ascontiguousarray(mat, dtype=np.uint8).copy()
+        return self.L.orc_invert(_p(a), a.shape[0]), a
+
     def mul(self, a, b):
         return int(self.L.orc_mul(a, b))
 
@@ -87,6 +93,13 @@ class Oracle:
         m = parity.shape[1]
         return self.L.orc_rs_reconstruct_contig(k, m, _p(np.ascontiguousarray(rows)), _p(data), _p(parity),
                                                 _p(marks_rs), G, length, pitch)
+
+    def rs_reconstruct_full(self, full, data, parity, marks_rs, length):
+        """reed_solomon_reconstruct with the handle's whole n x k matrix rs->m (rs.c:505, 536-556)."""
+        G, k, pitch = data.shape
+        m = parity.shape[1]
+        return self.L.orc_rs_reconstruct_full_contig(k, m, _p(np.ascontiguousarray(full, dtype=np.uint8)), _p(data),
+                                                     _p(parity), _p(marks_rs), G, length, pitch)
 
     def fec_reconstruct(self, rows, data, parity, marks_rs, length):
         G, k, pitch = data.shape

@@ -278,8 +278,8 @@ int orc_rs_encode(int k, int m, const u8 *parity_rows, u8 **shards, int nr_shard
 /* reed_solomon_decode() (rs.c:500-565) for one group.  `lost` are the erased data
  * indices (sorted here, rs.c:512-526), `fixp` the chosen parity buffers, `fixr` their
  * parity-row numbers, all of length e. */
-static int rs_decode_group(int k, const u8 *parity_rows, u8 **data, u8 **fixp, const int *fixr,
-                           int *lost, int e, int len)
+static int rs_decode_group(int k, const u8 *parity_rows, const u8 *full, u8 **data, u8 **fixp,
+                           const int *fixr, int *lost, int e, int len)
 {
     u8 *mat = (u8 *)malloc((size_t)k * (size_t)k);
     u8 **in = (u8 **)malloc(sizeof(u8 *) * (size_t)k);
@@ -288,16 +288,21 @@ static int rs_decode_group(int k, const u8 *parity_rows, u8 **data, u8 **fixp, c
     for (i = 0; i < e; ++i)
         for (j = i + 1; j < e; ++j)
             if (lost[i] > lost[j]) { int t = lost[i]; lost[i] = lost[j]; lost[j] = t; }
-    /* surviving data rows are unit rows, in ascending order (rs.c:528-542) */
+    /* surviving data rows in ascending order (rs.c:528-542): row i of rs->m when `full` is
+     * given (the n x k matrix the handle carries), else the unit row */
     for (i = 0; i < k; ++i) {
         if (x < e && lost[x] == i) { ++x; continue; }
-        memset(mat + rows * k, 0, (size_t)k);
-        mat[rows * k + i] = 1;
+        if (full) {
+            memcpy(mat + rows * k, full + (size_t)i * k, (size_t)k);
+        } else {
+            memset(mat + rows * k, 0, (size_t)k);
+            mat[rows * k + i] = 1;
+        }
         in[rows++] = data[i];
     }
-    /* then the chosen parity rows (rs.c:544-551) */
+    /* then the chosen parity rows (rs.c:544-551): rs->m row k + fixr[i] */
     for (i = 0; i < e && rows < k; ++i) {
-        memcpy(mat + rows * k, parity_rows + fixr[i] * k, (size_t)k);
+        memcpy(mat + rows * k, full ? full + (size_t)(k + fixr[i]) * k : parity_rows + fixr[i] * k, (size_t)k);
         in[rows++] = fixp[i];
     }
     if (rows < k) { free(mat); free(in); free(out); return -1; }
@@ -315,8 +320,8 @@ static int rs_decode_group(int k, const u8 *parity_rows, u8 **data, u8 **fixp, c
  * marks[G*k .. G*n-1] parity shards.  Per group the first e non-erased parity rows
  * (ascending) are used (rs.c:620-629); parity is never regenerated.  Returns -1 if
  * any group had fewer usable parity rows than erased data shards. */
-int orc_rs_reconstruct(int k, int m, const u8 *parity_rows, u8 **shards, const u8 *marks,
-                       int nr_shards, int len)
+static int rs_reconstruct(int k, int m, const u8 *parity_rows, const u8 *full, u8 **shards,
+                          const u8 *marks, int nr_shards, int len)
 {
     int groups = nr_shards / (k + m), g, i, err = 0;
     int *lost = (int *)malloc(sizeof(int) * (size_t)k);
@@ -336,12 +341,27 @@ int orc_rs_reconstruct(int k, int m, const u8 *parity_rows, u8 **shards, const u
         for (i = 0; i < m && p < e; ++i)
             if (!pm[i]) { fixr[p] = i; fixp[p] = par[i]; ++p; }
         if (p == e)
-            rs_decode_group(k, parity_rows, data, fixp, fixr, lost, e, len);
+            rs_decode_group(k, parity_rows, full, data, fixp, fixr, lost, e, len);
         else
             err = -1;
     }
     free(lost); free(fixr); free(fixp);
     return err;
+}
+
+int orc_rs_reconstruct(int k, int m, const u8 *parity_rows, u8 **shards, const u8 *marks,
+                       int nr_shards, int len)
+{
+    return rs_reconstruct(k, m, parity_rows, NULL, shards, marks, nr_shards, len);
+}
+
+/* The same with the handle's whole n x k matrix rs->m, as rs.c reads it (rs.c:505, 536-548):
+ * a caller may have edited it (data rows included), and a sub-matrix that is singular then
+ * decodes with invert_mat's partial state (its return value is ignored, rs.c:556). */
+int orc_rs_reconstruct_full(int k, int m, const u8 *full, u8 **shards, const u8 *marks,
+                            int nr_shards, int len)
+{
+    return rs_reconstruct(k, m, NULL, full, shards, marks, nr_shards, len);
 }
 
 /* ------------------------------------------------------------------ fec.c codec */
@@ -488,6 +508,21 @@ int orc_rs_reconstruct_contig(int k, int m, const u8 *parity_rows, u8 *data, u8 
         for (i = 0; i < m; ++i) sh[groups * k + g * m + i] = parity + (g * m + i) * pitch;
     }
     rc = orc_rs_reconstruct(k, m, parity_rows, sh, marks, (int)(groups * n), len);
+    free(sh);
+    return rc;
+}
+
+int orc_rs_reconstruct_full_contig(int k, int m, const u8 *full, u8 *data, u8 *parity,
+                                   const u8 *marks, long long groups, int len, long long pitch)
+{
+    long long g, n = k + m;
+    int i, rc;
+    u8 **sh = (u8 **)malloc(sizeof(u8 *) * (size_t)(groups * n));
+    for (g = 0; g < groups; ++g) {
+        for (i = 0; i < k; ++i) sh[g * k + i] = data + (g * k + i) * pitch;
+        for (i = 0; i < m; ++i) sh[groups * k + g * m + i] = parity + (g * m + i) * pitch;
+    }
+    rc = orc_rs_reconstruct_full(k, m, full, sh, marks, (int)(groups * n), len);
     free(sh);
     return rc;
 }

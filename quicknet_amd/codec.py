@@ -78,6 +78,17 @@ def percall_stats():
     return {"calls": out[0], "launches": out[1], "relaunches": out[2], "running": bool(out[3]), "usable": usable}
 
 
+def percall_counters():
+    """qfec_percall_counters: percall_stats plus timeouts, fec_encode group-cache hits / misses and
+    the current percall_idle_us."""
+    out = (C.c_ulonglong * 9)()
+    n = lib().qfec_percall_counters(out, 9)
+    check(n if n < 0 else 0, "qfec_percall_counters")
+    usable = out[4] if out[4] < 2**63 else out[4] - 2**64
+    return {"calls": out[0], "launches": out[1], "relaunches": out[2], "running": bool(out[3]), "usable": usable,
+            "timeouts": out[5], "group_hits": out[6], "group_misses": out[7], "idle_us": out[8]}
+
+
 def synth_fill(t, seed, stream=None):
     """Fill a device uint8 tensor with quicknet_amd.synth.synth_bytes(seed, t.numel())."""
     check(lib().qfec_synth_fill(_dev_ptr(t, what="synth_fill"), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(stream)),
@@ -418,6 +429,15 @@ class ReedSolomon:
     def parity(self):
         """The public parity matrix (editable, as in rs.h:12)."""
         return np.ctypeslib.as_array(self._h.contents.parity, shape=(self.m, self.k))
+
+    @property
+    def m_matrix(self):
+        """The public n x k matrix rs->m (editable, as in rs.h:11): reconstruct decodes from it."""
+        return np.ctypeslib.as_array(self._h.contents.m, shape=(self.k + self.m, self.k))
+
+    def code(self):
+        """The batched code behind this handle (qfec_rs_code): the handle's current matrices."""
+        return Code(lib().qfec_rs_code(self._h), owner=False)
 
     @staticmethod
     def _ptrs(data, parity):

@@ -8,7 +8,9 @@
 // matrices.
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "qfec_internal.hpp"
 
@@ -109,6 +111,59 @@ bool gf_invert(uint8_t* a, int k) {
     return true;
 }
 
+bool gf_invert_rs(uint8_t* a, int k) {
+    // module/rs.c:224-344 (invert_mat): in-place Gauss-Jordan whose pivot for step s is the
+    // diagonal a[s][s] when column s is unused and non-zero, else the first non-zero entry
+    // of an unused column in a row-major scan of the rows not yet pivoted.  The pivot row is
+    // swapped into row `col`, scaled so the pivot reads 1/p, and eliminated from every other
+    // row (skipped when it already is a unit row); the column swaps are undone at the end.
+    // rs.c ignores the result (rs.c:556), so on failure the caller uses `a` exactly as the
+    // elimination left it: rows swapped and reduced up to the failing step, no column swaps.
+    const Field& f = field();
+    std::vector<uint8_t> used((size_t)k, 0);
+    std::vector<int> sw_row((size_t)k, -1), sw_col((size_t)k, -1);
+    auto row = [&](int r) { return a + (size_t)r * k; };
+    for (int s = 0; s < k; ++s) {
+        int pr = -1, pc = -1;
+        if (!used[s] && row(s)[s]) {
+            pr = pc = s;
+        } else {
+            for (int r = 0; r < k && pc < 0; ++r) {
+                if (used[r]) continue;
+                for (int c = 0; c < k; ++c)
+                    if (!used[c] && row(r)[c]) { pr = r; pc = c; break; }
+            }
+            if (pc < 0) return false;  // "pivot not found"
+        }
+        used[pc] = 1;
+        if (pr != pc) std::swap_ranges(row(pr), row(pr) + k, row(pc));
+        sw_row[s] = pr;
+        sw_col[s] = pc;
+        uint8_t* p = row(pc);
+        if (p[pc] != 1) {
+            const uint8_t* sc = f.mul[f.inv[p[pc]]];
+            p[pc] = 1;
+            for (int c = 0; c < k; ++c) p[c] = sc[p[c]];
+        }
+        bool unit = true;
+        for (int c = 0; c < k && unit; ++c) unit = p[c] == (c == pc);
+        if (unit) continue;
+        for (int r = 0; r < k; ++r) {
+            if (r == pc) continue;
+            uint8_t* q = row(r);
+            const uint8_t x = q[pc];
+            q[pc] = 0;
+            if (!x) continue;
+            const uint8_t* mx = f.mul[x];
+            for (int c = 0; c < k; ++c) q[c] ^= mx[p[c]];
+        }
+    }
+    for (int s = k - 1; s >= 0; --s)
+        if (sw_row[s] != sw_col[s])
+            for (int r = 0; r < k; ++r) std::swap(row(r)[sw_row[s]], row(r)[sw_col[s]]);
+    return true;
+}
+
 bool cauchy_rows(int k, int m, std::vector<uint8_t>& out) {
     // module/rs.c:404 shape check, :437-440 rows
     if (k <= 0 || m <= 0 || k + m > 255) return false;
@@ -160,7 +215,7 @@ void perm_entry(uint8_t c, uint32_t* o) {
 }
 
 int decode_rows(const uint8_t* P, int k, int m, const uint8_t* marks, std::vector<uint8_t>& rows,
-                std::vector<int>& survivors, std::vector<int>& lost) {
+                std::vector<int>& survivors, std::vector<int>& lost, const uint8_t* full) {
     lost.clear();
     survivors.clear();
     for (int i = 0; i < k; ++i) {
@@ -174,12 +229,19 @@ int decode_rows(const uint8_t* P, int k, int m, const uint8_t* marks, std::vecto
         if (!marks[k + j]) survivors.push_back(k + j);
     if ((int)survivors.size() < k) return -1;
     std::vector<uint8_t> d((size_t)k * k, 0);
-    for (int r = 0; r < k; ++r) {
-        const int s = survivors[r];
-        if (s < k) d[(size_t)r * k + s] = 1;
-        else memcpy(&d[(size_t)r * k], P + (size_t)(s - k) * k, (size_t)k);
+    if (full) {
+        // module/rs.c:528-556: every row of the sub-matrix comes from the handle's n x k
+        // matrix `rs->m` (data rows included), and invert_mat's failure is ignored
+        for (int r = 0; r < k; ++r) memcpy(&d[(size_t)r * k], full + (size_t)survivors[r] * k, (size_t)k);
+        (void)gf_invert_rs(d.data(), k);
+    } else {
+        for (int r = 0; r < k; ++r) {
+            const int s = survivors[r];
+            if (s < k) d[(size_t)r * k + s] = 1;
+            else memcpy(&d[(size_t)r * k], P + (size_t)(s - k) * k, (size_t)k);
+        }
+        if (!gf_invert(d.data(), k)) return -1;  // cannot happen for the MDS flavours
     }
-    if (!gf_invert(d.data(), k)) return -1;  // cannot happen for the MDS flavours
     rows.assign((size_t)e * k, 0);
     for (int j = 0; j < e; ++j) memcpy(&rows[(size_t)j * k], &d[(size_t)lost[j] * k], (size_t)k);
     return e;

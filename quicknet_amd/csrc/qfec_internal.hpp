@@ -181,6 +181,9 @@ bool vandermonde_rows(int k, int m, std::vector<uint8_t>& out);  // module/fec.c
 
 // in-place GF inverse of a k x k matrix; false if singular
 bool gf_invert(uint8_t* a, int k);
+// the same with module/rs.c invert_mat's pivot order: on a singular matrix it returns false
+// and leaves `a` in the partially eliminated state rs.c then decodes with (rs.c:556)
+bool gf_invert_rs(uint8_t* a, int k);
 
 // one coefficient's 8-dword perm table
 void perm_entry(uint8_t c, uint32_t* out8);
@@ -188,8 +191,11 @@ void perm_entry(uint8_t c, uint32_t* out8);
 // decode record of one erasure pattern (see qfec_kernels.hip, "reconstruct").
 // group-order marks over n = k + m shards.  Returns e (>= 1), 0 if nothing is erased
 // or -1 if under-determined; on e >= 1 fills rows (e x k), survivors (k), lost (e).
+// `full` (n x k, nullable): module/rs.c's rs->m -- the sub-matrix is taken from it, data rows
+// included, and inverted with rs.c's semantics (a singular one decodes with its partial state)
 int decode_rows(const uint8_t* parity_rows, int k, int m, const uint8_t* marks_n,
-                std::vector<uint8_t>& rows, std::vector<int>& survivors, std::vector<int>& lost);
+                std::vector<uint8_t>& rows, std::vector<int>& survivors, std::vector<int>& lost,
+                const uint8_t* full = nullptr);
 
 // Record: [0] e, [surv_off + c] survivor shard id, [lost_off + j] erased data row,
 // [coff + j*k + c] byte offset of coefficient (j, c)'s perm table in the 256-entry table

@@ -162,7 +162,8 @@ __device__ __forceinline__ void pc_block_serve_k(const PcBell* bell, const uint8
 // then reads what the CPU wrote before the word.  Every iteration ends in the same place for
 // every lane, and the loop exits on idle or stop, so the grid always drains.
 __global__ void __launch_bounds__(256) k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st,
-                                                        uint32_t served, uint32_t gen, uint32_t trace) {
+                                                        uint32_t served, uint32_t gen, uint32_t trace,
+                                                        uint64_t idle_ticks) {
     __shared__ uint64_t s_bell;
     __shared__ uint32_t s_quit;
     const uint32_t t = threadIdx.x;
@@ -175,7 +176,7 @@ __global__ void __launch_bounds__(256) k_percall_server(PcBell* bell, const uint
             for (uint32_t it = 1;; ++it) {  // one load per poll; `stop` and the idle clock every 16th
                 b = ld_sys64(&bell->bell);
                 if ((uint32_t)b != served) break;
-                if ((it & 15u) == 0 && (ld_sys(&bell->stop) || wall_clock64() - t0 > kPcIdleTicks)) {
+                if ((it & 15u) == 0 && (ld_sys(&bell->stop) || wall_clock64() - t0 > idle_ticks)) {
                     quit = 1;
                     break;
                 }
@@ -212,8 +213,8 @@ __global__ void __launch_bounds__(256) k_percall_server(PcBell* bell, const uint
 }
 
 hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,
-                                 uint32_t gen, uint32_t trace, hipStream_t s) {
-    hipLaunchKernelGGL(k_percall_server, dim3(1), dim3(256), 0, s, bell, in, out, st, served, gen, trace);
+                                 uint32_t gen, uint32_t trace, uint64_t idle_ticks, hipStream_t s) {
+    hipLaunchKernelGGL(k_percall_server, dim3(1), dim3(256), 0, s, bell, in, out, st, served, gen, trace, idle_ticks);
     return hipGetLastError();
 }
 

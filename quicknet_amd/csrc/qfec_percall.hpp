@@ -36,11 +36,11 @@ hipError_t launch_percall(const PcArgs& a, hipStream_t s);
 // device memory it can map (fine-grained, host-visible), the block -- polling that word in its
 // own memory, not across PCIe -- computes the outputs into pinned host memory and stores the
 // request number into a completion word there, and the CPU spins on it.  Only posted writes
-// cross PCIe.  The block exits by itself after kPcIdleTicks without a request (or at once
+// cross PCIe.  The block exits by itself after `idle_ticks` without a request (or at once
 // when `stop` is set), so no grid outlives an idle caller, and the host relaunches it when
 // the next request finds it gone.
 constexpr int kPcMaxChunks = 256;             // 16-B columns per packet row (4 KiB)
-constexpr uint64_t kPcIdleTicks = 100000;     // 1 ms at the 100 MHz wall clock
+constexpr uint32_t kPcIdleUsDefault = 1000;   // qfec_tune "percall_idle_us": 1 ms (the wall clock ticks at 100 MHz)
 constexpr int kPcSrvMaxCoef = 64;             // the server serves k <= 16 and k * e <= 64 (lane c: coefficient c)
 constexpr int kPcTabWords = 8 * kPcSrvMaxCoef; // coefficient c's 5 table dwords at 8 c
 struct PcBell {                               // fine-grained device memory, written by the CPU
@@ -63,6 +63,6 @@ struct PcStatus {                             // coherent pinned host memory, wr
     uint64_t ts[4];
 };
 hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,
-                                 uint32_t gen, uint32_t trace, hipStream_t s);
+                                 uint32_t gen, uint32_t trace, uint64_t idle_ticks, hipStream_t s);
 
 }  // namespace qfec

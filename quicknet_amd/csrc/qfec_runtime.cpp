@@ -116,7 +116,7 @@ struct DevCtx {
         size_t tab_bytes = 0;
         uint32_t gen = 0;            // the last launch's generation
         bool launched = false;
-        unsigned long long calls = 0, launches = 0, relaunches = 0;
+        unsigned long long calls = 0, launches = 0, relaunches = 0, timeouts = 0;
         unsigned long long tr[5] = {0, 0, 0, 0, 0};  // QFEC_PERCALL_TRACE sums: invalidate, loads + compute, fence (ticks), host wait (ns), n
     } srv;
     int init_rc = QFEC_ENODEV;
@@ -222,6 +222,10 @@ int ensure_pc(DevCtx& c, size_t bytes) {
 // ---- the resident per-call server (qfec_percall.hpp)
 std::atomic<int> g_percall_resident{1};  // qfec_tune "percall_resident"
 std::atomic<int> g_percall_in{0};        // qfec_tune "percall_in": server inputs 0 in device memory, 1 in host memory
+std::atomic<int> g_percall_idle_us{(int)kPcIdleUsDefault};  // qfec_tune "percall_idle_us": the block's idle exit
+std::atomic<int> g_percall_timeout_us{2000000};  // qfec_tune "percall_timeout_us": give up spinning, wait instead
+std::atomic<int> g_percall_fault{0};     // qfec_tune "percall_fault" (tests): 1 = requests are never handed to a server
+std::atomic<int> g_percall_group{1};     // qfec_tune "percall_group": fec_encode computes a group's m rows at once
 constexpr size_t kPcSrvBytes = (size_t)kPcMaxCoef * kPcMaxChunks * 16;
 
 // true if [p, p + n) lies inside one readable, writable mapping of this process.  Fine-grained
@@ -253,10 +257,24 @@ int pc_server_setup(DevCtx& c) {
     DevCtx::PcServer& s = c.srv;
     if (s.usable) return s.usable > 0 ? QFEC_OK : QFEC_EHIP;
     s.usable = -1;
+    auto release = [&]() {  // nothing stays allocated on a device that keeps the launch-per-call path
+        if (s.stream) (void)hipStreamDestroy(s.stream);
+        if (s.bell) (void)hipFree(s.bell);
+        if (s.in) (void)hipFree(s.in);
+        if (s.h_in) (void)hipHostFree(s.h_in);
+        if (s.h_out) (void)hipHostFree(s.h_out);
+        if (s.h_st) (void)hipHostFree(s.h_st);
+        s.stream = nullptr;
+        s.bell = nullptr;
+        s.in = s.h_in = s.d_in = s.h_out = s.d_out = nullptr;
+        s.h_st = s.d_st = nullptr;
+        (void)hipGetLastError();
+    };
     auto fail = [&](hipError_t e, const char* what) {
         (void)hipGetLastError();
         fprintf(stderr, "[qfec] per-call server unavailable (%s: %s); launching per call\n", what,
                 hipGetErrorString(e));
+        release();
         return QFEC_EHIP;
     };
     hipError_t e;
@@ -279,6 +297,7 @@ int pc_server_setup(DevCtx& c) {
         return fail(e, "status word");
     if (!cpu_mapped(s.bell, sizeof(PcBell)) || !cpu_mapped(s.in, kPcSrvBytes)) {
         fprintf(stderr, "[qfec] per-call server unavailable (device memory not CPU-mapped); launching per call\n");
+        release();
         return QFEC_EHIP;
     }
     memset(s.bell, 0, sizeof(PcBell));
@@ -307,7 +326,11 @@ hipError_t pc_server_stop(DevCtx& c) {
     return e;
 }
 
-// one call through the server: QFEC_OK, or an error (the server then is stopped)
+// pc_server_call's answer when the request was not served: the caller runs it another way
+constexpr int kPcNotServed = 1;
+
+// one call through the server: QFEC_OK, kPcNotServed (the server is stopped and the request is
+// still the caller's to serve), or an error (the server then is stopped)
 int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, unsigned char* const* in,
                    unsigned char* const* out, int sz, size_t pitch) {
     DevCtx::PcServer& s = c.srv;
@@ -346,11 +369,16 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
         s.launched = true;
         ++s.launches;
         static const uint32_t trace = getenv("QFEC_PERCALL_TRACE") && atoi(getenv("QFEC_PERCALL_TRACE")) ? 1u : 0u;
-        return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, trace, s.stream);
+        const uint64_t idle = (uint64_t)std::max(0, g_percall_idle_us.load()) * 100u;  // 100 MHz wall clock
+        return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, trace, idle,
+                                     s.stream);
     };
     hipError_t he = hipSuccess;
-    if (!pc_server_alive(s)) he = launch();
+    const bool fault = g_percall_fault.load() != 0;  // test hook: as if no server ever got a CU
+    if (fault) (void)pc_server_stop(c);
+    else if (!pc_server_alive(s)) he = launch();
     const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = std::chrono::microseconds(g_percall_timeout_us.load());
     for (uint32_t it = 1; he == hipSuccess; ++it) {
         if (__atomic_load_n(&s.h_st->done, __ATOMIC_ACQUIRE) == req) {
             ++s.calls;
@@ -365,17 +393,27 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
             return QFEC_OK;
         }
         __builtin_ia32_pause();
-        if ((it & 63) == 0 && __atomic_load_n(&s.h_st->state, __ATOMIC_ACQUIRE) == (s.gen << 1)) {
+        if (!fault && (it & 63) == 0 && __atomic_load_n(&s.h_st->state, __ATOMIC_ACQUIRE) == (s.gen << 1)) {
             // the server went idle and exited just before the request arrived: its exit is
             // published after its last completion, so the request is not served -- relaunch
             if (__atomic_load_n(&s.h_st->done, __ATOMIC_ACQUIRE) == req) continue;
             ++s.relaunches;
             he = launch();
         }
-        if ((it & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-            set_error("per-call server: request %u not served within 2 s", req);
-            (void)pc_server_stop(c);
-            return QFEC_EHIP;
+        if ((it & 63) == 0 && std::chrono::steady_clock::now() - t0 > limit) {
+            // not served in time: the block may be waiting for a CU that other streams hold.
+            // Stop it and wait for it, like the launch path waits for its kernel: once it runs
+            // it serves the pending request before it sees `stop`.  A request it never saw is
+            // handed back to the caller, which launches it on its own.
+            ++s.timeouts;
+            const hipError_t se = pc_server_stop(c);
+            if (se != hipSuccess) return hip_fail(se, "per-call server: stop after a timeout");
+            if (__atomic_load_n(&s.h_st->done, __ATOMIC_ACQUIRE) == req) {
+                ++s.calls;
+                for (int j = 0; j < e; ++j) memcpy(out[j], s.h_out + (size_t)j * pitch, (size_t)sz);
+                return QFEC_OK;
+            }
+            return kPcNotServed;
         }
     }
     (void)pc_server_stop(c);
@@ -492,6 +530,7 @@ struct qfec_code {
     int quirk = 0;  // module/rs.c column-0 zero-coefficient behaviour
     std::mutex mu;
     std::vector<uint8_t> rows;  // m x k
+    std::vector<uint8_t> full;  // n x k decode matrix of a reed_solomon handle (rs->m), else empty
     uint64_t version = 0;
     std::map<int, DevTables> dev;
     // host-side decode cache: pattern key -> (record words); for explicit mode
@@ -524,6 +563,9 @@ void free_code(qfec_code* c) {
     if (have) (void)hipSetDevice(prev);
     delete c;
 }
+
+// module/rs.c decodes from rs->m (rs.c:505, 536-548); other codes from their parity rows
+const uint8_t* full_of(const qfec_code* c) { return c->full.empty() ? nullptr : c->full.data(); }
 
 void enc_table_host(const qfec_code* c, std::vector<uint32_t>& t) {
     const int k = c->k, m = c->m;
@@ -578,7 +620,7 @@ int record_for_key(const qfec_code* c, uint64_t key, std::vector<uint32_t>& rec)
     for (int j = 0; j < m; ++j) marks[k + j] = ((key >> (k + j)) & 1) ? 0 : 1;
     std::vector<uint8_t> rows;
     std::vector<int> surv, lost;
-    const int e = decode_rows(c->rows.data(), k, m, marks.data(), rows, surv, lost);
+    const int e = decode_rows(c->rows.data(), k, m, marks.data(), rows, surv, lost, full_of(c));
     if (e <= 0) return -1;
     const RecordLayout L = record_layout(k, m);
     rec.assign(L.words(e, k), 0);
@@ -756,7 +798,7 @@ int host_records(qfec_code* c, const uint8_t* marks, long long groups, std::vect
             for (int j : chosen) gm[k + j] = 0;
             std::vector<uint8_t> rows;
             std::vector<int> surv, lost;
-            const int ee = decode_rows(c->rows.data(), k, m, gm.data(), rows, surv, lost);
+            const int ee = decode_rows(c->rows.data(), k, m, gm.data(), rows, surv, lost, full_of(c));
             if (ee <= 0) { grec[g] = QFEC_REC_FAIL; ++*nfail; continue; }
             const RecordLayout L = record_layout(k, m);
             std::vector<uint32_t> one(L.words(ee, k));
@@ -863,6 +905,24 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
     if (!strcmp(key, "percall_spin") && (value == 0 || value == 1)) { g_percall_spin = value; return QFEC_OK; }
     if (!strcmp(key, "percall_in") && (value == 0 || value == 1)) { g_percall_in = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_group") && (value == 0 || value == 1)) { g_percall_group = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_fault") && (value == 0 || value == 1)) { g_percall_fault = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_timeout_us") && value >= 0) { g_percall_timeout_us = value; return QFEC_OK; }
+    if (!strcmp(key, "percall_idle_us") && value >= 0 && value <= 1000000) {
+        // a running block keeps the idle time it was launched with: stop it, the next call
+        // launches one with the new value
+        g_percall_idle_us = value;
+        for (DevCtx& c : g_ctx) {
+            std::lock_guard<std::mutex> lk(c.mu);
+            if (c.srv.usable <= 0 || !c.srv.launched) continue;
+            int prev = 0;
+            (void)hipGetDevice(&prev);
+            (void)hipSetDevice(c.device);
+            (void)pc_server_stop(c);
+            (void)hipSetDevice(prev);
+        }
+        return QFEC_OK;
+    }
     if (!strcmp(key, "percall_resident") && (value == 0 || value == 1)) {
         g_percall_resident = value;
         if (!value)
@@ -894,6 +954,31 @@ int qfec_percall_stats(unsigned long long out[5]) {
     out[3] = s.usable > 0 && pc_server_alive(s);
     out[4] = (unsigned long long)(long long)s.usable;
     return QFEC_OK;
+}
+
+static std::atomic<unsigned long long> g_group_hits{0}, g_group_misses{0};  // fec_encode's group cache (all handles)
+
+int qfec_percall_counters(unsigned long long* out, int n) {
+    if (!out || n < 0) return QFEC_EINVAL;
+    unsigned long long v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    DevCtx* ctx = nullptr;
+    int rc = current_ctx(&ctx);
+    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        const DevCtx::PcServer& s = ctx->srv;
+        v[0] = s.calls;
+        v[1] = s.launches;
+        v[2] = s.relaunches;
+        v[3] = s.usable > 0 && pc_server_alive(s);
+        v[4] = (unsigned long long)(long long)s.usable;
+        v[5] = s.timeouts;
+    }
+    v[6] = g_group_hits.load();
+    v[7] = g_group_misses.load();
+    v[8] = (unsigned long long)g_percall_idle_us.load();
+    for (int i = 0; i < n && i < 9; ++i) out[i] = v[i];
+    return std::min(n, 9);
 }
 
 qfec_code* qfec_code_new(int flavour, int k, int m) {
@@ -1180,7 +1265,7 @@ int qfec_decode_rows(const qfec_code* code, const unsigned char* marks_n, unsign
     if (!code || !marks_n) return QFEC_EINVAL;
     std::vector<uint8_t> rows;
     std::vector<int> surv, lost;
-    const int e = decode_rows(code->rows.data(), code->k, code->m, marks_n, rows, surv, lost);
+    const int e = decode_rows(code->rows.data(), code->k, code->m, marks_n, rows, surv, lost, full_of(code));
     if (e > 0) {
         if (rows_out) memcpy(rows_out, rows.data(), rows.size());
         if (survivors_out) memcpy(survivors_out, surv.data(), surv.size() * sizeof(int));
@@ -1928,12 +2013,17 @@ struct rs_handle {
 std::atomic<int> g_rs_errno{0};
 std::once_flag g_rs_init_once;
 
-// pick up edits callers made to the public parity matrix since the last call
+// pick up edits callers made to the public matrices since the last call: encode reads
+// `parity` (rs.c:583), reconstruct reads `m` (rs.c:505, 536-548); the two are separate copies
 void sync_rows(rs_handle* h) {
     qfec_code* c = h->code;
     std::lock_guard<std::mutex> lk(c->mu);
     if (memcmp(c->rows.data(), h->pub.parity, c->rows.size()) != 0) {
         memcpy(c->rows.data(), h->pub.parity, c->rows.size());
+        ++c->version;
+    }
+    if (memcmp(c->full.data(), h->pub.m, c->full.size()) != 0) {
+        memcpy(c->full.data(), h->pub.m, c->full.size());
         ++c->version;
     }
 }
@@ -1968,6 +2058,7 @@ reed_solomon* reed_solomon_new(int data_shards, int parity_shards) {
         memcpy(h->pub.parity, rows.data(), rows.size());
         h->code = make_code(k, m, std::move(rows), 1);
         if (!h->code) { err = 5; break; }
+        h->code->full.assign(h->pub.m, h->pub.m + (size_t)n * k);
         g_rs_errno = 0;
         return &h->pub;
     } while (0);
@@ -2151,6 +2242,17 @@ struct fec_handle {
         std::vector<uint32_t> tab;
     };
     std::unordered_map<uint64_t, std::shared_ptr<const Dec>> dec;  // keyed by a hash of the shuffled index[]
+    // fec_encode's group cache.  The network layer asks for a group's check packets one index at
+    // a time over the same inputs (get_fec_encoded_pkt for ik = k .. n-1, network/NetFecCodec.cpp:
+    // 133-166, network/FecCodecBuf.cpp:137-156).  The first such call computes all n - k rows in
+    // one request; the next ones are served from here when the src[] pointers, sz and every input
+    // byte (kept as a host copy, compared in full) are unchanged.  Any difference recomputes.
+    std::vector<uint32_t> enc_all;  // [n - k][k] perm tables of every parity row
+    std::mutex grp_mu;              // held across a group's compute: one computation per group
+    std::vector<unsigned char*> grp_src;
+    int grp_sz = -1;
+    std::vector<uint8_t> grp_in;    // k x sz: the inputs the rows were computed from
+    std::vector<uint8_t> grp_out;   // (n - k) x sz
 };
 constexpr size_t kFecDecCacheMax = 4096;
 
@@ -2166,8 +2268,11 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
     if (!dev && k * e <= kPcMaxCoef && g_percall_fast.load() && !is_device_ptr(out[0])) {
         // the resident server (packets of up to 4 KiB)
         if (pitch <= (size_t)kPcMaxChunks * 16 && k <= 16 && k * e <= kPcSrvMaxCoef && g_percall_resident.load() &&
-            pc_server_setup(*ctx) == QFEC_OK)
-            return pc_server_call(*ctx, tab, k, e, in, out, sz, pitch);
+            pc_server_setup(*ctx) == QFEC_OK) {
+            rc = pc_server_call(*ctx, tab, k, e, in, out, sz, pitch);
+            if (rc != kPcNotServed) return rc;
+            // not served within percall_timeout_us: the launch path below serves it
+        }
         // host packets: CPU staging into mapped pinned memory, one launch, one synchronise
         if ((rc = ensure_pc(*ctx, (size_t)(k + e) * pitch))) return rc;
         for (int c = 0; c < k; ++c) memcpy(ctx->h_pc + (size_t)c * pitch, in[c], (size_t)sz);
@@ -2295,6 +2400,49 @@ void fec_encode(void* code, unsigned char** src, unsigned char* dst, int index, 
         return;
     }
     if (sz <= 0) return;
+    const int m = h->n - k;
+    if (g_percall_group.load() && m > 1 && k <= 16 && k * m <= kPcSrvMaxCoef &&
+        round_up((size_t)sz, 16) <= (size_t)kPcMaxChunks * 16) {
+        // the whole group at once (see fec_handle::grp_*); host packets only
+        if (!is_device_ptr(dst) && !is_device_ptr(src[0])) {  // the kinds apply_rows checks
+            std::lock_guard<std::mutex> gl(h->grp_mu);
+            const size_t szz = (size_t)sz;
+            bool hit = h->grp_sz == sz && std::equal(src, src + k, h->grp_src.begin());
+            for (int i = 0; i < k && hit; ++i) hit = !memcmp(h->grp_in.data() + (size_t)i * szz, src[i], szz);
+            if (!hit) {
+                h->grp_sz = -1;
+                h->grp_src.assign(src, src + k);
+                h->grp_in.resize((size_t)k * szz);
+                h->grp_out.resize((size_t)m * szz);
+                for (int i = 0; i < k; ++i) memcpy(h->grp_in.data() + (size_t)i * szz, src[i], szz);
+                {
+                    std::lock_guard<std::mutex> lk(h->mu);
+                    if (h->enc_all.empty()) {
+                        h->enc_all.resize((size_t)m * k * QFEC_TAB_STRIDE);
+                        for (int r = 0; r < m; ++r)
+                            for (int i = 0; i < k; ++i)
+                                perm_entry(h->full[(size_t)(k + r) * k + i], &h->enc_all[((size_t)r * k + i) * QFEC_TAB_STRIDE]);
+                    }
+                }
+                unsigned char* outs[256];
+                for (int r = 0; r < m; ++r) outs[r] = h->grp_out.data() + (size_t)r * szz;
+                // the copy, not the caller's buffers: the rows belong to the bytes just compared
+                unsigned char* ins[256];
+                for (int i = 0; i < k; ++i) ins[i] = h->grp_in.data() + (size_t)i * szz;
+                const int rc = apply_rows(h->enc_all, k, m, ins, outs, sz);
+                if (rc) {
+                    fprintf(stderr, "[qfec] fec_encode: %s\n", qfec_last_error());
+                    return;
+                }
+                h->grp_sz = sz;
+                ++g_group_misses;
+            } else {
+                ++g_group_hits;
+            }
+            memcpy(dst, h->grp_out.data() + (size_t)(index - k) * szz, szz);
+            return;
+        }
+    }
     const std::vector<uint32_t>* tab = nullptr;
     {
         std::lock_guard<std::mutex> lk(h->mu);

@@ -1883,8 +1883,9 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
     }
     if constexpr (FP != 0) {
         // frames the FEC header rejected were not read by the passes: their RecvPacket checksum,
-        // one row at a time over the wave (only malformed rows come here)
-        uint32_t chk = (uint32_t)__ballot(lane < N && fst == 0 && !okh) & rowmask;
+        // one row at a time over the wave (only malformed rows come here).  A bad cmd is judged
+        // after the checksum, as RecvPacket does (ProtocolBasic.cpp:167-196), so those rows too.
+        uint32_t chk = (uint32_t)__ballot(lane < N && (fst == 0 || fst == 3) && !okh) & rowmask;
         while (chk) {
             const int r = __builtin_ctz(chk);
             chk &= chk - 1;
@@ -1897,7 +1898,8 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
             s = wave_total(s);
             if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (lane_of(v_fs, r) >> 24)) fbad |= 1u << r;
         }
-        if (fr.status && lane < N) fr.status[g * N + lane] = fst ? fst : ((fbad >> lane) & 1u) ? 2 : 0;
+        if (fr.status && lane < N)
+            fr.status[g * N + lane] = fst == 1 || fst == 4 ? fst : ((fbad >> lane) & 1u) ? 2 : fst;
     }
     if (lane < K) {
         a.status[g * K + lane] = st;

@@ -233,3 +233,38 @@ def test_fec_decode_shuffle_and_pattern_cache(oracle):
             where = {v: i for i, v in enumerate(idx)}
             assert [((p - base) // 4) for p in ptrs] == [where[v] for v in ia], (call, idx)
     L.fec_free(h)
+
+
+@pytest.mark.parametrize("name", ["p42", "m42", "s42", "s103", "m103w", "m164w"])
+def test_rs_edits_decode_rows_host(oracle, golden, name):
+    """The host half of reed_solomon_reconstruct on a handle whose public `m` / `parity` were
+    edited (rs_edits.npz, produced by the reference's rs.c): qfec_rs_code picks the edits up, and
+    every pattern's decode rows are rows `lost` of rs.c's invert_mat over rs->m's survivor rows
+    -- the partial elimination state when the sub-matrix is singular (rs.c:505-556).  CPU only:
+    the kernels that apply these rows are held to the fixture's bytes in test_gpu_parity.py."""
+    z = golden("rs_edits.npz")
+    k, m, B = (int(x) for x in z[f"shape_{name}"])
+    rs = qa.ReedSolomon(k, m)
+    rs.parity[:] = z[f"parity_{name}"]
+    rs.m_matrix[:] = z[f"m_{name}"]
+    code = rs.code()
+    assert np.array_equal(code.rows, z[f"parity_{name}"])
+    full = z[f"m_{name}"]
+    singular = 0
+    for mask in np.unique(z[f"marks_{name}"], axis=0)[:600]:
+        e, rows, surv, lost = code.decode_rows(mask)
+        lost_ref = [i for i in range(k) if mask[i]]
+        avail = [k + j for j in range(m) if not mask[k + j]]
+        if not lost_ref:
+            assert e == 0
+            continue
+        if len(avail) < len(lost_ref):
+            assert e == -1
+            continue
+        surv_ref = [i for i in range(k) if not mask[i]] + avail[:len(lost_ref)]
+        assert e == len(lost_ref) and list(surv) == surv_ref and list(lost) == lost_ref
+        rc, inv = oracle.invert_partial(full[surv_ref])
+        singular += rc != 0
+        assert np.array_equal(rows, inv[lost_ref]), mask
+    assert singular > 0 or name in ("p42", "m42")  # every other case has singular patterns by design
+    rs.close()

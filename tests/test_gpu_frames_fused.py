@@ -133,7 +133,7 @@ def test_unpack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session):
         if rng.random() < 0.5:
             j = int(rng.integers(0, n))
             if fl[g, j] > P + 13:
-                kind = int(rng.integers(0, 6))
+                kind = int(rng.integers(0, 7))
                 kinds[(g, j)] = kind
                 x = int(f[g, j, 0]) ^ GMASK ^ 0x5A
                 w = f[g, j, :fl[g, j]] ^ np.uint8(x)  # un-XORed frame (byte 0 garbage)
@@ -144,6 +144,11 @@ def test_unpack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session):
                     w[2] = 0x11
                     s_ = int(w[2:].astype(np.int64).sum())
                     w[1] = (~((s_ >> 16) + (s_ & 0xFFFF))) & 0xFF
+                    f[g, j, 1:fl[g, j]] = w[1:] ^ np.uint8(x)
+                elif kind == 6:  # cmd without 0xA0 AND a bad checksum: RecvPacket says checksum (2)
+                    w[2] = 0x11
+                    s_ = int(w[2:].astype(np.int64).sum())
+                    w[1] = ((~((s_ >> 16) + (s_ & 0xFFFF))) & 0xFF) ^ 0x01
                     f[g, j, 1:fl[g, j]] = w[1:] ^ np.uint8(x)
                 elif kind == 2:  # short
                     fl[g, j] = P - 1
@@ -208,7 +213,10 @@ def test_unpack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session):
             ok = fst == 0
             assert np.array_equal(cho[ok], ch.reshape(G, n, 2)[ok])
     if G >= 100:
-        assert set(kinds.values()) >= {0, 1, 2, 3, 4, 5}
+        assert set(kinds.values()) >= {0, 1, 2, 3, 4, 5, 6}
+    for (g, j), kd in kinds.items():  # both checks failing: the checksum verdict, as RecvPacket
+        if kd == 6:
+            assert st_ref[g, j] == 2
     # recoverable groups: every payload back
     (sh, status, psize, rx, fst, _) = outs[0]
     assert (status >= 0).sum() > G * k // 2

@@ -253,7 +253,11 @@ def test_per_packet_paths_vs_oracle(oracle, fast, spin, resident, k, n, sz):
         served = after["calls"] - before["calls"]
         if fast and resident and sz <= 4096 and after["usable"] > 0:
             lost = min(n - k, k)
-            want = (n - k) * 2 * (k <= 16) + (1 if lost and k <= 16 and k * lost <= 64 else 0)
+            # percall_group: one request computes a group's n - k rows, and both encode loops use
+            # the same inputs, so every later index is served from the handle's group copy
+            grouped = n - k > 1 and k <= 16 and k * (n - k) <= 64
+            enc = 1 if grouped else (n - k) * 2 * (k <= 16)
+            want = enc + (1 if lost and k <= 16 and k * lost <= 64 else 0)
             assert served == want, served  # every encode (checker + decode input) + the decode
         else:
             assert served == 0
@@ -403,6 +407,192 @@ def test_percall_server_idle_exit_and_relaunch(oracle):
     assert not qa.percall_stats()["running"]
     qa.tune("percall_resident", 1)
     call(400)
+
+
+def test_fec_encode_group_cache(oracle):
+    """fec_encode's group cache (percall_group 1): the n - k calls of one group (the way
+    get_fec_encoded_pkt asks for them, network/NetFecCodec.cpp:133-166) cost one request; inputs
+    mutated between the calls, reused pointers with new contents, another sz and interleaved
+    handles all get the rows of the bytes they pass, checked against the oracle every time."""
+    k, n, sz = 10, 13, 1028
+    fa, fb = qa.FecParms(k, n), qa.FecParms(k, n)
+    expect = _encode_checker(oracle, fa, k, n)
+    rng = np.random.default_rng(31)
+
+    def enc(fp, data, idx, size=sz):
+        dst = np.full(size, 0xEE, np.uint8)
+        fp.encode(data, dst, idx, size)
+        assert np.array_equal(dst, expect(data[:, :size], idx)), (idx, size)
+
+    def counters():
+        c = qa.percall_counters()
+        return c["group_hits"], c["group_misses"]
+
+    h0, m0 = counters()
+    data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    for idx in range(k, n):
+        enc(fa, data, idx)
+    h1, m1 = counters()
+    assert (h1 - h0, m1 - m0) == (n - k - 1, 1)
+    # a byte of one input changed between two calls of the group: recomputed
+    data[3, 500] ^= 0x5A
+    enc(fa, data, k + 1)
+    # the same buffers, wholly new contents (the pointers repeat): recomputed
+    data[:] = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    enc(fa, data, k + 2)
+    enc(fa, data, k)
+    # a shorter sz over the same pointers: recomputed
+    enc(fa, data, k + 1, size=700)
+    enc(fa, data, k + 2, size=700)
+    h2, m2 = counters()
+    assert (h2 - h1, m2 - m1) == (2, 3)
+    # two handles interleaved, each with its own group
+    da = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    db = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    for idx in range(k, n):
+        enc(fa, da, idx)
+        enc(fb, db, idx)
+    h3, m3 = counters()
+    assert (h3 - h2, m3 - m2) == (2 * (n - k - 1), 2)
+    # the index < k copy and the index >= n no-op stay as the reference has them
+    dst = np.zeros(sz, np.uint8)
+    fa.encode(da, dst, 4, sz)
+    assert np.array_equal(dst, da[4])
+    dst[:] = 0x33
+    fa.encode(da, dst, n, sz)
+    assert (dst == 0x33).all()
+    # percall_group 0: one request per index, same bytes
+    qa.tune("percall_group", 0)
+    try:
+        for idx in range(k, n):
+            enc(fa, da, idx)
+        assert counters() == (h3, m3)
+    finally:
+        qa.tune("percall_group", 1)
+
+
+def test_fec_encode_group_cache_threads(oracle):
+    """Four threads encoding groups through ONE handle: each group is computed under the handle's
+    group lock, so a thread never receives rows of another thread's inputs."""
+    import threading
+    k, n, sz = 10, 13, 1028
+    fp = qa.FecParms(k, n)
+    expect = _encode_checker(oracle, fp, k, n)
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(4100 + t)
+        try:
+            for g in range(60):
+                data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+                for idx in range(k, n):
+                    dst = np.zeros(sz, np.uint8)
+                    fp.encode(data, dst, idx, sz)
+                    if not np.array_equal(dst, expect(data, idx)):
+                        errors.append((t, g, idx))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(("raised", t, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errors, errors[:5]
+
+
+def test_percall_timeout_branch(oracle):
+    """a request the server does not serve within percall_timeout_us is not lost.  With
+    the limit at 0 every call stops the server and waits for it (it serves the pending request on
+    its way out); with percall_fault 1 no server ever takes the request, and the call runs it through
+    one launch.  Every output is the oracle's, encodes and decodes alike."""
+    k, n, sz = 10, 13, 1028
+    fp = qa.FecParms(k, n)
+    full = fp.matrix
+    expect = _encode_checker(oracle, fp, k, n)
+    rng = np.random.default_rng(55)
+    qa.tune("percall_resident", 1)
+    qa.tune("percall_group", 0)
+    c0 = qa.percall_counters()
+    if c0["usable"] < 0:
+        pytest.skip("device memory not CPU-mapped on this box: the launch-per-call path serves")
+    try:
+        for fault in (0, 1):
+            qa.tune("percall_timeout_us", 0)
+            qa.tune("percall_fault", fault)
+            before = qa.percall_counters()
+            for call in range(60):
+                data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+                idx = k + call % (n - k)
+                dst = np.zeros(sz, np.uint8)
+                fp.encode(data, dst, idx, sz)
+                assert np.array_equal(dst, expect(data, idx)), (fault, call)
+                if call % 10 == 0:
+                    coded = np.concatenate([data, np.stack([expect(data, j) for j in range(k, n)])])
+                    keep = list(range(3, n))
+                    rc, pk, ix = fp.decode(coded[keep], keep, sz)
+                    rc2, pk2, _ = oracle.fec_decode(k, n, full, coded[keep], keep)
+                    assert rc == rc2 == 0 and np.array_equal(pk, pk2) and np.array_equal(pk, data)
+            after = qa.percall_counters()
+            assert after["timeouts"] - before["timeouts"] >= (66 if fault else 1), after
+            if fault:
+                assert after["calls"] == before["calls"]  # no server ever served one
+    finally:
+        qa.tune("percall_fault", 0)
+        qa.tune("percall_timeout_us", 2000000)
+        qa.tune("percall_group", 1)
+    data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    dst = np.zeros(sz, np.uint8)
+    fp.encode(data, dst, k, sz)  # and the server serves again
+    assert np.array_equal(dst, expect(data, k))
+
+
+def test_percall_idle_knob_bounds_device_sync(oracle):
+    """The resident block's footprint (qfec.h): a hipDeviceSynchronize issued
+    right after a call waits for the block's idle exit, at most percall_idle_us (1 ms by default) --
+    measured here at <= 2 ms -- and percall_idle_us 0 makes the block exit right after each call."""
+    import time
+
+    import torch
+    k, n, sz = 10, 13, 1028
+    fp = qa.FecParms(k, n)
+    expect = _encode_checker(oracle, fp, k, n)
+    rng = np.random.default_rng(808)
+    qa.tune("percall_resident", 1)
+
+    def call():
+        data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+        dst = np.zeros(sz, np.uint8)
+        fp.encode(data, dst, k, sz)
+        assert np.array_equal(dst, expect(data, k))
+
+    call()
+    if qa.percall_counters()["usable"] < 0:
+        pytest.skip("device memory not CPU-mapped on this box: the launch-per-call path serves")
+    torch.cuda.synchronize()
+    waits = []
+    for _ in range(7):
+        call()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        waits.append(time.perf_counter() - t0)
+    assert qa.percall_counters()["idle_us"] == 1000
+    assert sorted(waits)[3] <= 2e-3, waits
+    qa.tune("percall_idle_us", 0)
+    try:
+        l0 = qa.percall_counters()["launches"]
+        zero = []
+        for _ in range(7):
+            call()
+            t0 = time.perf_counter()
+            torch.cuda.synchronize()
+            zero.append(time.perf_counter() - t0)
+        c = qa.percall_counters()
+        assert c["idle_us"] == 0 and c["launches"] - l0 >= 6  # a launch per call
+        assert sorted(zero)[3] <= 0.5e-3, zero
+    finally:
+        qa.tune("percall_idle_us", 1000)
+    call()
 
 
 def _gf_row(oracle, c, row):

@@ -440,3 +440,64 @@ def test_device_pointer_abi_paths():
     hd = data.cpu().numpy()
     qa.ReedSolomon(k, m).encode(hd, ref, B)
     assert np.array_equal(par.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("path", ["abi", "abi_dev", "batched"])
+@pytest.mark.parametrize("name", ["p42", "m42", "s42", "s103", "m103w", "m164w"])
+def test_rs_edits_vs_golden(golden, name, path):
+    """reed_solomon handles whose public matrices the caller edited, byte for byte and return
+    code for return code against what the reference's rs.c produced (rs_edits.npz): encode
+    reads `parity`, reconstruct decodes from `m` (data rows included) and, where an edit made a
+    pattern's sub-matrix singular, with invert_mat's partial state and err unchanged
+    (rs.c:505-556).  Paths: the ABI on host pointers, the ABI on device pointers, and the
+    batched device API on the handle's code (qfec_rs_code)."""
+    import ctypes as C
+    from test_oracle_golden import rs_edit_case, rs_edit_match
+    z = golden("rs_edits.npz")
+    k, m, B, G, data0, par, marks = rs_edit_case(z, name)
+    n = k + m
+    rs = qa.ReedSolomon(k, m)
+    rs.parity[:] = z[f"parity_{name}"]
+    rs.m_matrix[:] = z[f"m_{name}"]
+    L = qa.lib()
+    enc = par is None
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+    if path == "abi":
+        if enc:
+            par = np.full((G, m, B), 0x5A, np.uint8)
+            assert rs.encode(data0, par, B) == 0
+            assert rs_edit_match(z, f"enc_{name}", par)
+        rc = rs.reconstruct(d, par.copy(), marks, B)
+        out = d
+    elif path == "abi_dev":
+        dd, dp = to_dev(data0.copy()), to_dev(par if not enc else np.full((G, m, B), 0x5A, np.uint8))
+        ptrs = (C.c_void_p * (G * n))(*([dd.data_ptr() + i * B for i in range(G * k)] +
+                                         [dp.data_ptr() + i * B for i in range(G * m)]))
+        if enc:
+            assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == 0
+            torch.cuda.synchronize()
+            assert rs_edit_match(z, f"enc_{name}", dp.cpu().numpy())
+        dd.copy_(to_dev(d))
+        dmarks = to_dev(marks)
+        rc = L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(dmarks.data_ptr()), G * n, B)
+        torch.cuda.synchronize()
+        out = dd.cpu().numpy()
+    else:
+        code = rs.code()
+        pitch = round16(B)
+        if enc:
+            dp = to_dev(np.full((G, m, pitch), 0x5A, np.uint8))
+            code.encode(to_dev(padded(data0, pitch)), dp, B)
+            torch.cuda.synchronize()
+            par = np.ascontiguousarray(dp.cpu().numpy()[..., :B])
+            assert rs_edit_match(z, f"enc_{name}", par)
+        dd = to_dev(padded(d, pitch))
+        failed = torch.zeros(1, dtype=torch.int32, device=DEV)
+        code.reconstruct(dd, to_dev(padded(par, pitch)), to_dev(marks), B, failed)
+        torch.cuda.synchronize()
+        out = dd.cpu().numpy()[..., :B]
+        rc = -1 if int(failed.item()) else 0
+    assert rc == z[f"rc_{name}"][0]
+    assert rs_edit_match(z, f"out_{name}", out)
+    rs.close()

@@ -201,3 +201,52 @@ def test_wire_pack_unpack(oracle, golden, k, n, checksum):
                         if ik < k:
                             off, sz = oracle.dec_src(body, 2068, cs)
                             assert [off, sz] == list(srcinfo[g, ik]) or (off == -1 and srcinfo[g, ik, 0] == -1)
+
+
+RS_EDIT_CASES = ["p42", "m42", "s42", "s103", "m103w", "m164w"]
+
+
+def rs_edit_case(z, name):
+    """Inputs of one rs_edits.npz case (oracle/gen_golden.py gen_rs_edits): the handle's edited
+    matrices, the data, and the parity the reconstruct reads (None: the case encodes it first
+    with the edited parity rows, over 0x5A)."""
+    k, m, B = (int(x) for x in z[f"shape_{name}"])
+    gm = z[f"marks_{name}"]
+    G = gm.shape[0]
+    seed = int(z[f"seed_{name}"][0])
+    data0 = synth_bytes(seed, G * k * B).reshape(G, k, B)
+    par = None if f"enc_{name}" in z.files else synth_bytes(seed ^ 0xFFFF, G * m * B).reshape(G, m, B)
+    marks = np.concatenate([gm[:, :k].reshape(-1), gm[:, k:].reshape(-1)]).astype(np.uint8)
+    return k, m, B, G, data0, par, marks
+
+
+def rs_edit_match(z, key, arr):
+    """The fixture holds small outputs whole and large ones as sha256 digests."""
+    ref = z[key]
+    a = np.ascontiguousarray(arr)
+    if ref.dtype == np.uint8 and ref.ndim == 1 and ref.size == 32 and a.size != 32:
+        return hashlib.sha256(a.tobytes()).digest() == ref.tobytes()
+    return np.array_equal(a.reshape(ref.shape), ref)
+
+
+@pytest.mark.parametrize("name", RS_EDIT_CASES)
+def test_rs_edits(oracle, golden, name):
+    """reed_solomon handles with an edited public parity / m (singular sub-matrices included):
+    the oracle's rs.c restatement decodes from rs->m with invert_mat's partial state, as the
+    reference did when it produced the fixture."""
+    z = golden("rs_edits.npz")
+    k, m, B, G, data0, par, marks = rs_edit_case(z, name)
+    if par is None:
+        par = np.full((G, m, B), 0x5A, np.uint8)
+        oracle.rs_encode(z[f"parity_{name}"], data0, par, B)
+        assert rs_edit_match(z, f"enc_{name}", par)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+    rc = oracle.rs_reconstruct_full(z[f"m_{name}"], d, par.copy(), marks, B)
+    assert rc == z[f"rc_{name}"][0]
+    assert rs_edit_match(z, f"out_{name}", d)
+    if name == "m42":  # the edited data row of m matters: unit data rows decode differently
+        d2 = data0.copy()
+        d2.reshape(G * k, B)[marks[: G * k] == 1] = 0x5A
+        assert oracle.rs_reconstruct(z[f"m_{name}"][k:], d2, par.copy(), marks, B) == rc
+        assert not rs_edit_match(z, f"out_{name}", d2)
