@@ -769,8 +769,13 @@ def zfec_leg(timeout=240):
     64 sender sessions x 2 000 x 1 KiB payloads, RS(10,13), one send flush whose C callback hands
     every datagram it keeps to a receiving context (1 of 13 dropped per group), then one receive
     flush whose C callback folds every delivered payload; the best of reps 1-3 after a warm-up rep
-    (tools/zfec_rate.py, its own process).  Rates count payload bytes over each flush's wall time;
-    the reference's own per-packet pipeline on one core is cpu_baseline.wire.  Parity of the
+    (tools/zfec_rate.py, its own process).  send_gibs / recv_gibs count payload bytes over each
+    flush's wall time.  send_e2e_gibs / recv_e2e_gibs (interleaved reps, field `e2e`) also count the
+    per-packet input calls, made from C loops: pack_input for every payload + the send flush, and
+    unpack_input for every kept datagram + the receive flush -- the like-for-like figures beside
+    the reference's own per-packet pipeline on one core (cpu_baseline.wire), which includes all of
+    its per-packet work.  `verified`: delivery count, bytes and word sum, plus a byte-for-byte check
+    of every 61st delivery against the payload sent under its source index.  Parity of the
     control flow is unpinned (NetFecCodec.cpp does not build here; tests/test_gpu_zfec.py)."""
     try:
         r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "zfec_rate.py"), "--json"], capture_output=True,

@@ -17,6 +17,14 @@
  *     packet, whose index value is kept); returns 1 on a shuffle conflict, an index >= n
  *     or a singular matrix, else 0                                    (fec.c:738-862)
  *   - a negative index (undefined behaviour in the reference) is rejected with 1.
+ *
+ * Device footprint: host packets of up to 4 KiB (k <= 16, k * rows <= 64) are served by a
+ * resident one-block kernel on the library's own stream.  After the last call that block stays
+ * on the device for at most percall_idle_us (qfec_tune, default 1 ms) and then exits by itself,
+ * so a hipDeviceSynchronize() issued right after a call may wait up to that long;
+ * qfec_tune("percall_idle_us", 0) makes it exit after every call.
+ * fec_encode of a parity index computes the group's n - k rows at once and serves the group's
+ * other indices from a per-handle copy while src[], sz and every input byte are unchanged.
  */
 #ifndef QFEC_FEC_H
 #define QFEC_FEC_H

@@ -62,7 +62,8 @@ struct ReconArgs {
     int k, m;
     int surv_off, lost_off, hdr;
     int coff;                 // record word of the coefficient-table byte offsets (RecordLayout::coff)
-    const uint32_t* t256;     // [256][QFEC_TAB_STRIDE] perm tables of every coefficient value (compact mode)
+    const uint32_t* t256;     // [256][QFEC_TAB_STRIDE] perm tables of every coefficient value (compact mode),
+                              // then [256][8] = t1 t3 t4 0 t0 t2 0 0 of each (recon_impl 9)
     int compact;              // tuning "recon_compact": tables via t256 + the record's offsets
     int vec16;
     int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once,

@@ -38,6 +38,13 @@ def load_sink():
     s = C.CDLL(SINK_SO)
     s.sink_fold.argtypes = [C.c_char_p, C.c_uint]
     s.sink_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+    s.sink_pack_inputs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                   C.c_int, C.c_int, C.POINTER(C.c_ulonglong), C.c_void_p]
+    s.sink_unpack_inputs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+    s.sink_unpack_inputs.restype = C.c_longlong
+    for f, t in (("sink_nsamp", C.c_uint), ("sink_samp_peer", C.c_void_p), ("sink_samp_src", C.c_void_p),
+                 ("sink_samp_size", C.c_void_p), ("sink_samp_buf", C.c_void_p)):
+        getattr(s, f).restype = t
     for f, t in (("sink_count", C.c_size_t), ("sink_buf", C.c_void_p), ("sink_offs", C.c_void_p),
                  ("sink_lens", C.c_void_p), ("sink_peers", C.c_void_p), ("sink_ndeliv", C.c_ulonglong),
                  ("sink_dbytes", C.c_ulonglong), ("sink_dsum", C.c_ulonglong), ("sink_fold", C.c_ulonglong)):
@@ -89,6 +96,69 @@ def run(a, sink, st, rep, pay):
             "delivered": int(sink.sink_ndeliv()), "verified": bool(ok)}
 
 
+def check_samples(a, sink, pay, sent_before):
+    """The sampled deliveries (every 61st, tools/zfec_sink.c) byte for byte against the payload
+    the sender sent under that source index: sender session = peer - 1, and source index
+    sent_before + p is the p-th packet of this rep, payload (i * 7 + p + rep) % len(pay)."""
+    import numpy as np
+    ns = int(sink.sink_nsamp())
+    peer = np.ctypeslib.as_array(C.cast(sink.sink_samp_peer(), C.POINTER(C.c_int)), shape=(max(ns, 1),))
+    src = np.ctypeslib.as_array(C.cast(sink.sink_samp_src(), C.POINTER(C.c_uint)), shape=(max(ns, 1),))
+    size = np.ctypeslib.as_array(C.cast(sink.sink_samp_size(), C.POINTER(C.c_uint)), shape=(max(ns, 1),))
+    buf = np.ctypeslib.as_array(C.cast(sink.sink_samp_buf(), C.POINTER(C.c_ubyte)), shape=(max(ns, 1), 2048))
+    bad = 0
+    for t in range(ns):
+        i, p = int(peer[t]) - 1, int(src[t]) - sent_before
+        j = (i * 7 + p + sent_before // a.packets) % len(pay)
+        want = pay[j][0]
+        if not (0 <= p < a.packets and size[t] == len(want) and bytes(buf[t, :size[t]]) == want):
+            bad += 1
+    return {"sampled": ns, "mismatched": bad}
+
+
+def run_e2e(a, sink, st, rep, pay, pay_arr, pay_fold):
+    """End to end, every per-packet call in C (tools/zfec_sink.c): the senders' pack_input calls,
+    the send flush handing each datagram to a callback that copies it out (as a socket send), the
+    kept datagrams' unpack_input calls into the receiving context, and the receive flush folding
+    every delivery where it lies.  send_e2e = payload bytes / (pack inputs + send flush);
+    recv_e2e = payload bytes / (unpack inputs + receive flush).  Deliveries are counted, summed,
+    and every 61st is compared byte for byte with the payload sent under its source index."""
+    L = st["L"]
+    ztx, zrx, tx = st["ztx"], st["zrx"], st["tx"]
+    S = a.sessions
+    tx_arr = (C.c_int * S)(*tx)
+    ssum = C.c_ulonglong()
+    sink.sink_reset()
+    t0 = time.perf_counter()
+    rc = sink.sink_pack_inputs(ztx._h, C.cast(L.qfec_zfec_pack_input, C.c_void_p), tx_arr, S, a.packets,
+                               pay_arr.ctypes.data, len(pay), a.size, rep, C.byref(ssum), pay_fold.ctypes.data)
+    t1 = time.perf_counter()
+    assert rc == 0, rc
+    rc = L.qfec_zfec_flush(ztx._h, st["collect"], st["fold"], None)
+    t2 = time.perf_counter()
+    assert rc >= 0, rc
+    cnt = sink.sink_count()
+    t3 = time.perf_counter()
+    kept = sink.sink_unpack_inputs(zrx._h, C.cast(L.qfec_zfec_unpack_input, C.c_void_p), st["rx_of"], S, a.n,
+                                   st["nlost"])
+    t4 = time.perf_counter()
+    assert kept >= 0, kept
+    sink.sink_reset()
+    rc = L.qfec_zfec_flush(zrx._h, st["collect"], st["fold"], None)
+    t5 = time.perf_counter()
+    assert rc >= 0, rc
+    npk = S * a.packets
+    by = npk * a.size
+    samp = check_samples(a, sink, pay, rep * a.packets)
+    ok = (sink.sink_ndeliv() == npk and sink.sink_dbytes() == by and sink.sink_dsum() == ssum.value and
+          samp["sampled"] > 0 and samp["mismatched"] == 0)
+    return {"pack_inputs_s": round(t1 - t0, 4), "send_flush_s": round(t2 - t1, 4), "datagrams": int(cnt),
+            "unpack_inputs_s": round(t4 - t3, 4), "datagrams_kept": int(kept), "recv_flush_s": round(t5 - t4, 4),
+            "send_e2e_gibs": round(by / (t2 - t0) / 2**30, 3), "recv_e2e_gibs": round(by / (t5 - t3) / 2**30, 3),
+            "send_e2e_mpkts": round(npk / (t2 - t0) / 1e6, 3), "recv_e2e_mpkts": round(npk / (t5 - t3) / 1e6, 3),
+            "delivered": int(sink.sink_ndeliv()), "byte_check": samp, "verified": bool(ok)}
+
+
 def setup(a, sink):
     L = zlib(a)
     ztx, zrx = qa.Zfec(_lib=L), qa.Zfec(_lib=L)
@@ -98,8 +168,9 @@ def setup(a, sink):
     nlost = min(a.n - a.k, int(round(a.loss * a.n)))
     rx_of = (C.c_int * a.sessions)(*rx)
     sink.sink_forward(zrx._h, C.cast(L.qfec_zfec_unpack_input, C.c_void_p), rx_of, a.sessions, a.n, nlost)
-    return {"L": L, "ztx": ztx, "zrx": zrx, "tx": tx, "rx": rx, "nlost": nlost,
+    return {"L": L, "ztx": ztx, "zrx": zrx, "tx": tx, "rx": rx, "nlost": nlost, "rx_of": rx_of,
             "fwd": _PACK_OUT(C.cast(sink.sink_pack_forward, C.c_void_p).value),
+            "collect": _PACK_OUT(C.cast(sink.sink_pack, C.c_void_p).value),
             "fold": _UNPACK_OUT(C.cast(sink.sink_unpack_fold, C.c_void_p).value)}
 
 
@@ -122,9 +193,28 @@ def main():
     for _ in range(257):
         b = r.randbytes(a.size)
         pay.append((b, int(sink.sink_fold(b, len(b)))))
+    import numpy as np
+    pay_arr = np.frombuffer(b"".join(b for b, _ in pay), dtype=np.uint8)
+    pay_fold = np.array([f for _, f in pay], dtype=np.uint64)
     best = None
+    best_e2e = None
     st = setup(a, sink)
-    for rep in range(a.reps):
+    for rep in range(2 * a.reps):
+        if rep % 2:  # end-to-end reps interleaved with the flush-only ones, same contexts
+            res = run_e2e(a, sink, st, rep, pay, pay_arr, pay_fold)
+            if not a.json:
+                print(f"rep {rep} (end to end, inputs in C): pack inputs {res['pack_inputs_s']:.4f}s + send flush "
+                      f"{res['send_flush_s']:.4f}s = {res['send_e2e_gibs']:.2f} GiB/s; unpack inputs "
+                      f"{res['unpack_inputs_s']:.4f}s + receive flush {res['recv_flush_s']:.4f}s = "
+                      f"{res['recv_e2e_gibs']:.2f} GiB/s; byte check {res['byte_check']} verified={res['verified']}",
+                      flush=True)
+            if rep > 1 and (best_e2e is None or res["send_e2e_gibs"] + res["recv_e2e_gibs"] >
+                            best_e2e["send_e2e_gibs"] + best_e2e["recv_e2e_gibs"]):
+                best_e2e = res
+            if not res["verified"]:
+                best_e2e = res
+                break
+            continue
         res = run(a, sink, st, rep, pay)
         if not a.json:
             print(f"rep {rep}: {a.sessions} sessions x {a.packets} x {a.size} B, RS({a.k},{a.n}), loss {a.loss} "
@@ -138,6 +228,12 @@ def main():
     st["ztx"].close()
     st["zrx"].close()
     if a.json:
+        best = dict(best or {})
+        best["e2e"] = best_e2e
+        if best_e2e is not None:
+            best["send_e2e_gibs"] = best_e2e["send_e2e_gibs"]
+            best["recv_e2e_gibs"] = best_e2e["recv_e2e_gibs"]
+            best["verified"] = bool(best.get("verified")) and bool(best_e2e["verified"])
         print(json.dumps(best), flush=True)
 
 

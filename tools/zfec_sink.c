@@ -62,14 +62,82 @@ int sink_pack_forward(void *peer, const char *p, unsigned int size) {
     return fwd_fn(fwd_z, fwd_rx[s], p, size);
 }
 
+/* sampled deliveries, for a byte check of the payloads against what was sent: every
+ * `samp_every`-th delivery's peer, source index, size and bytes (up to SAMP_MAX of them) */
+#define SAMP_MAX 4096
+#define SAMP_BYTES 2048
+static unsigned samp_every = 61, nsamp;
+static int samp_peer[SAMP_MAX];
+static unsigned samp_src[SAMP_MAX], samp_size[SAMP_MAX];
+static unsigned char samp_buf[SAMP_MAX][SAMP_BYTES];
+
 /* receive side without a copy: fold the payload where the layer hands it over */
 int sink_unpack_fold(void *peer, const char *p, unsigned int size, unsigned int src) {
-    (void)peer;
-    (void)src;
+    if (samp_every && ndeliv % samp_every == 0 && nsamp < SAMP_MAX) {
+        samp_peer[nsamp] = (int)(intptr_t)peer;
+        samp_src[nsamp] = src;
+        samp_size[nsamp] = size;
+        memcpy(samp_buf[nsamp], p, size < SAMP_BYTES ? size : SAMP_BYTES);
+        ++nsamp;
+    }
     ndeliv++;
     dbytes += size;
     dsum += fold((const unsigned char *)p, size);
     return 0;
+}
+
+unsigned sink_nsamp(void) { return nsamp; }
+const int *sink_samp_peer(void) { return samp_peer; }
+const unsigned *sink_samp_src(void) { return samp_src; }
+const unsigned *sink_samp_size(void) { return samp_size; }
+const unsigned char *sink_samp_buf(void) { return &samp_buf[0][0]; }
+
+/* end-to-end drivers: the per-packet input calls an application makes, as C loops, so their
+ * cost is timed with the flushes.
+ * sink_pack_inputs: sender session sess[i] gets `packets` payloads, the p-th being payload
+ * (i * 7 + p + rep) % npay of the `npay` payloads of `size` bytes at pay; returns 0 or the first
+ * failing call's code.  *sum = the fold of everything sent. */
+typedef int (*pack_input_fn)(void *z, int s, const void *d, unsigned int size);
+int sink_pack_inputs(void *z, void *fn, const int *sess, int nsess, int packets, const unsigned char *pay, int npay,
+                     int size, int rep, unsigned long long *sum, const unsigned long long *pay_fold) {
+    pack_input_fn f = (pack_input_fn)fn;
+    unsigned long long s = 0;
+    for (int i = 0; i < nsess; ++i)
+        for (int p = 0; p < packets; ++p) {
+            const int j = (i * 7 + p + rep) % npay;
+            const int rc = f(z, sess[i], pay + (size_t)j * (size_t)size, (unsigned)size);
+            if (rc < 0) return rc;
+            s += pay_fold[j];
+        }
+    *sum = s;
+    return 0;
+}
+
+/* sink_unpack_inputs: the datagrams sink_pack collected go to a receiving context's
+ * unpack_input, session peer - 1 -> rx_of[peer - 1], dropping `ndrop` of every n consecutive
+ * datagrams of a session the way sink_pack_forward does; returns the number handed over or a
+ * negative code */
+long long sink_unpack_inputs(void *z, void *fn, const int *rx_of, int nsess, int nn, int ndrop) {
+    unpack_input_fn f = (unpack_input_fn)fn;
+    unsigned long long *cnt = calloc((size_t)nsess, sizeof(unsigned long long));
+    long long kept = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const int s = (int)peers[i] - 1;
+        const unsigned long long c = cnt[s]++;
+        const int j = (int)(c % (unsigned long long)nn), g = (int)(c / (unsigned long long)nn);
+        int drop = 0;
+        for (int t = 0; t < ndrop; ++t)
+            if ((g + t) % nn == j) drop = 1;
+        if (drop) continue;
+        const int rc = f(z, rx_of[s], buf + offs[i], lens[i]);
+        if (rc < 0) {
+            free(cnt);
+            return rc;
+        }
+        ++kept;
+    }
+    free(cnt);
+    return kept;
 }
 
 int sink_pack(void *peer, const char *p, unsigned int size) {
@@ -120,7 +188,7 @@ int sink_unpack(void *peer, const char *p, unsigned int size, unsigned int src) 
 
 unsigned long long sink_fold(const unsigned char *q, unsigned int size) { return fold(q, size); }
 
-void sink_reset(void) { used = n = 0; ndeliv = dbytes = dsum = 0; }
+void sink_reset(void) { used = n = 0; ndeliv = dbytes = dsum = 0; nsamp = 0; }
 size_t sink_count(void) { return n; }
 const unsigned char *sink_buf(void) { return buf; }
 const uint32_t *sink_offs(void) { return offs; }
