@@ -890,7 +890,12 @@ def load_traffic(path, workload_key, sources=KERNEL_SOURCES):
     want = kernel_sources_hash(sources)
     if ent.get("kernel_sources_sha256") != want:
         return None, f"stale: measured on kernel sources {ent.get('kernel_sources_sha256')}, now {want}"
-    return ent, f"{os.path.relpath(path, ROOT)} ({ent.get('run', 'PMC run')}, kernel sources {want})"
+    run = ent.get("run", "PMC run")
+    # the counter CSVs behind the entry: profiles/<run>_pmc/ or profiles/<run>/pmc/ (tracked)
+    csv = next((d for d in (f"profiles/{run}_pmc", f"profiles/{run}/pmc") if os.path.isdir(os.path.join(ROOT, d))),
+               None)
+    return ent, (f"{os.path.relpath(path, ROOT)} ({run}, kernel sources {want}; counter CSVs "
+                 f"{csv or 'not found under profiles/'})")
 
 
 def kernel_sources_hash(sources=KERNEL_SOURCES):
