@@ -257,6 +257,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "wire_rx_tail"     1 (k_unpack_fused) tail dwords ride on the last 16-B pass | 0 their own pass
  *   "frame_rows"       2 framing kernels run two rows per wave, loads first, frames built in LDS and
  *                      stored flat (rows <= 2 KiB) | 3 the same, stored directly | 1 | 4
+ *   "wire_rx_skip_lost" 1 k_unpack_v2 does not read rows whose length is 0 (not received) | 0 it reads
+ *                      every row's header
  *   "wire_rx_lds"      1 k_unpack_v2 stages the K data rows in LDS and stores them flat where that
  *                      keeps 3/4 of the waves | 2 whenever they fit 16 KiB | 0 row by row
  *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged

@@ -94,6 +94,7 @@ struct WireArgs {
     int checksum;
     int dec_pkt_size;
     int store_nt;             // fused send: bit 0 body, bit 1 head use non-temporal stores
+    int rx_skip_lost;         // receive (k_unpack_v2): rows with wire_len <= 0 are not read at all
 };
 
 hipError_t launch_build_shards(const WireArgs& a, hipStream_t s);
@@ -158,6 +159,7 @@ struct Tuning {
     int wire_rx_lds = 1;    // fused receive: K rows staged in LDS, stored flat (one wave per block)
     int frame_rows = 2;     // ProtocolUdp framing: rows per wave, loads issued first (2 or 4; 1: one row per wave)
     int wire_rx_split = 1;  // fused receive: k_unpack_v2 (1 auto lanes, 2 16-B, 3 8-B); 0 k_unpack_fused
+    int wire_rx_skip_lost = 0;  // k_unpack_v2: skip the header load of rows not received (A/B)
 };
 Tuning& tuning();
 

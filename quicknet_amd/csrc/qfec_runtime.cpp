@@ -914,6 +914,7 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "wire_rx_lds") && value >= 0 && value <= 2) { tuning().wire_rx_lds = value; return QFEC_OK; }
     if (!strcmp(key, "frame_rows") && value >= 1 && value <= 4) { tuning().frame_rows = value; return QFEC_OK; }
     if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 4) { tuning().wire_rx_split = value; return QFEC_OK; }
+    if (!strcmp(key, "wire_rx_skip_lost") && (value == 0 || value == 1)) { tuning().wire_rx_skip_lost = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
     if (!strcmp(key, "percall_spin") && (value == 0 || value == 1)) { g_percall_spin = value; return QFEC_OK; }
     if (!strcmp(key, "percall_in") && (value == 0 || value == 1)) { g_percall_in = value; return QFEC_OK; }
@@ -2268,16 +2269,17 @@ struct fec_handle {
 };
 constexpr size_t kFecDecCacheMax = 4096;
 
-// run `rows` (e x k coefficient rows) over k input packets of sz bytes -> e outputs
+// run `rows` (e x k coefficient rows) over k input packets of sz bytes -> e outputs.  in_dev /
+// out_dev: whether in[0] / out[0] are device memory (-1: find out here)
 int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* const* in, unsigned char* const* out,
-               int sz) {
+               int sz, int in_dev = -1, int out_dev = -1) {
     DevCtx* ctx = nullptr;
     int rc = current_ctx(&ctx);
     if (rc) return rc;
-    const bool dev = is_device_ptr(in[0]);
+    const bool dev = in_dev < 0 ? is_device_ptr(in[0]) : in_dev != 0;
     const size_t pitch = round_up((size_t)sz, 16);
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (!dev && k * e <= kPcMaxCoef && g_percall_fast.load() && !is_device_ptr(out[0])) {
+    if (!dev && k * e <= kPcMaxCoef && g_percall_fast.load() && !(out_dev < 0 ? is_device_ptr(out[0]) : out_dev != 0)) {
         // the resident server (packets of up to 4 KiB)
         if (pitch <= (size_t)kPcMaxChunks * 16 && k <= 16 && k * e <= kPcSrvMaxCoef && g_percall_resident.load() &&
             pc_server_setup(*ctx) == QFEC_OK) {
@@ -2339,7 +2341,7 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
                          ctx->stream)))
         return rc;
     return scatter_rows(*ctx, out, (size_t)e, sz, pitch, ctx->d_stage + ib, ctx->h_stage + ib,
-                        is_device_ptr(out[0]), nullptr);
+                        out_dev < 0 ? is_device_ptr(out[0]) : out_dev != 0, nullptr);
 }
 
 std::once_flag g_fec_init_once;
@@ -2441,7 +2443,7 @@ void fec_encode(void* code, unsigned char** src, unsigned char* dst, int index, 
                 // the copy, not the caller's buffers: the rows belong to the bytes just compared
                 unsigned char* ins[256];
                 for (int i = 0; i < k; ++i) ins[i] = h->grp_in.data() + (size_t)i * szz;
-                const int rc = apply_rows(h->enc_all, k, m, ins, outs, sz);
+                const int rc = apply_rows(h->enc_all, k, m, ins, outs, sz, 0, 0);  // both host copies
                 if (rc) {
                     fprintf(stderr, "[qfec] fec_encode: %s\n", qfec_last_error());
                     return;

@@ -1653,10 +1653,18 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
     if (lane < N) {
         len = wire_len[g * N + lane];
         int dlen = len;
-        uint4 h;
+        uint4 h = make_uint4(0u, 0u, 0u, 0u);
+        // rx_skip_lost: a row not received (length <= 0) is not read -- its first line is otherwise
+        // fetched for nothing (3 of 13 rows: ~4 % of the receive's reads), at the price of the
+        // header load waiting for the length
+        const bool rd = !a.rx_skip_lost || len > 0;
         if constexpr (FP != 0) {
             const uint8_t* frow = wire_g + (uint64_t)lane * wp;
-            const uint4 f0 = *reinterpret_cast<const uint4*>(frow), f1 = *reinterpret_cast<const uint4*>(frow + 16);
+            uint4 f0 = make_uint4(0u, 0u, 0u, 0u), f1 = f0;
+            if (rd) {
+                f0 = *reinterpret_cast<const uint4*>(frow);
+                f1 = *reinterpret_cast<const uint4*>(frow + 16);
+            }
             v_fx = (get_byte(f0, 0) ^ fr.gmask ^ 0x5Au) & 0xFFu;
             const uint32_t mmx = v_fx * 0x01010101u;
             const uint4 u0 = xor16(f0, mmx), u1 = xor16(f1, mmx);
@@ -1674,7 +1682,7 @@ __global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const
             }
             v_fs = pre | (get_byte(u0, 1) << 24);
         } else {
-            h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
+            if (rd) h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
         }
         const uint32_t tag = get_byte(h, 0);
         hdr = tag == 0xED ? 13 : 11;
@@ -2442,8 +2450,10 @@ hipError_t launch_pack_frames(const WireArgs& a, const FrameSend& fs, int fp, co
 // the lean single-wave receive for one (K, M): 16-B lanes (NVA 4) or 8-B lanes (NVA 2); fp 4 / 12
 // reads ProtocolUdp frames (qfec_unpack_frames)
 template <int K, int M, int FP>
-hipError_t unpack_v2_launch(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
+hipError_t unpack_v2_launch(const WireArgs& a0, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
                             hipStream_t s, int nva, const FrameRecv& fr) {
+    WireArgs a = a0;
+    a.rx_skip_lost = tuning().wire_rx_skip_lost;
     const dim3 grid((unsigned)((a.groups + 3) / 4)), block(256);
     // the K rows staged in LDS and stored flat (tuning "wire_rx_lds"): 1 where the staging leaves
     // at least 3/4 of the waves per CU the registers allow (16 on 16-B lanes, 24 on 8-B lanes;

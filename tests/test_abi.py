@@ -189,7 +189,9 @@ def test_tune_keys_documented_and_accepted():
     assert L.qfec_tune(b"percall_in", 7) != 0
     assert L.qfec_tune(b"recon_impl", 99) != 0
     # back to the defaults the rest of this process expects
-    for key, value in (("recon_impl", -1), ("wire_store_nt", 3), ("percall_resident", 1), ("percall_in", 0)):
+    for key, value in (("recon_impl", -1), ("wire_store_nt", 3), ("percall_resident", 1), ("percall_in", 0),
+                       ("percall_idle_us", 1000), ("percall_timeout_us", 2000000), ("percall_fault", 0),
+                       ("percall_group", 1), ("wire_rx_skip_lost", 0)):
         assert L.qfec_tune(key.encode(), value) == 0
 
 

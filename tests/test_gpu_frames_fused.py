@@ -182,14 +182,16 @@ def test_unpack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session):
     torch.cuda.synchronize()
     want = [t.cpu().numpy() for t in want]
     outs = []
-    for fused in (1, 0):
+    for fused, skip in ((1, 0), (0, 0), (1, 1)):  # one pass, two calls, one pass not reading lost rows
         qa.tune("wire_fused_rx", fused)
+        qa.tune("wire_rx_skip_lost", skip)
         try:
             got = code.unpack_frames(dev(f), dev(fl), gmask=GMASK, session=session, checksum=bool(checksum),
                                      shard_pitch=sp)
             torch.cuda.synchronize()
         finally:
             qa.tune("wire_fused_rx", 1)
+            qa.tune("wire_rx_skip_lost", 0)
         outs.append([t.cpu().numpy() if t is not None else None for t in got])
     for sh, status, psize, rx, fst, cho in outs:
         assert np.array_equal(fst, st_ref)

@@ -19,6 +19,17 @@ import quicknet_amd as qa  # noqa: E402
 from quicknet_amd.synth import erasure_marks, marks_to_rs_layout  # noqa: E402
 
 
+if os.environ.get("QFEC_LIB"):  # an older build (tools/ab_lib.sh): knobs it predates are skipped
+    _tune = qa.tune
+
+    def _tune_compat(key, value):
+        try:
+            _tune(key, value)
+        except qa.QfecError:
+            pass
+    qa.tune = _tune_compat
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rounds", type=int, default=12)
@@ -73,6 +84,7 @@ def main():
         ("encode impl1 (row loop)", lambda: qa.tune("encode_impl", 1), enc, enc_bytes),
         ("encode ldslog", lambda: (qa.tune("encode_impl", 0), qa.set_kernel_variant(1)), enc, enc_bytes),
         ("probe xor (traffic only)", lambda: None, probe, enc_bytes),
+        ("recon auto (the library's own choice)", lambda: qa.tune("recon_impl", -1), rec, dec_bytes),
         ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
         ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
         ("recon impl2 (exact e rows)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),

@@ -16,7 +16,7 @@ for i in 1 2 3; do
   for n in r02 head; do
     echo "== $n ($i)" >> $OUT/ab_lib.txt
     QFEC_LIB=$PWD/tools/_abl/libqfec_$n.so timeout -k 10 120 python tools/ab.py $C4 \
-      --only "encode_impl0,probe,recon_impl8" >> $OUT/ab_lib.txt 2>&1 || exit 5
+      --only "encode_impl0,probe,recon_auto" >> $OUT/ab_lib.txt 2>&1 || exit 5
   done
 done
 tail -30 $OUT/ab_lib.txt
