@@ -232,10 +232,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
 
 /* Experiment knobs for interleaved A/B timing (tools/ab.py, tools/wire_ab.py).  Defaults are
  * the measured best; results are identical either way.
- *   "encode_impl"      0 all rows | 1 row loop
- *   "recon_impl"       -1 auto | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B | 5 one wave per group on 8-B slabs | 6 = 3 at 8 waves/SIMD | 8 = 3 with one group per block (auto picks it for 3 where a group is <= 4 waves) | 9 = 8 with
- *                      two of each coefficient's five table dwords broadcast from LDS instead of moved
- *                      from SGPRs (k * m <= 64)
+ *   "encode_impl"      0 all rows | 1 row loop | 2 all rows, the inputs loaded in two halves (fewer registers)
+ *   "recon_impl"       -1 auto | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B | 5 one wave per group on 8-B slabs | 6 = 3 at 8 waves/SIMD | 8 = 3 with one group per block (auto picks it for 3 where a group is <= 4 waves)
  *   "recon_compact"    1 tables via the 256-entry table at the record header's offsets | 0 from the record
  *   "recon_full_lines" 1 8-/12-B lanes cover the 16-B columns' span for k < 14 | 2 always | 0 stop at B
  *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies
@@ -258,7 +256,7 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "frame_rows"       2 framing kernels run two rows per wave, loads first, frames built in LDS and
  *                      stored flat (rows <= 2 KiB) | 3 the same, stored directly | 1 | 4
  *   "wire_rx_skip_lost" 1 k_unpack_v2 does not read rows whose length is 0 (not received) | 0 it reads
- *                      every row's header
+ *                      every row's header (A/B)
  *   "wire_rx_lds"      1 k_unpack_v2 stages the K data rows in LDS and stores them flat where that
  *                      keeps 3/4 of the waves | 2 whenever they fit 16 KiB | 0 row by row
  *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged

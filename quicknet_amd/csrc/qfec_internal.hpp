@@ -62,8 +62,7 @@ struct ReconArgs {
     int k, m;
     int surv_off, lost_off, hdr;
     int coff;                 // record word of the coefficient-table byte offsets (RecordLayout::coff)
-    const uint32_t* t256;     // [256][QFEC_TAB_STRIDE] perm tables of every coefficient value (compact mode),
-                              // then [256][8] = t1 t3 t4 0 t0 t2 0 0 of each (recon_impl 9)
+    const uint32_t* t256;     // [256][QFEC_TAB_STRIDE] perm tables of every coefficient value (compact mode)
     int compact;              // tuning "recon_compact": tables via t256 + the record's offsets
     int vec16;
     int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once,
@@ -159,7 +158,7 @@ struct Tuning {
     int wire_rx_lds = 1;    // fused receive: K rows staged in LDS, stored flat (one wave per block)
     int frame_rows = 2;     // ProtocolUdp framing: rows per wave, loads issued first (2 or 4; 1: one row per wave)
     int wire_rx_split = 1;  // fused receive: k_unpack_v2 (1 auto lanes, 2 16-B, 3 8-B); 0 k_unpack_fused
-    int wire_rx_skip_lost = 0;  // k_unpack_v2: skip the header load of rows not received (A/B)
+    int wire_rx_skip_lost = 1;  // k_unpack_v2: rows not received are not read (r04b: 479 vs 483 us)
 };
 Tuning& tuning();
 

@@ -81,6 +81,59 @@ __global__ void __launch_bounds__(256) k_encode_perm(EncodeArgs a) {
     for (int r = 0; r < M; ++r) st16(dst + (uint64_t)r * a.pitch, acc[r]);
 }
 
+// Variant (tuning "encode_impl" = 2): the K inputs in two halves, the second half's loads issued
+// only after the first half has been multiplied in -- half the input registers live at a time
+// (RS(16,4): 69 instead of 116 VGPRs, 7 waves per SIMD instead of 4; RS(10,3): 60 instead of 102),
+// so more waves share the memory latency; each wave has one round trip more.  Same VALU as impl 0.
+template <int K, int M>
+__global__ void __launch_bounds__(256) k_encode_perm_halves(EncodeArgs a) {
+    constexpr int H = (K + 1) / 2;
+    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (t >= a.work) return;
+    const uint64_t g = fast_div(t, a.cols_div);
+    const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
+    const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
+    uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
+    const uint32_t* __restrict__ tab = a.tab;
+    uint4 acc[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+        acc[r] = make_uint4(0, 0, 0, 0);
+        if (tab[(r * K) * QFEC_TAB_STRIDE + 5]) acc[r] = *reinterpret_cast<const uint4*>(dst + (uint64_t)r * a.pitch);
+    }
+#pragma unroll
+    for (int c0 = 0; c0 < K; c0 += H) {
+        // a scheduling fence, not a memory one: the next half's loads are not hoisted above this
+        // half's multiply (and the table loads stay scalar -- an asm pin would make them vector)
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int HH = H;
+        const int n = min(HH, K - c0);
+        uint4 x[H];
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+            if (i < n) x[i] = ld16(src + (uint64_t)(c0 + i) * a.pitch);
+#pragma unroll
+        for (int i = 0; i + 1 < H; i += 2) {
+            if (i + 1 >= n) continue;
+            Sel sa[4], sb[4];
+            sel16(sa, x[i]);
+            sel16(sb, x[i + 1]);
+#pragma unroll
+            for (int r = 0; r < M; ++r)
+                gf_mac16x2(acc[r], sa, sb, tab + (r * K + c0 + i) * QFEC_TAB_STRIDE,
+                           tab + (r * K + c0 + i + 1) * QFEC_TAB_STRIDE);
+        }
+        if (n & 1) {
+            Sel sl[4];
+            sel16(sl, x[n - 1]);
+#pragma unroll
+            for (int r = 0; r < M; ++r) gf_mac16(acc[r], sl, tab + (r * K + c0 + n - 1) * QFEC_TAB_STRIDE);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) st16(dst + (uint64_t)r * a.pitch, acc[r]);
+}
+
 // Variant (tuning "encode_impl" = 1): one output row at a time, selectors re-formed per
 // row (pinned against LICM) -- fewer registers, more VALU.
 template <int K, int M>
@@ -393,7 +446,6 @@ template <int CT>
 struct RTab;
 template <>
 struct RTab<0> {
-    static constexpr bool kLds = false;
     const uint32_t* __restrict__ tab;
     __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const { return tab + (j * K + c) * QFEC_TAB_STRIDE; }
     __device__ __forceinline__ bool quirk(int j, int K) const { return tab[(j * K) * QFEC_TAB_STRIDE + 5] != 0; }
@@ -404,7 +456,6 @@ struct RTab<0> {
 };
 template <>
 struct RTab<1> {
-    static constexpr bool kLds = false;
     const uint32_t* __restrict__ offs;
     const uint32_t* __restrict__ t256;
     __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const {
@@ -416,59 +467,12 @@ struct RTab<1> {
         for (int i = 0; i < 5; ++i) t5[i] = at(j, c, K)[i];
     }
 };
-// compact, with dwords 0 and 2 of every coefficient's table (the low halves of the two 8-entry
-// lookups) held in the wave's LDS row instead of SGPRs.  v_perm_b32 is VOP3 and gfx950 reads one
-// SGPR per VALU instruction, so with both halves in SGPRs the compiler spends a v_mov per half and
-// coefficient (2 of the ~11 VALU per coefficient of an 8-B lane); a broadcast ds_read_b64 puts both
-// in VGPRs through the LDS pipe, which this kernel otherwise leaves idle (recon_impl 9).
-// the LDS rows of recon_impl 9: [wave of the block][j * K + c] = (t0, t2) of coefficient (j, c).
-// Named directly (not through a pointer) so the compiler knows the stores into it cannot clobber
-// the global tables, whose loads then stay scalar.
-__shared__ uint2 g_recon_lt[4][64];
-template <>
-struct RTab<2> {
-    static constexpr bool kLds = true;
-    const uint32_t* __restrict__ offs;
-    const uint32_t* __restrict__ t256b;  // the split table: [t1 t3 t4 0 | t0 t2 0 0] per value
-    __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const {
-        return reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t256b) + (offs[j * K + c] & ~31u));
-    }
-    __device__ __forceinline__ bool quirk(int j, int K) const { return (offs[j * K] & 1u) != 0; }
-    __device__ __forceinline__ uint2 lt(int i) const { return g_recon_lt[threadIdx.x >> 6][i]; }
-    __device__ __forceinline__ void set_lt(int i, uint2 v) const { g_recon_lt[threadIdx.x >> 6][i] = v; }
-    __device__ __forceinline__ void load5(int j, int c, int K, uint32_t (&t5)[5]) const {
-        const uint32_t* p = at(j, c, K);
-        const uint2 v = lt(j * K + c);
-        t5[0] = v.x;
-        t5[1] = p[0];
-        t5[2] = v.y;
-        t5[3] = p[1];
-        t5[4] = p[2];
-    }
-};
 template <int K, int E, int D, class TT>
 __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                               uint64_t lost_bits, const TT& T, uint64_t pitch, uint64_t off,
-                                               bool active = true) {
+                                               uint64_t lost_bits, const TT& T, uint64_t pitch, uint64_t off) {
     uint32_t x[K][D];
-    uint32_t o_lane = 0;
-    const int lane = threadIdx.x & 63;
-    if constexpr (TT::kLds) {  // lane j*K + c: coefficient (j, c)'s table offset, loaded before the shards
-        if (lane < E * K) o_lane = T.offs[lane];
-    }
 #pragma unroll
     for (int c = 0; c < K; ++c) ldv<D>(x[c], src[c] + off);
-    if constexpr (TT::kLds) {
-        uint2 tv = make_uint2(0u, 0u);
-        if (lane < E * K) {
-            tv = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(T.t256b) + (o_lane & ~31u) + 16u);
-        }
-        // every lane of the wave runs this (inactive columns are clamped, not masked).  No fence:
-        // the LDS unit runs one wave's DS instructions in order, so the reads below see these
-        // stores, and an acquire fence would make the compiler turn the scalar table loads into
-        // vector loads (memory after an acquire is no longer provably unclobbered)
-        T.set_lt(lane, tv);
-    }
     uint8_t* dst[E];
     uint32_t acc[E][D];
 #pragma unroll
@@ -507,24 +511,21 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
                 acc[j][d] = xor3(acc[j][d], pp0(sl[d], t[0], t[1]), pp1(sl[d], t[2], t[3])) ^ pp2(sl[d], t[4]);
         }
     }
-    if (active) {
 #pragma unroll
-        for (int j = 0; j < E; ++j) stv<D>(dst[j], acc[j]);
-    }
+    for (int j = 0; j < E; ++j) stv<D>(dst[j], acc[j]);
 }
 
 // wave-uniform dispatch on e to the exact-row-count body
 template <int K, int M, int D, class TT, int E = M>
 __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                                  uint64_t lost_bits, const TT& T, int e, uint64_t pitch, uint64_t off,
-                                                  bool active = true) {
+                                                  uint64_t lost_bits, const TT& T, int e, uint64_t pitch, uint64_t off) {
     if constexpr (E > 1) {
         if (e < E) {
-            recon_column_by_e<K, M, D, TT, E - 1>(src, data_g, lost_bits, T, e, pitch, off, active);
+            recon_column_by_e<K, M, D, TT, E - 1>(src, data_g, lost_bits, T, e, pitch, off);
             return;
         }
     }
-    recon_column_e<K, E, D>(src, data_g, lost_bits, T, pitch, off, active);
+    recon_column_e<K, E, D>(src, data_g, lost_bits, T, pitch, off);
 }
 
 // LUT mode, compile-time K, M.  The survivor set follows from the erasure mask alone --
@@ -537,7 +538,7 @@ __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K]
 // IMPL 8: IMPL 3 launched with one group per block (blocks of wpg8 waves), so a group's slab
 // waves share a CU and its scalar data (marks, LUT entry, record header, tables)
 template <int K, int M, int IMPL_, int CT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMPL_ == 6 ? 8 : IMPL_ == 9 ? 6 : 1)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMPL_ == 6 ? 8 : 1)))
 k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ parity,
                                                           const uint8_t* __restrict__ marks,
@@ -545,11 +546,10 @@ k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint32_t* __restrict__ records) {
     // __restrict__ parameters: the LUT and records are provably not written by this
     // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
-    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8 || IMPL_ == 9) ? 3 : IMPL_;
+    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8) ? 3 : IMPL_;
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * ((IMPL_ == 8 || IMPL_ == 9) ? a.wpg8 : 4u) +
-                                                        (threadIdx.x >> 6));
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (IMPL_ == 8 ? a.wpg8 : 4u) + (threadIdx.x >> 6));
     const uint32_t wpg = IMPL == 5 ? 1u : IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
@@ -588,13 +588,6 @@ k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
         return;
     }
     const uint32_t col = part * 64u + lane;
-    if constexpr (IMPL_ == 9) {  // every lane runs the body (it fills the wave's LDS row); idle ones store nothing
-        const RTab<2> TL{records + rec + a.coff, a.t256 + 256 * QFEC_TAB_STRIDE};
-        const bool act = col < a.cols8;
-        recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TL, e, pitch, (uint64_t)(act ? col : a.cols8 - 1u) * 8u,
-                                   act);
-        return;
-    }
     if (col < (IMPL == 3 ? a.cols8 : IMPL == 4 ? a.cols12 : a.cols)) {
         if constexpr (CT != 0) {
             if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 16u);
@@ -724,6 +717,8 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
     if (a.k == KK && a.m == MM) {                                                             \
         if (a.impl == 1)                                                                      \
             hipLaunchKernelGGL((k_encode_perm_rows<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
+        else if (a.impl == 2)                                                                 \
+            hipLaunchKernelGGL((k_encode_perm_halves<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
         else                                                                                  \
             hipLaunchKernelGGL((k_encode_perm<KK, MM>), dim3(grid), dim3(256), 0, stream, a);  \
         return hipGetLastError();                                                             \
@@ -762,11 +757,8 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 
 #define QFEC_REC_LAUNCH(KK, MM, AR)                                                                        \
     do {                                                                                                   \
-        const dim3 blk(AR >= 8 ? 64u * a.wpg8 : 256u), grd(AR >= 8 ? (unsigned)a.groups : pgrid);          \
-        if (AR == 9)                                                                                       \
-            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, 9, 1>), grd, blk, 0, stream, a, a.data, a.parity,  \
-                               a.marks, a.lut, a.records);                                                 \
-        else if (AR >= 2 && a.compact && a.t256)                                                           \
+        const dim3 blk(AR == 8 ? 64u * a.wpg8 : 256u), grd(AR == 8 ? (unsigned)a.groups : pgrid);          \
+        if (AR >= 2 && a.compact && a.t256)                                                                \
             hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, (AR >= 2) * 1>), grd, blk, 0, stream, a,   \
                                a.data, a.parity, a.marks, a.lut, a.records);                               \
         else                                                                                               \
@@ -786,10 +778,8 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
         /* 8-B lanes run one group per block where a group is at most 4 waves: its slab */ \
         /* waves share a CU (RS(16,4) B=1400: 1 218 against 1 224 us, r03blk)            */ \
         if (im == 3 && a.impl < 0) im = 8;                                         \
-        if ((im == 8 || im == 9) && (a.wpg8 < 1 || a.wpg8 > 4)) im = 3;            \
-        if (im == 9 && !(a.compact && a.t256 && KK * MM <= 64)) im = 8;           \
-        if (im == 9) QFEC_REC_LAUNCH(KK, MM, 9);                                   \
-        else if (im == 8) QFEC_REC_LAUNCH(KK, MM, 8);                              \
+        if (im == 8 && (a.wpg8 < 1 || a.wpg8 > 4)) im = 3;                         \
+        if (im == 8) QFEC_REC_LAUNCH(KK, MM, 8);                                   \
         else if (im == 6) QFEC_REC_LAUNCH(KK, MM, 6);                              \
         else if (im == 5) QFEC_REC_LAUNCH(KK, MM, 5);                              \
         else if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                              \

@@ -145,20 +145,8 @@ int init_ctx(DevCtx& c, int dev) {
     HIP_TRY(hipMemcpy(c.d_gf, f.exp, 512, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c.d_gf + 512, f.log, 256, hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&c.d_counter, 256));
-    // two tables of all 256 coefficient values: the perm-table layout, then (recon_impl 9) the
-    // same dwords split by where the kernel keeps them: [t1 t3 t4 0 | t0 t2 0 0] -- one scalar
-    // load for the SGPR halves, one vector load for the two that go through LDS
-    std::vector<uint32_t> t256(2 * 256 * QFEC_TAB_STRIDE, 0);
-    for (int v = 0; v < 256; ++v) {
-        uint32_t* e = &t256[(size_t)v * QFEC_TAB_STRIDE];
-        perm_entry((uint8_t)v, e);
-        uint32_t* b = &t256[(size_t)(256 + v) * QFEC_TAB_STRIDE];
-        b[0] = e[1];
-        b[1] = e[3];
-        b[2] = e[4];
-        b[4] = e[0];
-        b[5] = e[2];
-    }
+    std::vector<uint32_t> t256(256 * QFEC_TAB_STRIDE);
+    for (int v = 0; v < 256; ++v) perm_entry((uint8_t)v, &t256[(size_t)v * QFEC_TAB_STRIDE]);
     HIP_TRY(hipMalloc(&c.d_t256, t256.size() * 4));
     HIP_TRY(hipMemcpy(c.d_t256, t256.data(), t256.size() * 4, hipMemcpyHostToDevice));
     return QFEC_OK;
@@ -898,9 +886,9 @@ int qfec_get_kernel_variant(void) { return g_variant.load(); }
 // experiment knobs, for A/B timing in one process (tools/ab.py); not needed in production
 int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
-    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 9 && value != 7) { tuning().recon_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 8 && value != 7) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "host_chunk") && value >= 0) { tuning().host_chunk = value; return QFEC_OK; }
-    if (!strcmp(key, "encode_impl") && (value == 0 || value == 1)) { tuning().encode_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "encode_impl") && value >= 0 && value <= 2) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
     if (!strcmp(key, "wire_chunk") && value >= 0) { tuning().wire_chunk = value; return QFEC_OK; }
     if (!strcmp(key, "wire_send_wave") && value >= 0 && value <= 4) { tuning().wire_send_wave = value; return QFEC_OK; }

@@ -82,6 +82,7 @@ def main():
     variants = [
         ("encode impl0 (all rows)", lambda: qa.tune("encode_impl", 0), enc, enc_bytes),
         ("encode impl1 (row loop)", lambda: qa.tune("encode_impl", 1), enc, enc_bytes),
+        ("encode impl2 (inputs in halves)", lambda: qa.tune("encode_impl", 2), enc, enc_bytes),
         ("encode ldslog", lambda: (qa.tune("encode_impl", 0), qa.set_kernel_variant(1)), enc, enc_bytes),
         ("probe xor (traffic only)", lambda: None, probe, enc_bytes),
         ("recon auto (the library's own choice)", lambda: qa.tune("recon_impl", -1), rec, dec_bytes),
@@ -100,7 +101,6 @@ def main():
         ("recon impl5 (one wave per group, 8-B slabs)", lambda: qa.tune("recon_impl", 5), rec, dec_bytes),
         ("recon impl6 (impl3 at 8 waves/SIMD)", lambda: qa.tune("recon_impl", 6), rec, dec_bytes),
         ("recon impl8 (impl3, one group per block)", lambda: qa.tune("recon_impl", 8), rec, dec_bytes),
-        ("recon impl9 (impl8, table halves via LDS)", lambda: qa.tune("recon_impl", 9), rec, dec_bytes),
     ]
     if a.recon_only:
         variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]

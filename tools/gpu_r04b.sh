@@ -19,9 +19,9 @@ for i in 1 2 3; do
   done
 done
 grep -E "==|median" $OUT/ab_lib.txt
-timeout -k 10 200 python tools/ab.py $C4 --only "encode_impl0,probe,recon_auto,recon_impl8,recon_impl9" > $OUT/ab_c4.txt 2>&1 || { tail $OUT/ab_c4.txt; exit 6; }
+timeout -k 10 200 python tools/ab.py $C4 --only "encode_impl0,encode_impl2,probe,recon_auto,recon_impl8" > $OUT/ab_c4.txt 2>&1 || { tail $OUT/ab_c4.txt; exit 6; }
 cat $OUT/ab_c4.txt
-timeout -k 10 200 python tools/ab.py --rounds 6 --reps 5 --only "encode_impl0,probe,recon_auto,recon_impl8,recon_impl9" > $OUT/ab_c1.txt 2>&1 || { tail $OUT/ab_c1.txt; exit 7; }
+timeout -k 10 200 python tools/ab.py --rounds 6 --reps 5 --only "encode_impl0,encode_impl2,probe,recon_auto,recon_impl8" > $OUT/ab_c1.txt 2>&1 || { tail $OUT/ab_c1.txt; exit 7; }
 cat $OUT/ab_c1.txt
 timeout -k 10 200 python tools/wire_ab.py --unpack --wire-align 64 --rounds 5 --variants "base;wire_rx_skip_lost=1" > $OUT/ab_rx.txt 2>&1 || { tail $OUT/ab_rx.txt; exit 8; }
 cat $OUT/ab_rx.txt
