@@ -143,7 +143,7 @@ hipError_t launch_check_payloads(const WireArgs& a, hipStream_t s);
 // runtime tuning knobs (qfec_tune); defaults are the measured best
 struct Tuning {
     int recon_impl = -1;  // -1 auto (per shape), 0 row loop, 1 all rows
-    int encode_impl = 0;
+    int encode_impl = -1;   // -1 auto (inputs in halves for k >= 16), 0 all rows, 1 row loop, 2 halves
     int wire_fused = 1;     // fused datagram send where a (k, m) instance exists (0: staged)
     int wire_fused_rx = 1;  // fused datagram receive likewise
     int wire_rx_tail = 1;   // fused receive: 1 = tail dwords ride on the last 16-B pass (0: own pass)

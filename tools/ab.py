@@ -80,6 +80,7 @@ def main():
         code.encode(data, par, B)
 
     variants = [
+        ("encode auto (the library's own choice)", lambda: qa.tune("encode_impl", -1), enc, enc_bytes),
         ("encode impl0 (all rows)", lambda: qa.tune("encode_impl", 0), enc, enc_bytes),
         ("encode impl1 (row loop)", lambda: qa.tune("encode_impl", 1), enc, enc_bytes),
         ("encode impl2 (inputs in halves)", lambda: qa.tune("encode_impl", 2), enc, enc_bytes),
@@ -101,6 +102,8 @@ def main():
         ("recon impl5 (one wave per group, 8-B slabs)", lambda: qa.tune("recon_impl", 5), rec, dec_bytes),
         ("recon impl6 (impl3 at 8 waves/SIMD)", lambda: qa.tune("recon_impl", 6), rec, dec_bytes),
         ("recon impl8 (impl3, one group per block)", lambda: qa.tune("recon_impl", 8), rec, dec_bytes),
+        ("recon impl9 (impl4, survivors in halves)", lambda: qa.tune("recon_impl", 9), rec, dec_bytes),
+        ("recon impl10 (impl8, survivors in halves)", lambda: qa.tune("recon_impl", 10), rec, dec_bytes),
     ]
     if a.recon_only:
         variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]
@@ -160,7 +163,7 @@ def main():
                       f"{dec_bytes/(med*1e-3)/1e9:7.1f} GB/s")
         qa.tune("recon_impl", -1)
     qa.set_kernel_variant(0)
-    qa.tune("encode_impl", 0)
+    qa.tune("encode_impl", -1)
     qa.tune("recon_impl", 0)
     code.encode(data, par, B)
     torch.cuda.synchronize()
