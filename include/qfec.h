@@ -234,8 +234,7 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  * the measured best; results are identical either way.
  *   "encode_impl"      -1 auto (2 for k >= 16, else 0) | 0 all rows | 1 row loop | 2 all rows, the inputs
  *                      loaded in two halves (fewer registers, more waves per SIMD)
- *   "recon_impl"       -1 auto | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B | 5 one wave per group on 8-B slabs | 6 = 3 at 8 waves/SIMD | 8 = 3 with one group per block (auto picks it for 3 where a group is <= 4 waves) | 9 = 4 and 10 = 8 with
- *                      the survivors loaded in two halves (compact tables)
+ *   "recon_impl"       -1 auto | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B | 5 one wave per group on 8-B slabs | 6 = 3 at 8 waves/SIMD | 8 = 3 with one group per block (auto picks it for 3 where a group is <= 4 waves)
  *   "recon_compact"    1 tables via the 256-entry table at the record header's offsets | 0 from the record
  *   "recon_full_lines" 1 8-/12-B lanes cover the 16-B columns' span for k < 14 | 2 always | 0 stop at B
  *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies

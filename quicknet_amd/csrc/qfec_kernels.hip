@@ -515,77 +515,17 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
     for (int j = 0; j < E; ++j) stv<D>(dst[j], acc[j]);
 }
 
-// The same with the K survivors loaded in two halves (recon_impl 9 / 10): the second half's loads
-// issue after the first half is multiplied in, so half the input registers are live at a time
-// (the encode's impl 2; RS(16,4) on 12-B lanes: 91 -> 70 VGPRs).  Unlike the encode, no
-// scheduling barrier: here one turns the coefficient tables' scalar loads into vector loads.
-template <int K, int E, int D, class TT>
-__device__ __forceinline__ void recon_column_e_halves(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                                      uint64_t lost_bits, const TT& T, uint64_t pitch, uint64_t off) {
-    constexpr int H = (K + 1) / 2;
-    uint8_t* dst[E];
-    uint32_t acc[E][D];
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(lost_bits);
-        lost_bits &= lost_bits - 1;
-        dst[j] = data_g + (uint64_t)l * pitch + off;
-#pragma unroll
-        for (int d = 0; d < D; ++d) acc[j][d] = 0;
-        if (T.quirk(j, K)) ldv_plain<D>(acc[j], dst[j]);  // rs.c column-0 quirk
-    }
-#pragma unroll
-    for (int c0 = 0; c0 < K; c0 += H) {
-        const int n = K - c0 < H ? K - c0 : H;
-        uint32_t x[H][D];
-#pragma unroll
-        for (int i = 0; i < H; ++i)
-            if (i < n) ldv<D>(x[i], src[c0 + i] + off);
-#pragma unroll
-        for (int i = 0; i + 1 < H; i += 2) {
-            if (i + 1 >= n) continue;
-            Sel sa[D], sb[D];
-#pragma unroll
-            for (int d = 0; d < D; ++d) { sa[d] = gf_sel(x[i][d]); sb[d] = gf_sel(x[i + 1][d]); }
-#pragma unroll
-            for (int j = 0; j < E; ++j) {
-                uint32_t a5[5], b5[5];
-                T.load5(j, c0 + i, K, a5);
-                T.load5(j, c0 + i + 1, K, b5);
-#pragma unroll
-                for (int d = 0; d < D; ++d) acc[j][d] = mac2(acc[j][d], sa[d], sb[d], a5, b5);
-            }
-        }
-        if (n & 1) {
-            Sel sl[D];
-#pragma unroll
-            for (int d = 0; d < D; ++d) sl[d] = gf_sel(x[n - 1][d]);
-#pragma unroll
-            for (int j = 0; j < E; ++j) {
-                uint32_t t[5];
-                T.load5(j, c0 + n - 1, K, t);
-#pragma unroll
-                for (int d = 0; d < D; ++d)
-                    acc[j][d] = xor3(acc[j][d], pp0(sl[d], t[0], t[1]), pp1(sl[d], t[2], t[3])) ^ pp2(sl[d], t[4]);
-            }
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < E; ++j) stv<D>(dst[j], acc[j]);
-}
-
-// wave-uniform dispatch on e to the exact-row-count body (HV: survivors loaded in halves)
-template <int K, int M, int D, class TT, int E = M, bool HV = false>
+// wave-uniform dispatch on e to the exact-row-count body
+template <int K, int M, int D, class TT, int E = M>
 __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
                                                   uint64_t lost_bits, const TT& T, int e, uint64_t pitch, uint64_t off) {
     if constexpr (E > 1) {
         if (e < E) {
-            recon_column_by_e<K, M, D, TT, E - 1, HV>(src, data_g, lost_bits, T, e, pitch, off);
+            recon_column_by_e<K, M, D, TT, E - 1>(src, data_g, lost_bits, T, e, pitch, off);
             return;
         }
     }
-    if constexpr (HV) recon_column_e_halves<K, E, D>(src, data_g, lost_bits, T, pitch, off);
-    else recon_column_e<K, E, D>(src, data_g, lost_bits, T, pitch, off);
+    recon_column_e<K, E, D>(src, data_g, lost_bits, T, pitch, off);
 }
 
 // LUT mode, compile-time K, M.  The survivor set follows from the erasure mask alone --
@@ -606,13 +546,10 @@ k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint32_t* __restrict__ records) {
     // __restrict__ parameters: the LUT and records are provably not written by this
     // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
-    // IMPL 9: IMPL 4 (12-B lanes) with the survivors loaded in halves; IMPL 10: IMPL 8 likewise
-    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8 || IMPL_ == 10) ? 3 : IMPL_ == 9 ? 4 : IMPL_;
-    constexpr bool HV = IMPL_ == 9 || IMPL_ == 10;
+    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8) ? 3 : IMPL_;
     constexpr int N = K + M;
     const int lane = threadIdx.x & 63;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * ((IMPL_ == 8 || IMPL_ == 10) ? a.wpg8 : 4u) +
-                                                        (threadIdx.x >> 6));
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (IMPL_ == 8 ? a.wpg8 : 4u) + (threadIdx.x >> 6));
     const uint32_t wpg = IMPL == 5 ? 1u : IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
@@ -654,10 +591,8 @@ k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
     if (col < (IMPL == 3 ? a.cols8 : IMPL == 4 ? a.cols12 : a.cols)) {
         if constexpr (CT != 0) {
             if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 16u);
-            else if (IMPL == 3)
-                recon_column_by_e<K, M, 2, RTab<1>, M, HV>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 8u);
-            else if (IMPL == 4)
-                recon_column_by_e<K, M, 3, RTab<1>, M, HV>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 12u);
+            else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 8u);
+            else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 12u);
         } else if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 16u);
         else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 8u);
         else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 12u);
@@ -826,8 +761,7 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 
 #define QFEC_REC_LAUNCH(KK, MM, AR)                                                                        \
     do {                                                                                                   \
-        const dim3 blk((AR == 8 || AR == 10) ? 64u * a.wpg8 : 256u),                                     \
-            grd((AR == 8 || AR == 10) ? (unsigned)a.groups : pgrid);                                       \
+        const dim3 blk(AR == 8 ? 64u * a.wpg8 : 256u), grd(AR == 8 ? (unsigned)a.groups : pgrid);          \
         if (AR >= 2 && a.compact && a.t256)                                                                \
             hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, (AR >= 2) * 1>), grd, blk, 0, stream, a,   \
                                a.data, a.parity, a.marks, a.lut, a.records);                               \
@@ -843,16 +777,13 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
         const bool wide8 = KK >= 10 && fill8 >= fill16 - 0.01;                     \
         int im = a.impl < 0 ? (KK * MM <= 64 ? (KK * MM <= 30 && lanes12 ? 4 : (lanes8 || wide8) ? 3 : 2) : 0) \
                             : a.impl;                                              \
-        if ((im == 4 || im == 9) && !lanes12_ok) im = 2;                           \
-        if (im == 10 && (a.wpg8 < 1 || a.wpg8 > 4)) im = 3;                        \
-        const unsigned pgrid = im == 5 ? grid : (im == 3 || im == 6) ? pgrid8 : (im == 4 || im == 9) ? pgrid12 : pgrid16; \
+        if (im == 4 && !lanes12_ok) im = 2;                                        \
+        const unsigned pgrid = im == 5 ? grid : (im == 3 || im == 6) ? pgrid8 : im == 4 ? pgrid12 : pgrid16; \
         /* 8-B lanes run one group per block where a group is at most 4 waves: its slab */ \
         /* waves share a CU (RS(16,4) B=1400: 1 218 against 1 224 us, r03blk)            */ \
         if (im == 3 && a.impl < 0) im = 8;                                         \
         if (im == 8 && (a.wpg8 < 1 || a.wpg8 > 4)) im = 3;                         \
-        if (im == 10) QFEC_REC_LAUNCH(KK, MM, 10);                                 \
-        else if (im == 9) QFEC_REC_LAUNCH(KK, MM, 9);                              \
-        else if (im == 8) QFEC_REC_LAUNCH(KK, MM, 8);                              \
+        if (im == 8) QFEC_REC_LAUNCH(KK, MM, 8);                                   \
         else if (im == 6) QFEC_REC_LAUNCH(KK, MM, 6);                              \
         else if (im == 5) QFEC_REC_LAUNCH(KK, MM, 5);                              \
         else if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                              \

@@ -886,7 +886,7 @@ int qfec_get_kernel_variant(void) { return g_variant.load(); }
 // experiment knobs, for A/B timing in one process (tools/ab.py); not needed in production
 int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
-    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 10 && value != 7) { tuning().recon_impl = value; return QFEC_OK; }
+    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 8 && value != 7) { tuning().recon_impl = value; return QFEC_OK; }
     if (!strcmp(key, "host_chunk") && value >= 0) { tuning().host_chunk = value; return QFEC_OK; }
     if (!strcmp(key, "encode_impl") && value >= -1 && value <= 2) { tuning().encode_impl = value; return QFEC_OK; }
     if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }

@@ -102,8 +102,6 @@ def main():
         ("recon impl5 (one wave per group, 8-B slabs)", lambda: qa.tune("recon_impl", 5), rec, dec_bytes),
         ("recon impl6 (impl3 at 8 waves/SIMD)", lambda: qa.tune("recon_impl", 6), rec, dec_bytes),
         ("recon impl8 (impl3, one group per block)", lambda: qa.tune("recon_impl", 8), rec, dec_bytes),
-        ("recon impl9 (impl4, survivors in halves)", lambda: qa.tune("recon_impl", 9), rec, dec_bytes),
-        ("recon impl10 (impl8, survivors in halves)", lambda: qa.tune("recon_impl", 10), rec, dec_bytes),
     ]
     if a.recon_only:
         variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]
