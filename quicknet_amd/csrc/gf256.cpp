@@ -269,11 +269,12 @@ void build_record(const RecordLayout& L, int k, int e, const uint8_t* rows, cons
             out[L.coff + j * k + c] = (uint32_t)rows[(size_t)j * k + c] * (QFEC_TAB_STRIDE * 4);
         }
     // module/rs.c:116-117: a zero column-0 coefficient leaves the output's bytes in place
+    // (flag in the row's first table; word 1 holds the same flags as a bit per row)
     if (rs_quirk)
         for (int j = 0; j < e; ++j)
             if (rows[(size_t)j * k] == 0) {
                 out[L.hdr + ((size_t)j * k) * QFEC_TAB_STRIDE + 5] = 1;
-                out[L.coff + j * k] |= 1u;
+                out[1] |= 1u << j;
             }
 }
 

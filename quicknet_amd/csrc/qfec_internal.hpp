@@ -199,9 +199,10 @@ int decode_rows(const uint8_t* parity_rows, int k, int m, const uint8_t* marks_n
                 std::vector<uint8_t>& rows, std::vector<int>& survivors, std::vector<int>& lost,
                 const uint8_t* full = nullptr);
 
-// Record: [0] e, [surv_off + c] survivor shard id, [lost_off + j] erased data row,
+// Record: [0] e, [1] rs.c quirk flags (bit j: row j's column-0 coefficient is zero),
+// [surv_off + c] survivor shard id, [lost_off + j] erased data row,
 // [coff + j*k + c] byte offset of coefficient (j, c)'s perm table in the 256-entry table
-// (c * 32; bit 0 on column 0 = the rs.c quirk flag), then from [hdr] the tables themselves
+// (value * 32), then from [hdr] the tables themselves
 // ([j][c][QFEC_TAB_STRIDE]).  A kernel that reads the offsets touches only the record's
 // first (coff + m*k) words, so the records of every pattern stay cache-resident.
 struct RecordLayout {

@@ -442,12 +442,18 @@ __device__ __forceinline__ void ldv_plain(uint32_t (&v)[D], const uint8_t* p) {
 // byte offsets the record's header lists (RecordLayout::coff).  The compact form reads only
 // the record's header, so the records of all patterns stay cache-resident (RS(16,4): 4 844
 // records of 2.4 KB would not fit the 4 MB L2; their headers do).
+// The tables are read through the constant address space: loads from it are scalar (SMEM)
+// whatever stores the kernel makes, also inside a loop over items (recon_impl 9), where the
+// clobber analysis would turn global-address loads into per-lane vector loads.
+typedef const __attribute__((address_space(4))) uint32_t* cptr32;
+typedef const __attribute__((address_space(4))) uint8_t* cptr8;
 template <int CT>
 struct RTab;
 template <>
 struct RTab<0> {
-    const uint32_t* __restrict__ tab;
-    __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const { return tab + (j * K + c) * QFEC_TAB_STRIDE; }
+    cptr32 tab;
+    __device__ RTab(const uint32_t* t) : tab((cptr32)t) {}
+    __device__ __forceinline__ cptr32 at(int j, int c, int K) const { return tab + (j * K + c) * QFEC_TAB_STRIDE; }
     __device__ __forceinline__ bool quirk(int j, int K) const { return tab[(j * K) * QFEC_TAB_STRIDE + 5] != 0; }
     __device__ __forceinline__ void load5(int j, int c, int K, uint32_t (&t5)[5]) const {
 #pragma unroll
@@ -456,12 +462,15 @@ struct RTab<0> {
 };
 template <>
 struct RTab<1> {
-    const uint32_t* __restrict__ offs;
-    const uint32_t* __restrict__ t256;
-    __device__ __forceinline__ const uint32_t* at(int j, int c, int K) const {
-        return reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t256) + (offs[j * K + c] & ~31u));
+    cptr32 rec;  // the record: [1] quirk flags, [coff + j*K + c] table byte offsets
+    cptr32 offs;
+    cptr32 t256;
+    __device__ RTab(const uint32_t* r, int coff, const uint32_t* t)
+        : rec((cptr32)r), offs((cptr32)r + coff), t256((cptr32)t) {}
+    __device__ __forceinline__ cptr32 at(int j, int c, int K) const {
+        return (cptr32)((cptr8)t256 + offs[j * K + c]);
     }
-    __device__ __forceinline__ bool quirk(int j, int K) const { return (offs[j * K] & 1u) != 0; }
+    __device__ __forceinline__ bool quirk(int j, int K) const { return (rec[1] >> j) & 1u; }
     __device__ __forceinline__ void load5(int j, int c, int K, uint32_t (&t5)[5]) const {
 #pragma unroll
         for (int i = 0; i < 5; ++i) t5[i] = at(j, c, K)[i];
@@ -537,19 +546,12 @@ __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K]
 // IMPL 6: IMPL 3 compiled for 8 waves per SIMD (register caps; 7 otherwise: 106 SGPRs)
 // IMPL 8: IMPL 3 launched with one group per block (blocks of wpg8 waves), so a group's slab
 // waves share a CU and its scalar data (marks, LUT entry, record header, tables)
-template <int K, int M, int IMPL_, int CT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMPL_ == 6 ? 8 : 1)))
-k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
-                                                          const uint8_t* __restrict__ parity,
-                                                          const uint8_t* __restrict__ marks,
-                                                          const int32_t* __restrict__ lut,
-                                                          const uint32_t* __restrict__ records) {
-    // __restrict__ parameters: the LUT and records are provably not written by this
-    // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
-    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8) ? 3 : IMPL_;
+template <int K, int M, int IMPL, int CT>
+__device__ __forceinline__ void recon_item(const ReconArgs& a, uint8_t* __restrict__ data,
+                                           const uint8_t* __restrict__ parity, const uint8_t* __restrict__ marks,
+                                           const int32_t* __restrict__ lut, const uint32_t* __restrict__ records,
+                                           uint32_t wid, int lane) {
     constexpr int N = K + M;
-    const int lane = threadIdx.x & 63;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (IMPL_ == 8 ? a.wpg8 : 4u) + (threadIdx.x >> 6));
     const uint32_t wpg = IMPL == 5 ? 1u : IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
@@ -566,10 +568,10 @@ k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
         if (part == 0 && lane == 0 && a.failed) atomicAdd(a.failed, 1u);
         return;
     }
-    const int rec = __builtin_amdgcn_readfirstlane(lut[mask]);
+    const int rec = ((const __attribute__((address_space(4))) int32_t*)lut)[mask];
     const uint32_t* tab = records + rec + a.hdr;
     const RTab<0> TD{tab};
-    const RTab<1> TC{records + rec + a.coff, a.t256};
+    const RTab<1> TC{records + rec, a.coff, a.t256};
     const uint64_t pitch = a.pitch;
     uint8_t* data_g = data + g * a.dgs;
     const uint8_t* par_g = parity + g * a.pgs;
@@ -599,6 +601,21 @@ k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
         else if (IMPL == 1) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
         else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
     }
+}
+
+template <int K, int M, int IMPL_, int CT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMPL_ == 6 ? 8 : 1)))
+k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
+                                                          const uint8_t* __restrict__ parity,
+                                                          const uint8_t* __restrict__ marks,
+                                                          const int32_t* __restrict__ lut,
+                                                          const uint32_t* __restrict__ records) {
+    // __restrict__ parameters: the LUT and records are provably not written by this
+    // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
+    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8) ? 3 : IMPL_;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (IMPL_ == 8 ? a.wpg8 : 4u) + (threadIdx.x >> 6));
+    recon_item<K, M, IMPL, CT>(a, data, parity, marks, lut, records, wid, lane);
 }
 
 // runtime k, e; any vector width via the byte path when the layout is not 16-B aligned

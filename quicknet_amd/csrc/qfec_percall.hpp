@@ -63,6 +63,6 @@ struct PcStatus {                             // coherent pinned host memory, wr
     uint64_t ts[4];
 };
 hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,
-                                 uint32_t gen, uint32_t trace, uint64_t idle_ticks, hipStream_t s);
+                                 uint32_t gen, uint32_t flags, uint64_t idle_ticks, hipStream_t s);
 
 }  // namespace qfec

@@ -225,6 +225,7 @@ std::atomic<int> g_percall_in{0};        // qfec_tune "percall_in": server input
 std::atomic<int> g_percall_idle_us{(int)kPcIdleUsDefault};  // qfec_tune "percall_idle_us": the block's idle exit
 std::atomic<int> g_percall_timeout_us{2000000};  // qfec_tune "percall_timeout_us": give up spinning, wait instead
 std::atomic<int> g_percall_fault{0};     // qfec_tune "percall_fault" (tests): 1 = requests are never handed to a server
+std::atomic<int> g_percall_split{0};  // qfec_tune "percall_split": the server's 8-wave layout (qfec_percall.hip)
 std::atomic<int> g_percall_group{1};     // qfec_tune "percall_group": fec_encode computes a group's m rows at once
 constexpr size_t kPcSrvBytes = (size_t)kPcMaxCoef * kPcMaxChunks * 16;
 
@@ -368,9 +369,12 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
         ++s.gen;
         s.launched = true;
         ++s.launches;
-        static const uint32_t trace = getenv("QFEC_PERCALL_TRACE") && atoi(getenv("QFEC_PERCALL_TRACE")) ? 1u : 0u;
+        // QFEC_PERCALL_TRACE: 1 stage times, 2 also serve every request twice and time the second
+        static const int trace_env = getenv("QFEC_PERCALL_TRACE") ? atoi(getenv("QFEC_PERCALL_TRACE")) : 0;
+        static const uint32_t trace = trace_env ? (trace_env == 2 ? 5u : 1u) : 0u;
         const uint64_t idle = (uint64_t)std::max(0, g_percall_idle_us.load()) * 100u;  // 100 MHz wall clock
-        return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, trace, idle,
+        const uint32_t flags = trace | (g_percall_split.load() ? 2u : 0u);  // qfec_percall.hip
+        return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, flags, idle,
                                      s.stream);
     };
     hipError_t he = hipSuccess;
@@ -451,14 +455,26 @@ int ensure_small(DevCtx& c, size_t words) {
 }
 
 // true if p is device (or managed) memory visible to the current device
+// Plain (malloc'd, unregistered) host pointers this thread has probed, a small direct-mapped
+// cache: the per-packet ABIs probe every packet pointer, and a probe costs a runtime lookup
+// (tools/ptr_probe.cpp).  An address the runtime does not know is outside the HSA runtime's
+// device and managed allocations, and those are never placed at it later (they come from the
+// GPU virtual-address apertures the runtime reserves when it starts), so the answer "not device
+// memory" cannot go stale; registering or pinning the block later still leaves it host memory.
 bool is_device_ptr(const void* p) {
     if (!p) return false;
+    thread_local const void* plain[64] = {};
+    const uintptr_t u = (uintptr_t)p;
+    const void*& slot = plain[((u >> 4) ^ (u >> 10) ^ (u >> 16)) & 63u];
+    if (slot == p) return false;
     hipPointerAttribute_t attr;
     hipError_t e = hipPointerGetAttributes(&attr, p);
     if (e != hipSuccess) {
         (void)hipGetLastError();  // clear the sticky error of the probe
+        slot = p;
         return false;
     }
+    if (attr.type == hipMemoryTypeUnregistered) slot = p;
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
@@ -909,10 +925,12 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "percall_group") && (value == 0 || value == 1)) { g_percall_group = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fault") && (value == 0 || value == 1)) { g_percall_fault = value; return QFEC_OK; }
     if (!strcmp(key, "percall_timeout_us") && value >= 0) { g_percall_timeout_us = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_idle_us") && value >= 0 && value <= 1000000) {
-        // a running block keeps the idle time it was launched with: stop it, the next call
-        // launches one with the new value
-        g_percall_idle_us = value;
+    const bool bp_key = !strcmp(key, "percall_split") && (value == 0 || value == 1);
+    if (bp_key || (!strcmp(key, "percall_idle_us") && value >= 0 && value <= 1000000)) {
+        // a running block keeps the idle time / layout it was launched with: stop it, the
+        // next call launches one with the new value
+        if (bp_key) g_percall_split = value;
+        else g_percall_idle_us = value;
         for (DevCtx& c : g_ctx) {
             std::lock_guard<std::mutex> lk(c.mu);
             if (c.srv.usable <= 0 || !c.srv.launched) continue;

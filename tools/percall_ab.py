@@ -22,8 +22,9 @@ def main():
     ap.add_argument("--variants", default="percall_resident=1;percall_resident=0,percall_spin=1;percall_resident=0,percall_spin=0")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=2000)
+    ap.add_argument("--ref", action="store_true", help="also time the reference fec.c per-call on this CPU")
     a = ap.parse_args()
-    res = {v: {"enc": [], "dec": []} for v in a.variants.split(";")}
+    res = {v: {"enc": [], "dec": [], "grp": []} for v in a.variants.split(";")}
     for _ in range(a.rounds):
         for v in res:
             for kv in v.split(","):
@@ -32,9 +33,14 @@ def main():
             out = bench.per_call_leg(reps=a.reps, batched=False)
             res[v]["enc"].append(out["gpu_fec_encode_us"])
             res[v]["dec"].append(out["gpu_fec_decode_us"])
+            res[v]["grp"].append(out.get("gpu_fec_encode_group_us", float("nan")))
+    if a.ref:  # the reference system/fec.c on this box's CPU, same harness (oracle/_ref build)
+        from oracle.oracle import RefCodec
+        out = bench.per_call_leg(reps=a.reps, ref_lib=RefCodec().fec, batched=False)
+        print("reference CPU:", {kk: vv for kk, vv in out.items() if kk.startswith("ref_cpu_")})
     for v, r in res.items():
         print(f"{v:28s} fec_encode {statistics.median(r['enc']):7.2f} us  fec_decode {statistics.median(r['dec']):7.2f} us"
-              f"  (min {min(r['enc']):.2f} / {min(r['dec']):.2f})")
+              f"  group {statistics.median(r['grp']):7.2f} us  (min {min(r['enc']):.2f} / {min(r['dec']):.2f} / {min(r['grp']):.2f})")
 
 
 if __name__ == "__main__":
