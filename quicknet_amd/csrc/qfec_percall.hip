@@ -79,7 +79,7 @@ __device__ __forceinline__ void st_rel_sys(uint32_t* p, uint32_t v) {
 template <int NQ, int KB>
 __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
                                                uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t,
-                                               uint64_t& ts_loaded) {
+                                               uint64_t& ts_loaded, bool nostore = false) {
     const uint32_t lane = t & 63u;
     uint2 x[NQ][KB];
 #pragma unroll
@@ -101,7 +101,7 @@ __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t
     }
     if (ts_loaded) {  // QFEC_PERCALL_TRACE: when every load has landed
         __builtin_amdgcn_s_waitcnt(0);
-        ts_loaded = wall_clock64();
+        ts_loaded = __builtin_amdgcn_s_memtime();
     }
     if ((t & ~63u) >= cols) return;  // a wave with no column (wave-uniform)
     for (uint32_t j0 = 0; j0 < e; j0 += 4) {
@@ -143,7 +143,8 @@ __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     if ((uint32_t)j < ej)
-                        *reinterpret_cast<uint2*>(out + (uint64_t)(j0 + j) * pitch + (uint64_t)col * 8u) = acc[q][j];
+                        if (nostore) asm volatile("" ::"v"(acc[q][j].x), "v"(acc[q][j].y));  // trace 3 only
+                        else *reinterpret_cast<uint2*>(out + (uint64_t)(j0 + j) * pitch + (uint64_t)col * 8u) = acc[q][j];
             }
         }
     }
@@ -151,10 +152,11 @@ __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t
 
 template <int NQ>
 __device__ __forceinline__ void pc_block_serve_k(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
-                                                 uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t, uint64_t& ts) {
-    if (k <= 4) pc_block_serve<NQ, 4>(bell, in, out, k, e, cols, pitch, t, ts);
-    else if (k <= 10) pc_block_serve<NQ, 10>(bell, in, out, k, e, cols, pitch, t, ts);
-    else pc_block_serve<NQ, 16>(bell, in, out, k, e, cols, pitch, t, ts);
+                                                 uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t, uint64_t& ts,
+                                                 bool nostore = false) {
+    if (k <= 4) pc_block_serve<NQ, 4>(bell, in, out, k, e, cols, pitch, t, ts, nostore);
+    else if (k <= 10) pc_block_serve<NQ, 10>(bell, in, out, k, e, cols, pitch, t, ts, nostore);
+    else pc_block_serve<NQ, 16>(bell, in, out, k, e, cols, pitch, t, ts, nostore);
 }
 
 // SPLIT layout (tuning "percall_split" 1): a block of 8 waves, two per SIMD.  A wave alone on
@@ -198,7 +200,7 @@ __device__ __forceinline__ void pc_split_serve(const PcBell* bell, const uint8_t
     }
     if (ts_loaded) {  // QFEC_PERCALL_TRACE: when every load has landed
         __builtin_amdgcn_s_waitcnt(0);
-        ts_loaded = wall_clock64();
+        ts_loaded = __builtin_amdgcn_s_memtime();
     }
     if (busy) {
         for (uint32_t j0 = 0; j0 < e; j0 += 4) {
@@ -282,7 +284,11 @@ k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, ui
         }
         __syncthreads();
         if (s_quit) break;
-        const uint64_t ts0 = trace ? wall_clock64() : 0;
+        // QFEC_PERCALL_TRACE stage stamps in shader clocks (s_memtime, read in the CU): a
+        // s_memrealtime read takes a round trip of its own that would land in the stage it
+        // brackets; two wall-clock reads at the ends calibrate the clock
+        const uint64_t rt0 = trace ? wall_clock64() : 0;
+        const uint64_t ts0 = trace ? __builtin_amdgcn_s_memtime() : 0;
         const uint64_t b = s_bell;
         const uint32_t r = (uint32_t)b, k = (uint32_t)(b >> 32) & 0xFFu, e = (uint32_t)(b >> 40) & 0xFFu,
                        chunks = (uint32_t)(b >> 48) + 1u, pitch = chunks * 16u, cols = chunks * 2u;
@@ -307,18 +313,22 @@ k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, ui
             else if (per <= 4) pc_split_serve<4>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts1);
             else if (per <= 8) pc_split_serve<8>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts1);
             else pc_split_serve<16>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts1);
+        } else if (flags & 8u) {  // QFEC_PERCALL_TRACE=3 (diagnostic, outputs not written): the stores' share
+            if (cols <= 256) pc_block_serve_k<1>(bell, in, out, k, e, cols, pitch, t, ts1, true);
+            else pc_block_serve_k<2>(bell, in, out, k, e, cols, pitch, t, ts1, true);
         } else {
             if (cols <= 256) pc_block_serve_k<1>(bell, in, out, k, e, cols, pitch, t, ts1);
             else pc_block_serve_k<2>(bell, in, out, k, e, cols, pitch, t, ts1);
         }
-        const uint64_t ts2 = trace ? wall_clock64() : 0;
+        const uint64_t ts2 = trace ? __builtin_amdgcn_s_memtime() : 0;
         __threadfence_system();  // every lane's outputs reach the host before the completion word
         __syncthreads();         // (and s_bell is not rewritten before every lane has read it)
         if (trace && t == 0) {
             st->ts[0] = ts0;
             st->ts[1] = ts1;
             st->ts[2] = ts2;
-            st->ts[3] = wall_clock64();
+            st->ts[3] = __builtin_amdgcn_s_memtime();
+            st->rt = wall_clock64() - rt0;
             __threadfence_system();
         }
         if (t == 0) st_rel_sys(&st->done, r);

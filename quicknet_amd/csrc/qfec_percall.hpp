@@ -57,9 +57,10 @@ __host__ __device__ constexpr uint64_t pc_bell(uint32_t req, uint32_t k, uint32_
 struct PcStatus {                             // coherent pinned host memory, written by the block
     uint32_t done;                            // the last request served
     uint32_t state;                           // (launch generation << 1) | running
-    uint32_t pad[6];
-    // QFEC_PERCALL_TRACE=1: wall-clock ticks (100 MHz) of the last request -- seen (twice),
-    // outputs issued, system fence done
+    uint64_t rt;                              // QFEC_PERCALL_TRACE: wall-clock ticks (100 MHz) over ts[0..3]
+    uint32_t pad[4];
+    // QFEC_PERCALL_TRACE=1: shader-clock stamps (s_memtime) of the last request -- seen, inputs
+    // and tables in registers, outputs issued, system fence done
     uint64_t ts[4];
 };
 hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,

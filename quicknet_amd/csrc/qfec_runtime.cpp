@@ -117,7 +117,9 @@ struct DevCtx {
         uint32_t gen = 0;            // the last launch's generation
         bool launched = false;
         unsigned long long calls = 0, launches = 0, relaunches = 0, timeouts = 0;
-        unsigned long long tr[5] = {0, 0, 0, 0, 0};  // QFEC_PERCALL_TRACE sums: invalidate, loads + compute, fence (ticks), host wait (ns), n
+        // QFEC_PERCALL_TRACE sums: loads, compute, fence (shader clocks), host wait (ns), n, clocks and
+        // wall ticks over the traced span (the clock calibration)
+        unsigned long long tr[7] = {0, 0, 0, 0, 0, 0, 0};
     } srv;
     int init_rc = QFEC_ENODEV;
     // qfec_encode_host: two chunk slots, each with its own stream, event, device buffers
@@ -369,9 +371,10 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
         ++s.gen;
         s.launched = true;
         ++s.launches;
-        // QFEC_PERCALL_TRACE: 1 stage times, 2 also serve every request twice and time the second
+        // QFEC_PERCALL_TRACE: 1 stage times, 2 also serve every request twice and time the second,
+        // 3 skip the output stores (diagnostic: the results are wrong)
         static const int trace_env = getenv("QFEC_PERCALL_TRACE") ? atoi(getenv("QFEC_PERCALL_TRACE")) : 0;
-        static const uint32_t trace = trace_env ? (trace_env == 2 ? 5u : 1u) : 0u;
+        static const uint32_t trace = trace_env ? (trace_env == 2 ? 5u : trace_env == 3 ? 9u : 1u) : 0u;
         const uint64_t idle = (uint64_t)std::max(0, g_percall_idle_us.load()) * 100u;  // 100 MHz wall clock
         const uint32_t flags = trace | (g_percall_split.load() ? 2u : 0u);  // qfec_percall.hip
         return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, flags, idle,
@@ -386,10 +389,12 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
     for (uint32_t it = 1; he == hipSuccess; ++it) {
         if (__atomic_load_n(&s.h_st->done, __ATOMIC_ACQUIRE) == req) {
             ++s.calls;
-            if (s.h_st->ts[0]) {  // QFEC_PERCALL_TRACE: sum the device stage times (ticks)
+            if (s.h_st->ts[0]) {  // QFEC_PERCALL_TRACE: sum the device stage times (shader clocks)
                 s.tr[0] += s.h_st->ts[1] - s.h_st->ts[0];
                 s.tr[1] += s.h_st->ts[2] - s.h_st->ts[1];
                 s.tr[2] += s.h_st->ts[3] - s.h_st->ts[2];
+                s.tr[5] += s.h_st->ts[3] - s.h_st->ts[0];
+                s.tr[6] += s.h_st->rt;
                 s.tr[3] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
                 ++s.tr[4];
             }
@@ -426,11 +431,13 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
 
 void pc_server_stop_all() {
     for (DevCtx& c : g_ctx) {
-        if (c.srv.tr[4])  // QFEC_PERCALL_TRACE
-            fprintf(stderr, "[qfec] per-call server, device %d, %llu traced calls: seen -> inputs and tables in %.2f us, "
-                    "compute -> outputs issued %.2f us, system fence %.2f us, host request -> completion "
-                    "seen %.2f us\n", c.device, c.srv.tr[4], c.srv.tr[0] * 0.01 / c.srv.tr[4],
-                    c.srv.tr[1] * 0.01 / c.srv.tr[4], c.srv.tr[2] * 0.01 / c.srv.tr[4], c.srv.tr[3] * 1e-3 / c.srv.tr[4]);
+        if (c.srv.tr[4]) {  // QFEC_PERCALL_TRACE
+            const double n = (double)c.srv.tr[4], ghz = c.srv.tr[6] ? c.srv.tr[5] / (c.srv.tr[6] * 10.0) : 2.4;
+            fprintf(stderr, "[qfec] per-call server, device %d, %llu traced calls (shader clock %.2f GHz): seen -> "
+                    "inputs and tables in %.2f us, compute -> outputs issued %.2f us, system fence %.2f us, host "
+                    "request -> completion seen %.2f us\n", c.device, c.srv.tr[4], ghz, c.srv.tr[0] / n / ghz * 1e-3,
+                    c.srv.tr[1] / n / ghz * 1e-3, c.srv.tr[2] / n / ghz * 1e-3, c.srv.tr[3] * 1e-3 / n);
+        }
         if (c.srv.usable <= 0 || !c.srv.launched) continue;
         int prev = 0;
         (void)hipGetDevice(&prev);
