@@ -76,10 +76,45 @@ __device__ __forceinline__ void st_rel_sys(uint32_t* p, uint32_t v) {
 // k rows (KB - k < 6 rows re-read row k - 1), only lanes inside the packet, all loads issued
 // before any is used (one enclosing branch per group of loads: a branch per load makes the
 // compiler wait for each load before it issues the next).
+// rows j0 .. j0 + E - 1 of the request over the KB (k when KX) inputs in registers
+template <int NQ, int KB, int E, bool KX>
+__device__ __forceinline__ void pc_mac(const uint2 (&x)[NQ][KB], const uint4& ta, uint32_t tb, uint32_t k, uint32_t j0,
+                                       uint2 (&acc)[NQ][4], uint32_t ej = E) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[q][j] = make_uint2(0, 0);
+#pragma unroll
+    for (int i = 0; i < KB; ++i) {
+        if (!KX && (uint32_t)i >= k) continue;  // wave-uniform
+        Sel sl[NQ][2];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            sl[q][0] = gf_sel(x[q][i].x);
+            sl[q][1] = gf_sel(x[q][i].y);
+        }
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+            if ((uint32_t)j >= ej) continue;  // the generic body only (ej == E otherwise)
+            const int c = (int)((j0 + j) * (KX ? (uint32_t)KB : k) + i);  // wave-uniform
+            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)ta.x, c),
+                           t1 = (uint32_t)__builtin_amdgcn_readlane((int)ta.y, c),
+                           t2 = (uint32_t)__builtin_amdgcn_readlane((int)ta.z, c),
+                           t3 = (uint32_t)__builtin_amdgcn_readlane((int)ta.w, c),
+                           t4 = (uint32_t)__builtin_amdgcn_readlane((int)tb, c);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                acc[q][j].x = xor3(acc[q][j].x, pp0(sl[q][0], t0, t1), pp1(sl[q][0], t2, t3)) ^ pp2(sl[q][0], t4);
+                acc[q][j].y = xor3(acc[q][j].y, pp0(sl[q][1], t0, t1), pp1(sl[q][1], t2, t3)) ^ pp2(sl[q][1], t4);
+            }
+        }
+    }
+}
+
 template <int NQ, int KB>
 __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
                                                uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t,
-                                               uint64_t& ts_loaded, bool nostore = false) {
+                                               uint64_t& ts_loaded) {
     const uint32_t lane = t & 63u;
     uint2 x[NQ][KB];
 #pragma unroll
@@ -104,37 +139,23 @@ __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t
         ts_loaded = __builtin_amdgcn_s_memtime();
     }
     if ((t & ~63u) >= cols) return;  // a wave with no column (wave-uniform)
+    const bool kx = k == (uint32_t)KB;
     for (uint32_t j0 = 0; j0 < e; j0 += 4) {
         const uint32_t ej = min(4u, e - j0);
         uint2 acc[NQ][4];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[q][j] = make_uint2(0, 0);
-#pragma unroll
-        for (int i = 0; i < KB; ++i) {
-            if ((uint32_t)i >= k) continue;
-            Sel sl[NQ][2];
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                sl[q][0] = gf_sel(x[q][i].x);
-                sl[q][1] = gf_sel(x[q][i].y);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if ((uint32_t)j >= ej) continue;
-                const int c = (int)((j0 + j) * k + i);  // wave-uniform
-                const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)ta.x, c),
-                               t1 = (uint32_t)__builtin_amdgcn_readlane((int)ta.y, c),
-                               t2 = (uint32_t)__builtin_amdgcn_readlane((int)ta.z, c),
-                               t3 = (uint32_t)__builtin_amdgcn_readlane((int)ta.w, c),
-                               t4 = (uint32_t)__builtin_amdgcn_readlane((int)tb, c);
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) {
-                    acc[q][j].x = xor3(acc[q][j].x, pp0(sl[q][0], t0, t1), pp1(sl[q][0], t2, t3)) ^ pp2(sl[q][0], t4);
-                    acc[q][j].y = xor3(acc[q][j].y, pp0(sl[q][1], t0, t1), pp1(sl[q][1], t2, t3)) ^ pp2(sl[q][1], t4);
-                }
-            }
+        // straight-line bodies for the chunk's exact row count (and k == KB): no branch between
+        // coefficients, so the table reads of the next coefficient overlap this one's multiply
+        if constexpr (NQ != 1) {  // rows over 2 KiB: one generic body
+            pc_mac<NQ, KB, 4, false>(x, ta, tb, k, j0, acc, ej);
+        } else switch (ej * 2u + (kx ? 1u : 0u)) {
+            case 2: pc_mac<NQ, KB, 1, false>(x, ta, tb, k, j0, acc); break;
+            case 3: pc_mac<NQ, KB, 1, true>(x, ta, tb, k, j0, acc); break;
+            case 4: pc_mac<NQ, KB, 2, false>(x, ta, tb, k, j0, acc); break;
+            case 5: pc_mac<NQ, KB, 2, true>(x, ta, tb, k, j0, acc); break;
+            case 6: pc_mac<NQ, KB, 3, false>(x, ta, tb, k, j0, acc); break;
+            case 7: pc_mac<NQ, KB, 3, true>(x, ta, tb, k, j0, acc); break;
+            case 8: pc_mac<NQ, KB, 4, false>(x, ta, tb, k, j0, acc); break;
+            default: pc_mac<NQ, KB, 4, true>(x, ta, tb, k, j0, acc); break;
         }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -143,8 +164,7 @@ __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     if ((uint32_t)j < ej)
-                        if (nostore) asm volatile("" ::"v"(acc[q][j].x), "v"(acc[q][j].y));  // trace 3 only
-                        else *reinterpret_cast<uint2*>(out + (uint64_t)(j0 + j) * pitch + (uint64_t)col * 8u) = acc[q][j];
+                        *reinterpret_cast<uint2*>(out + (uint64_t)(j0 + j) * pitch + (uint64_t)col * 8u) = acc[q][j];
             }
         }
     }
@@ -152,115 +172,21 @@ __device__ __forceinline__ void pc_block_serve(const PcBell* bell, const uint8_t
 
 template <int NQ>
 __device__ __forceinline__ void pc_block_serve_k(const PcBell* bell, const uint8_t* in, uint8_t* out, uint32_t k,
-                                                 uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t, uint64_t& ts,
-                                                 bool nostore = false) {
-    if (k <= 4) pc_block_serve<NQ, 4>(bell, in, out, k, e, cols, pitch, t, ts, nostore);
-    else if (k <= 10) pc_block_serve<NQ, 10>(bell, in, out, k, e, cols, pitch, t, ts, nostore);
-    else pc_block_serve<NQ, 16>(bell, in, out, k, e, cols, pitch, t, ts, nostore);
-}
-
-// SPLIT layout (tuning "percall_split" 1): a block of 8 waves, two per SIMD.  A wave alone on
-// its SIMD issues a VALU instruction every ~5 cycles and two interleave to ~2.6
-// (tools/valu_rate.hip, profiles/r04i/valu_rate.txt), and the multiply is the longest stage of a
-// call (2.3 us of RS(10,3) group's 3 rows: the QFEC_PERCALL_TRACE table in DESIGN §7).  Wave w
-// takes 64-column slab w % nslab and the inputs [h k / nh, (h + 1) k / nh) of split h = w / nslab
-// for all e rows; every wave leaves its partial rows in LDS and the block XORs the nh partials of
-// each (row, column) into the output.
-constexpr int kPcSplitWaves = 8;
-constexpr int kPcSplitLds = 6144;  // uint2 partials: nh * e * cols <= 6144 (48 KB)
-__device__ __forceinline__ void pc_split_shape(uint32_t k, uint32_t e, uint32_t cols, uint32_t& nslab, uint32_t& nh) {
-    nslab = (cols + 63u) / 64u;
-    nh = max(1u, min(k, (uint32_t)kPcSplitWaves / nslab));
-    while (nh > 1u && nh * e * cols > (uint32_t)kPcSplitLds) --nh;
-}
-template <int KB>
-__device__ __forceinline__ void pc_split_serve(const PcBell* bell, const uint8_t* in, uint8_t* out, uint2* part,
-                                               uint32_t k, uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t,
-                                               uint32_t nslab, uint32_t nh, uint64_t& ts_loaded) {
-    const uint32_t lane = t & 63u, w = __builtin_amdgcn_readfirstlane(t >> 6);
-    const uint32_t s = w % nslab, h = w / nslab;  // wave-uniform (SGPRs)
-    const bool busy = h < nh;
-    const uint32_t c0 = busy ? h * k / nh : 0u, ni = busy ? (h + 1u) * k / nh - c0 : 0u;
-    const uint32_t col = s * 64u + lane;
-    const bool inside = busy && col < cols;
-    uint2 x[KB];
-#pragma unroll
-    for (int i = 0; i < KB; ++i) x[i] = make_uint2(0, 0);
-    if (inside) {  // all loads issued before any is used (rows past ni re-read the last one)
-#pragma unroll
-        for (int i = 0; i < KB; ++i)
-            x[i] = *reinterpret_cast<const uint2*>(in + (uint64_t)(c0 + min((uint32_t)i, ni - 1u)) * pitch +
-                                                   (uint64_t)col * 8u);
-    }
-    uint4 ta = make_uint4(0, 0, 0, 0);  // coefficient `lane`: table dwords 0-3, then 4
-    uint32_t tb = 0;
-    if (lane < k * e) {
-        ta = *reinterpret_cast<const uint4*>(bell->tab + 8u * lane);
-        tb = bell->tab[8u * lane + 4u];
-    }
-    if (ts_loaded) {  // QFEC_PERCALL_TRACE: when every load has landed
-        __builtin_amdgcn_s_waitcnt(0);
-        ts_loaded = __builtin_amdgcn_s_memtime();
-    }
-    if (busy) {
-        for (uint32_t j0 = 0; j0 < e; j0 += 4) {
-            const uint32_t ej = min(4u, e - j0);
-            uint2 acc[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[j] = make_uint2(0, 0);
-#pragma unroll
-            for (int i = 0; i < KB; ++i) {
-                if ((uint32_t)i >= ni) continue;  // wave-uniform
-                const Sel s0 = gf_sel(x[i].x), s1 = gf_sel(x[i].y);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if ((uint32_t)j >= ej) continue;
-                    const int c = (int)((j0 + j) * k + c0 + i);  // wave-uniform
-                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)ta.x, c),
-                                   t1 = (uint32_t)__builtin_amdgcn_readlane((int)ta.y, c),
-                                   t2 = (uint32_t)__builtin_amdgcn_readlane((int)ta.z, c),
-                                   t3 = (uint32_t)__builtin_amdgcn_readlane((int)ta.w, c),
-                                   t4 = (uint32_t)__builtin_amdgcn_readlane((int)tb, c);
-                    acc[j].x = xor3(acc[j].x, pp0(s0, t0, t1), pp1(s0, t2, t3)) ^ pp2(s0, t4);
-                    acc[j].y = xor3(acc[j].y, pp0(s1, t0, t1), pp1(s1, t2, t3)) ^ pp2(s1, t4);
-                }
-            }
-            if (col < cols) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if ((uint32_t)j >= ej) continue;
-                    if (nh == 1u) *reinterpret_cast<uint2*>(out + (uint64_t)(j0 + j) * pitch + (uint64_t)col * 8u) = acc[j];
-                    else part[(h * e + j0 + j) * cols + col] = acc[j];
-                }
-            }
-        }
-    }
-    if (nh > 1u) {  // block-uniform
-        __syncthreads();
-        for (uint32_t i = t; i < e * cols; i += 64u * kPcSplitWaves) {
-            const uint32_t j = i / cols, cc = i - j * cols;
-            uint2 v = part[j * cols + cc];
-            for (uint32_t hh = 1; hh < nh; ++hh) {
-                const uint2 p = part[(hh * e + j) * cols + cc];
-                v.x ^= p.x;
-                v.y ^= p.y;
-            }
-            *reinterpret_cast<uint2*>(out + (uint64_t)j * pitch + (uint64_t)cc * 8u) = v;
-        }
-    }
+                                                 uint32_t e, uint32_t cols, uint32_t pitch, uint32_t t, uint64_t& ts) {
+    if (k <= 4) pc_block_serve<NQ, 4>(bell, in, out, k, e, cols, pitch, t, ts);
+    else if (k <= 10) pc_block_serve<NQ, 10>(bell, in, out, k, e, cols, pitch, t, ts);
+    else pc_block_serve<NQ, 16>(bell, in, out, k, e, cols, pitch, t, ts);
 }
 
 // Lane 0 polls the 8-byte request word (system-scope loads that bypass the caches), which carries
 // the call's shape, and after it a system-scope acquire fence invalidates the caches, so the block
 // then reads what the CPU wrote before the word.  Every iteration ends in the same place for
 // every lane, and the loop exits on idle or stop, so the grid always drains.
-template <bool SPLIT>
-__global__ void __launch_bounds__(SPLIT ? 64 * kPcSplitWaves : 256)
+__global__ void __launch_bounds__(256)
 k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served, uint32_t gen,
                  uint32_t flags, uint64_t idle_ticks) {
     const uint32_t trace = flags & 1u;
     __shared__ uint64_t s_bell;
-    __shared__ uint2 s_part[SPLIT ? kPcSplitLds : 1];
     __shared__ uint32_t s_quit;
     const uint32_t t = threadIdx.x;
     if (t == 0) st_rel_sys(&st->state, (gen << 1) | 1u);
@@ -293,33 +219,8 @@ k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, ui
         const uint32_t r = (uint32_t)b, k = (uint32_t)(b >> 32) & 0xFFu, e = (uint32_t)(b >> 40) & 0xFFu,
                        chunks = (uint32_t)(b >> 48) + 1u, pitch = chunks * 16u, cols = chunks * 2u;
         uint64_t ts1 = trace;
-        if (flags & 4u) {  // QFEC_PERCALL_TRACE=2: the request served twice, the second one timed
-            uint64_t ts_first = 0;
-            if constexpr (SPLIT) {
-                uint32_t nslab, nh;
-                pc_split_shape(k, e, cols, nslab, nh);
-                pc_split_serve<16>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts_first);
-            } else {
-                if (cols <= 256) pc_block_serve_k<1>(bell, in, out, k, e, cols, pitch, t, ts_first);
-                else pc_block_serve_k<2>(bell, in, out, k, e, cols, pitch, t, ts_first);
-            }
-            __syncthreads();
-        }
-        if constexpr (SPLIT) {
-            uint32_t nslab, nh;
-            pc_split_shape(k, e, cols, nslab, nh);
-            const uint32_t per = (k + nh - 1u) / nh;  // inputs of the largest split
-            if (per <= 2) pc_split_serve<2>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts1);
-            else if (per <= 4) pc_split_serve<4>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts1);
-            else if (per <= 8) pc_split_serve<8>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts1);
-            else pc_split_serve<16>(bell, in, out, s_part, k, e, cols, pitch, t, nslab, nh, ts1);
-        } else if (flags & 8u) {  // QFEC_PERCALL_TRACE=3 (diagnostic, outputs not written): the stores' share
-            if (cols <= 256) pc_block_serve_k<1>(bell, in, out, k, e, cols, pitch, t, ts1, true);
-            else pc_block_serve_k<2>(bell, in, out, k, e, cols, pitch, t, ts1, true);
-        } else {
-            if (cols <= 256) pc_block_serve_k<1>(bell, in, out, k, e, cols, pitch, t, ts1);
-            else pc_block_serve_k<2>(bell, in, out, k, e, cols, pitch, t, ts1);
-        }
+        if (cols <= 256) pc_block_serve_k<1>(bell, in, out, k, e, cols, pitch, t, ts1);
+        else pc_block_serve_k<2>(bell, in, out, k, e, cols, pitch, t, ts1);
         const uint64_t ts2 = trace ? __builtin_amdgcn_s_memtime() : 0;
         __threadfence_system();  // every lane's outputs reach the host before the completion word
         __syncthreads();         // (and s_bell is not rewritten before every lane has read it)
@@ -340,12 +241,7 @@ k_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, ui
 
 hipError_t launch_percall_server(PcBell* bell, const uint8_t* in, uint8_t* out, PcStatus* st, uint32_t served,
                                  uint32_t gen, uint32_t flags, uint64_t idle_ticks, hipStream_t s) {
-    if (flags & 2u)
-        hipLaunchKernelGGL(k_percall_server<true>, dim3(1), dim3(64 * kPcSplitWaves), 0, s, bell, in, out, st, served,
-                           gen, flags, idle_ticks);
-    else
-        hipLaunchKernelGGL(k_percall_server<false>, dim3(1), dim3(256), 0, s, bell, in, out, st, served, gen, flags,
-                           idle_ticks);
+    hipLaunchKernelGGL(k_percall_server, dim3(1), dim3(256), 0, s, bell, in, out, st, served, gen, flags, idle_ticks);
     return hipGetLastError();
 }
 

@@ -227,7 +227,6 @@ std::atomic<int> g_percall_in{0};        // qfec_tune "percall_in": server input
 std::atomic<int> g_percall_idle_us{(int)kPcIdleUsDefault};  // qfec_tune "percall_idle_us": the block's idle exit
 std::atomic<int> g_percall_timeout_us{2000000};  // qfec_tune "percall_timeout_us": give up spinning, wait instead
 std::atomic<int> g_percall_fault{0};     // qfec_tune "percall_fault" (tests): 1 = requests are never handed to a server
-std::atomic<int> g_percall_split{0};  // qfec_tune "percall_split": the server's 8-wave layout (qfec_percall.hip)
 std::atomic<int> g_percall_group{1};     // qfec_tune "percall_group": fec_encode computes a group's m rows at once
 constexpr size_t kPcSrvBytes = (size_t)kPcMaxCoef * kPcMaxChunks * 16;
 
@@ -371,12 +370,9 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
         ++s.gen;
         s.launched = true;
         ++s.launches;
-        // QFEC_PERCALL_TRACE: 1 stage times, 2 also serve every request twice and time the second,
-        // 3 skip the output stores (diagnostic: the results are wrong)
-        static const int trace_env = getenv("QFEC_PERCALL_TRACE") ? atoi(getenv("QFEC_PERCALL_TRACE")) : 0;
-        static const uint32_t trace = trace_env ? (trace_env == 2 ? 5u : trace_env == 3 ? 9u : 1u) : 0u;
+        static const uint32_t trace = getenv("QFEC_PERCALL_TRACE") && atoi(getenv("QFEC_PERCALL_TRACE")) ? 1u : 0u;
         const uint64_t idle = (uint64_t)std::max(0, g_percall_idle_us.load()) * 100u;  // 100 MHz wall clock
-        const uint32_t flags = trace | (g_percall_split.load() ? 2u : 0u);  // qfec_percall.hip
+        const uint32_t flags = trace;  // bit 0: QFEC_PERCALL_TRACE (qfec_percall.hip)
         return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, flags, idle,
                                      s.stream);
     };
@@ -932,12 +928,10 @@ int qfec_tune(const char* key, int value) {
     if (!strcmp(key, "percall_group") && (value == 0 || value == 1)) { g_percall_group = value; return QFEC_OK; }
     if (!strcmp(key, "percall_fault") && (value == 0 || value == 1)) { g_percall_fault = value; return QFEC_OK; }
     if (!strcmp(key, "percall_timeout_us") && value >= 0) { g_percall_timeout_us = value; return QFEC_OK; }
-    const bool bp_key = !strcmp(key, "percall_split") && (value == 0 || value == 1);
-    if (bp_key || (!strcmp(key, "percall_idle_us") && value >= 0 && value <= 1000000)) {
-        // a running block keeps the idle time / layout it was launched with: stop it, the
-        // next call launches one with the new value
-        if (bp_key) g_percall_split = value;
-        else g_percall_idle_us = value;
+    if (!strcmp(key, "percall_idle_us") && value >= 0 && value <= 1000000) {
+        // a running block keeps the idle time it was launched with: stop it, the next call
+        // launches one with the new value
+        g_percall_idle_us = value;
         for (DevCtx& c : g_ctx) {
             std::lock_guard<std::mutex> lk(c.mu);
             if (c.srv.usable <= 0 || !c.srv.launched) continue;
