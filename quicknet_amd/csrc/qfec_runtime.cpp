@@ -331,10 +331,23 @@ hipError_t pc_server_stop(DevCtx& c) {
 // pc_server_call's answer when the request was not served: the caller runs it another way
 constexpr int kPcNotServed = 1;
 
+// CPU work a per-call path runs while the device serves the request (once, in every path)
+struct Overlap {
+    void (*fn)(void*) = nullptr;
+    void* arg = nullptr;
+    bool done = false;
+    void run() {
+        if (fn && !done) {
+            done = true;
+            fn(arg);
+        }
+    }
+};
+
 // one call through the server: QFEC_OK, kPcNotServed (the server is stopped and the request is
 // still the caller's to serve), or an error (the server then is stopped)
 int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, unsigned char* const* in,
-                   unsigned char* const* out, int sz, size_t pitch) {
+                   unsigned char* const* out, int sz, size_t pitch, Overlap* ov = nullptr) {
     DevCtx::PcServer& s = c.srv;
     PcBell* b = s.bell;
     const int mode = g_percall_in.load();
@@ -380,6 +393,7 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
     const bool fault = g_percall_fault.load() != 0;  // test hook: as if no server ever got a CU
     if (fault) (void)pc_server_stop(c);
     else if (!pc_server_alive(s)) he = launch();
+    if (ov) ov->run();  // the caller's CPU work, while the request crosses PCIe
     const auto t0 = std::chrono::steady_clock::now();
     const auto limit = std::chrono::microseconds(g_percall_timeout_us.load());
     for (uint32_t it = 1; he == hipSuccess; ++it) {
@@ -2279,7 +2293,13 @@ constexpr size_t kFecDecCacheMax = 4096;
 // run `rows` (e x k coefficient rows) over k input packets of sz bytes -> e outputs.  in_dev /
 // out_dev: whether in[0] / out[0] are device memory (-1: find out here)
 int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* const* in, unsigned char* const* out,
-               int sz, int in_dev = -1, int out_dev = -1) {
+               int sz, int in_dev = -1, int out_dev = -1, Overlap* ov = nullptr) {
+    struct RunOnExit {  // the overlap work runs in every path, at the latest on the way out
+        Overlap* o;
+        ~RunOnExit() {
+            if (o) o->run();
+        }
+    } run_on_exit{ov};
     DevCtx* ctx = nullptr;
     int rc = current_ctx(&ctx);
     if (rc) return rc;
@@ -2290,7 +2310,7 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
         // the resident server (packets of up to 4 KiB)
         if (pitch <= (size_t)kPcMaxChunks * 16 && k <= 16 && k * e <= kPcSrvMaxCoef && g_percall_resident.load() &&
             pc_server_setup(*ctx) == QFEC_OK) {
-            rc = pc_server_call(*ctx, tab, k, e, in, out, sz, pitch);
+            rc = pc_server_call(*ctx, tab, k, e, in, out, sz, pitch, ov);
             if (rc != kPcNotServed) return rc;
             // not served within percall_timeout_us: the launch path below serves it
         }
@@ -2435,7 +2455,6 @@ void fec_encode(void* code, unsigned char** src, unsigned char* dst, int index, 
                 h->grp_src.assign(src, src + k);
                 h->grp_in.resize((size_t)k * szz);
                 h->grp_out.resize((size_t)m * szz);
-                for (int i = 0; i < k; ++i) memcpy(h->grp_in.data() + (size_t)i * szz, src[i], szz);
                 {
                     std::lock_guard<std::mutex> lk(h->mu);
                     if (h->enc_all.empty()) {
@@ -2447,10 +2466,23 @@ void fec_encode(void* code, unsigned char** src, unsigned char* dst, int index, 
                 }
                 unsigned char* outs[256];
                 for (int r = 0; r < m; ++r) outs[r] = h->grp_out.data() + (size_t)r * szz;
-                // the copy, not the caller's buffers: the rows belong to the bytes just compared
-                unsigned char* ins[256];
-                for (int i = 0; i < k; ++i) ins[i] = h->grp_in.data() + (size_t)i * szz;
-                const int rc = apply_rows(h->enc_all, k, m, ins, outs, sz, 0, 0);  // both host copies
+                // the inputs are staged for the device from the caller's packets, and the host copy
+                // that later calls compare against is taken while the device computes (the packets
+                // are the caller's and unchanged for the duration of the call)
+                struct Keep {
+                    fec_handle* h;
+                    unsigned char** src;
+                    int k;
+                    size_t sz;
+                    static void copy(void* p) {
+                        const Keep& q = *static_cast<const Keep*>(p);
+                        for (int i = 0; i < q.k; ++i) memcpy(q.h->grp_in.data() + (size_t)i * q.sz, q.src[i], q.sz);
+                    }
+                } keep{h, src, k, szz};
+                Overlap ov;
+                ov.fn = &Keep::copy;
+                ov.arg = &keep;
+                const int rc = apply_rows(h->enc_all, k, m, src, outs, sz, 0, 0, &ov);  // host packets, host rows
                 if (rc) {
                     fprintf(stderr, "[qfec] fec_encode: %s\n", qfec_last_error());
                     return;
