@@ -212,7 +212,8 @@ def test_two_ranks_share_gpu_match_single(oracle):
 
 @pytest.mark.parametrize("fast,spin,resident", [(1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 1, 0)])
 @pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 37), (3, 5, 2052), (16, 20, 1400), (3, 5, 4096),
-                                    (3, 5, 8200), (1, 161, 64), (160, 161, 100), (13, 18, 1028), (17, 19, 200)])
+                                    (3, 5, 8200), (1, 161, 64), (160, 161, 100), (13, 18, 1028), (17, 19, 200),
+                                    (7, 12, 300), (2, 3, 1028), (12, 16, 1028)])
 def test_per_packet_paths_vs_oracle(oracle, fast, spin, resident, k, n, sz):
     """fec_encode / fec_decode on host packets through the resident server (percall_resident 1:
     rows and tables stored into device memory, a request word polled by one resident wave),
@@ -222,7 +223,9 @@ def test_per_packet_paths_vs_oracle(oracle, fast, spin, resident, k, n, sz):
     sz 4096 is the server's largest packet; sz 8200 needs a multi-block launch, which is always
     waited for on the stream; (1, 161) and (160, 161) are the 160-coefficient limit's two ends;
     the server takes k <= 16 and k * e <= 64 ((16, 20) decodes 64 coefficients, (13, 18) 65 and
-    (17, 19) k = 17 go to the one-launch kernel)."""
+    (17, 19) k = 17 go to the one-launch kernel).  The server's straight-line bodies: k == 10 / 4 /
+    16 (exact) and k = 7, 2, 12 (padded), one to four rows per chunk, (7, 12) five rows in two
+    chunks."""
     rng = np.random.default_rng(k * 100 + sz)
     fp = qa.FecParms(k, n)
     full = fp.matrix
