@@ -463,6 +463,40 @@ def cpu_check_host_sample(samples):
             "checker": "reference module/rs.c (oracle/_ref)" if use_ref else "oracle/liboracle.so (C restatement)"}
 
 
+def cpu_check_rs_sample(sm):
+    """The cpu_baseline leg's checker for rs_abi_host: the sampled groups through the reference's
+    own module/rs.c (oracle/_ref; the C restatement oracle/liboracle.so without it) -- its encode
+    must give the parity reed_solomon_encode wrote, and its reconstruct of the same damaged groups
+    the rows reed_solomon_reconstruct restored."""
+    from oracle.oracle import Oracle, RefCodec
+    k, m, B = sm["k"], sm["m"], sm["B"]
+    data, gm = np.ascontiguousarray(sm["data"]), sm["marks_gn"]
+    S = data.shape[0]
+    par = np.zeros((S, m, B), np.uint8)
+    marks = marks_to_rs_layout(gm, k)
+    dmg = data.copy()
+    dmg[gm[:, :k].astype(bool)] = 0x5A
+    if RefCodec.available():
+        ref = RefCodec()
+        h = ref.rs.reed_solomon_new(k, m)
+        ptrs = ref.shard_ptrs(data, par)
+        ref.rs_encode(h, ptrs, S * (k + m), B)
+        ptrs = ref.shard_ptrs(dmg, par)
+        rc = ref.rs_reconstruct(h, ptrs, marks, S * (k + m), B)
+        ref.rs.reed_solomon_release(h)
+        kind = "reference rs.c (oracle/_ref)"
+    else:
+        orc = Oracle()
+        rows = orc.cauchy(k, m)
+        orc.rs_encode(rows, data, par, B)
+        rc = orc.rs_reconstruct(rows, dmg, par, marks, B)
+        kind = "C restatement (oracle/liboracle.so)"
+    par_ok = bool(np.array_equal(par, sm["par"]))
+    rec_ok = bool(np.array_equal(dmg, sm["restored"]))
+    return {"groups": int(S), "checker": kind, "parity_match": par_ok, "restored_match": rec_ok, "rc": int(rc),
+            "match": par_ok and rec_ok and rc == 0}
+
+
 def cpu_config0(budget_s):
     """BASELINE configs[0] literally: RS(10,3) encode of 10 000 x 1 KiB packets (1 000 groups)
     through the reference's own per-packet fec.c, as network/FecCodec.cpp drives it
@@ -1056,6 +1090,17 @@ def main(argv=None):
             host_line = host_encode_leg(code, data, parity, B)
             ok = ok and bool(host_line.get("verified"))
 
+    # module/rs.h unchanged on host shard pointers (the reference's own batched interface), rank 0
+    rs_host = rs_host_sample = None
+    if rank == 0 and not args.no_host:
+        from quicknet_amd.hoststream import rs_abi_host_leg
+        try:
+            rs_host = rs_abi_host_leg()
+            rs_host_sample = rs_host.pop("_sample", None)
+        except Exception as exc:  # report, never fake
+            rs_host = {"error": repr(exc), "verified": False}
+        ok = ok and bool(rs_host.get("verified"))
+
     per_call = None
     if rank == 0 and not args.no_host:
         try:
@@ -1106,6 +1151,17 @@ def main(argv=None):
                         per_call["group_vs_reference"] = round(per_call["gpu_fec_encode_group_us"] / ref_g, 3)
         except Exception as exc:
             cpu["per_call"] = {"error": repr(exc)}
+        if rs_host_sample is not None:  # the checker role: the rs.h host path against the reference rs.c
+            try:
+                rs_host["reference_check"] = cpu_check_rs_sample(rs_host_sample)
+                ok = ok and bool(rs_host["reference_check"].get("match"))
+            except Exception as exc:
+                rs_host["reference_check"] = {"error": repr(exc)}
+                rs_host["verified"] = False
+                ok = False
+            for tag, base in (("vs_cpu_1thread", cpu), ("vs_cpu_threads", cpu_mt)):
+                if isinstance(base, dict) and base.get("value") and rs_host.get("value"):
+                    rs_host[tag] = round(rs_host["value"] / base["value"], 2)
         if host_sample is not None:  # the checker role: config 5's output against the reference rs.c
             try:
                 host_mixed["reference_check"] = cpu_check_host_sample(host_sample)
@@ -1160,6 +1216,7 @@ def main(argv=None):
             "config4": config4,
             "host_to_host_mixed": host_mixed,
             "host_to_host_encode": host_line,
+            "rs_abi_host": rs_host,
             "per_call": per_call,
             "verified": ok,
             "cpu_baseline": cpu,

@@ -238,7 +238,10 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "recon_compact"    1 tables via the 256-entry table at the record header's offsets | 0 from the record
  *   "recon_full_lines" 1 8-/12-B lanes cover the 16-B columns' span for k < 14 | 2 always | 0 stop at B
  *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies
- *   "host_chunk"       groups per staged host chunk (0: ~32 MiB)
+ *   "host_chunk"       groups per staged host chunk (0: by bytes: ~32 MiB for qfec_*_host, ~16 MiB of
+ *                      caller shards for module/rs.h on host pointers)
+ *   "host_threads"     host threads that gather / scatter module/rs.h host shard pointers (0: the
+ *                      CPUs this process may use -- affinity and cgroup quota -- at most 32)
  *   "wire_fused"       1 fused datagram send where a (k, m) instance exists | 0 staged build -> encode -> emit
  *   "wire_fused_rx"    1 fused datagram receive | 0 staged parse -> reconstruct -> check
  *   "wire_rx_split"    1 k_unpack_v2, lanes by pitch | 2 16-B | 3 8-B | 4 16-B with a remainder of up
@@ -282,6 +285,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "percall_fault"    (tests) 1 requests are never handed to a server, so every call takes the
  *                      timeout branch */
 int qfec_tune(const char *key, int value);
+/* The current value of a knob of qfec_tune (*value); QFEC_EINVAL for an unknown key. */
+int qfec_tune_get(const char *key, int *value);
 
 /* The resident per-call server of the current device (qfec_tune "percall_resident"): out[0] calls
  * it served, out[1] launches, out[2] relaunches because it had exited (idle) just before a request

@@ -52,13 +52,16 @@ reed_solomon *reed_solomon_new(int data_shards, int parity_shards);
 /* rs.h:25 / rs.c:478 */
 void reed_solomon_release(reed_solomon *rs);
 
-/* rs.h:34 / rs.c:574 -- G = nr_shards / (k + m) groups of block_size bytes. Returns 0
- * (the reference always returns 0; a device failure is reported on stderr and by
- * qfec_last_error()). */
+/* rs.h:34 / rs.c:574 -- G = nr_shards / (k + m) groups of block_size bytes. Returns 0 on
+ * success, as rs.c always does.  A device failure (no HIP device, a failed launch or copy)
+ * returns the negative QFEC_E* code of include/qfec.h instead -- a deviation: rs.c has no
+ * device that can fail -- and is also reported on stderr and by qfec_last_error().
+ * shards[] may mix host and device pointers; each pointer is classified on its own. */
 int reed_solomon_encode(reed_solomon *rs, unsigned char **shards, int nr_shards, int block_size);
 
 /* rs.h:44 / rs.c:598 -- erased data shards are rewritten in place. Returns 0, or -1 if
- * any group had more erased data shards than surviving parity shards. */
+ * any group had more erased data shards than surviving parity shards (such groups are left
+ * untouched, as in rs.c), or a negative QFEC_E* code (< -1) on a device failure. */
 int reed_solomon_reconstruct(reed_solomon *rs, unsigned char **shards, unsigned char *marks,
                              int nr_shards, int block_size);
 

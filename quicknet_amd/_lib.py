@@ -20,7 +20,7 @@ EXPORTS = {
                "qfec_pipe_new", "qfec_pipe_free", "qfec_pipe_encode", "qfec_pipe_reconstruct", "qfec_pipe_wait", "qfec_pipe_slots",
                "qfec_fec_code", "qfec_rs_code", "qfec_fec_matrix", "qfec_pack_datagrams", "qfec_unpack_datagrams",
                "qfec_frame_udp", "qfec_unframe_udp", "qfec_pack_frames", "qfec_unpack_frames", "qfec_gather_rows", "qfec_synth_fill", "qfec_probe_stream",
-               "qfec_tune", "qfec_percall_stats", "qfec_percall_counters", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
+               "qfec_tune", "qfec_tune_get", "qfec_percall_stats", "qfec_percall_counters", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
                "qfec_last_error", "qfec_version"],
     "qfec_net.h": ["qfec_net_new", "qfec_net_free", "qfec_net_session", "qfec_net_enable", "qfec_net_pack_input", "qfec_net_flush_pack",
                    "qfec_net_unpack_input", "qfec_net_flush_unpack", "qfec_net_stats"],
@@ -100,6 +100,7 @@ def lib():
         "qfec_synth_fill": (i, [vp, ll, u64, vp]),
         "qfec_probe_stream": (i, [vp, vp, ll, i, i, i, ll, vp]),
         "qfec_tune": (i, [C.c_char_p, i]),
+        "qfec_tune_get": (i, [C.c_char_p, C.POINTER(i)]),
         "qfec_percall_stats": (i, [vp]),
         "qfec_percall_counters": (i, [vp, i]),
         "qfec_set_kernel_variant": (i, [i]),
@@ -120,12 +121,18 @@ def lib():
         "reed_solomon_error": (i, []),
     }
     sig.update(ZFEC_SIG)
+    compat = os.environ.get("QFEC_LIB_COMPAT") == "1"
+    skipped = []
     for name, (res, args) in sig.items():
-        if os.environ.get("QFEC_LIB") and not hasattr(L, name):
-            continue  # an older build for a before/after A/B: entry points it predates stay unbound
+        if compat and not hasattr(L, name):
+            skipped.append(name)  # an older build for a before/after A/B: entry points it predates
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    if skipped:
+        import sys
+        print(f"[qfec] QFEC_LIB_COMPAT: {LIB_PATH} lacks {', '.join(skipped)} (left unbound)", file=sys.stderr)
     _lib = L
     return L
 

@@ -70,6 +70,13 @@ def tune(key, value):
     check(lib().qfec_tune(key.encode(), int(value)), f"qfec_tune({key})")
 
 
+def tune_get(key):
+    """The current value of a qfec_tune knob."""
+    v = C.c_int(0)
+    check(lib().qfec_tune_get(key.encode(), C.byref(v)), f"qfec_tune_get({key})")
+    return v.value
+
+
 def percall_stats():
     """The current device's resident per-call server (include/qfec.h qfec_percall_stats)."""
     out = (C.c_ulonglong * 5)()

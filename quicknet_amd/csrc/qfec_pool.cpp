@@ -1,0 +1,110 @@
+// qfec_pool.cpp -- host thread pool for the copies around the device (qfec_pool.hpp).
+#include "qfec_pool.hpp"
+
+#include <sched.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "qfec_internal.hpp"
+
+namespace qfec {
+
+HostPool::HostPool(int nthreads) {
+    for (int i = 1; i < nthreads; ++i) workers_.emplace_back([this, i] { loop(i); });
+}
+
+HostPool::~HostPool() {
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+    }
+    cv_job_.notify_all();
+    for (auto& t : workers_) t.join();
+}
+
+void HostPool::loop(int id) {
+    unsigned long long seen = 0;
+    for (;;) {
+        const std::function<void(int, int)>* job;
+        int nt;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_job_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            job = job_;
+            nt = nt_;
+        }
+        if (id < nt) (*job)(id, nt);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) cv_done_.notify_one();
+        }
+    }
+}
+
+void HostPool::run(const std::function<void(int, int)>& fn, int parts) {
+    const int nt = std::max(1, std::min(threads(), parts));
+    if (nt == 1 || workers_.empty()) {
+        fn(0, 1);
+        return;
+    }
+    std::lock_guard<std::mutex> one(run_mu_);
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        job_ = &fn;
+        nt_ = nt;
+        pending_ = (int)workers_.size();
+        ++gen_;
+    }
+    cv_job_.notify_all();
+    fn(0, nt);
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+}
+
+static int read_int_file(const char* path, long long* a, long long* b) {
+    FILE* f = fopen(path, "r");
+    if (!f) return 0;
+    char buf[128] = {0};
+    const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+    fclose(f);
+    if (!ok) return 0;
+    if (!strncmp(buf, "max", 3)) return -1;  // cgroup v2: no quota
+    return sscanf(buf, "%lld %lld", a, b);
+}
+
+int usable_cpus() {
+    int n = 1;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = std::max(1, CPU_COUNT(&set));
+    long long q = 0, p = 0;
+    if (read_int_file("/sys/fs/cgroup/cpu.max", &q, &p) == 2 && q > 0 && p > 0) {
+        n = std::min<long long>(n, std::max<long long>(1, (q + p - 1) / p));
+    } else {
+        long long q1 = 0, p1 = 0, d = 0;
+        if (read_int_file("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", &q1, &d) >= 1 && q1 > 0 &&
+            read_int_file("/sys/fs/cgroup/cpu/cpu.cfs_period_us", &p1, &d) >= 1 && p1 > 0)
+            n = std::min<long long>(n, std::max<long long>(1, (q1 + p1 - 1) / p1));
+    }
+    return n;
+}
+
+std::shared_ptr<HostPool> host_pool() {
+    static std::mutex mu;
+    static std::shared_ptr<HostPool> pool;
+    static int made_with = -1;
+    std::lock_guard<std::mutex> lk(mu);
+    const int want = tuning().host_threads;
+    if (!pool || want != made_with) {
+        const int n = want > 0 ? std::min(want, 64) : std::min(usable_cpus(), 32);
+        pool = std::make_shared<HostPool>(n);
+        made_with = want;
+    }
+    return pool;
+}
+
+}  // namespace qfec

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -36,6 +37,7 @@
 #include "../../include/qfec_rs.h"
 #include "qfec_internal.hpp"
 #include "qfec_percall.hpp"
+#include "qfec_pool.hpp"
 
 #define QFEC_VERSION_STRING "qfec 0.1.0 (gfx950)"
 
@@ -569,6 +571,10 @@ struct qfec_code {
     // host-side decode cache: pattern key -> (record words); for explicit mode
     std::unordered_map<uint64_t, std::vector<uint32_t>> rec_cache;
     uint64_t rec_cache_version = ~0ull;
+    // per LUT mask: 1 if its record seeds a row from the output's old bytes (the rs.c quirk), so a
+    // host-pointer reconstruct must stage the erased rows too (filled with the LUT)
+    std::vector<uint8_t> lut_seed;
+    uint64_t lut_seed_version = ~0ull;
 };
 
 namespace {
@@ -673,6 +679,7 @@ int ensure_lut(qfec_code* c, int dev, DevTables** out) {
     }
     const size_t nmask = (size_t)1 << n;
     std::vector<int32_t> lut(nmask);
+    std::vector<uint8_t> seed(nmask, 0);
     std::unordered_map<uint64_t, int32_t> off_of;
     std::vector<uint32_t> recs, one;
     for (size_t mask = 0; mask < nmask; ++mask) {
@@ -681,9 +688,14 @@ int ensure_lut(qfec_code* c, int dev, DevTables** out) {
         if (!pattern_key(mask, k, m, &key, &e)) { lut[mask] = QFEC_REC_FAIL; continue; }
         if (e == 0) { lut[mask] = QFEC_REC_NONE; continue; }
         auto it = off_of.find(key);
-        if (it != off_of.end()) { lut[mask] = it->second; continue; }
+        if (it != off_of.end()) {
+            lut[mask] = it->second;
+            seed[mask] = recs[(size_t)it->second + 1] != 0;
+            continue;
+        }
         if (record_for_key(c, key, one) <= 0) { lut[mask] = QFEC_REC_FAIL; continue; }
         one.resize(record_layout(k, m).words(m, k), 0);  // pad to m rows (branch-free kernel)
+        seed[mask] = one[1] != 0;  // record word 1: the rows the rs.c quirk seeds from the output
         const int32_t off = (int32_t)recs.size();
         recs.insert(recs.end(), one.begin(), one.end());
         off_of.emplace(key, off);
@@ -698,6 +710,8 @@ int ensure_lut(qfec_code* c, int dev, DevTables** out) {
     HIP_TRY(hipMemcpy(d.d_lut, lut.data(), nmask * 4, hipMemcpyHostToDevice));
     if (!recs.empty()) HIP_TRY(hipMemcpy(d.d_rec, recs.data(), recs.size() * 4, hipMemcpyHostToDevice));
     d.rec_version = c->version;
+    c->lut_seed.swap(seed);
+    c->lut_seed_version = c->version;
     return QFEC_OK;
 }
 
@@ -916,62 +930,85 @@ int qfec_set_kernel_variant(int v) {
 
 int qfec_get_kernel_variant(void) { return g_variant.load(); }
 
-// experiment knobs, for A/B timing in one process (tools/ab.py); not needed in production
+}  // extern "C"
+
+// knobs: integration settings and A/B switches (include/qfec.h); every one an atomic int
+namespace {
+struct Knob {
+    const char* key;
+    std::atomic<int>* v;
+    int lo, hi;
+};
+const std::vector<Knob>& knob_table() {
+    static const std::vector<Knob> t = {
+        {"recon_impl", &tuning().recon_impl, -1, 8},
+        {"host_chunk", &tuning().host_chunk, 0, 0x7FFFFFFF},
+        {"host_threads", &tuning().host_threads, 0, 64},
+        {"encode_impl", &tuning().encode_impl, -1, 2},
+        {"wire_store_nt", &tuning().wire_store_nt, 0, 3},
+        {"wire_chunk", &tuning().wire_chunk, 0, 0x7FFFFFFF},
+        {"wire_send_wave", &tuning().wire_send_wave, 0, 4},
+        {"wire_line", &tuning().wire_line, 0, 1},
+        {"wire_rx_tail", &tuning().wire_rx_tail, 0, 1},
+        {"wire_fused_rx", &tuning().wire_fused_rx, 0, 1},
+        {"wire_fused", &tuning().wire_fused, 0, 1},
+        {"host_zero_copy", &tuning().host_zero_copy, 0, 1},
+        {"recon_compact", &tuning().recon_compact, 0, 2},
+        {"recon_full_lines", &tuning().recon_full_lines, 0, 2},
+        {"wire_rx_lds", &tuning().wire_rx_lds, 0, 2},
+        {"frame_rows", &tuning().frame_rows, 1, 4},
+        {"wire_rx_split", &tuning().wire_rx_split, 0, 4},
+        {"wire_rx_skip_lost", &tuning().wire_rx_skip_lost, 0, 1},
+        {"percall_fast", &g_percall_fast, 0, 1},
+        {"percall_spin", &g_percall_spin, 0, 1},
+        {"percall_in", &g_percall_in, 0, 1},
+        {"percall_group", &g_percall_group, 0, 1},
+        {"percall_fault", &g_percall_fault, 0, 1},
+        {"percall_timeout_us", &g_percall_timeout_us, 0, 0x7FFFFFFF},
+        {"percall_idle_us", &g_percall_idle_us, 0, 1000000},
+        {"percall_resident", &g_percall_resident, 0, 1},
+    };
+    return t;
+}
+
+// a running per-call server keeps the settings it was launched with: stop it, the next call
+// launches one with the new ones
+void stop_percall_servers() {
+    for (DevCtx& c : g_ctx) {
+        std::lock_guard<std::mutex> lk(c.mu);
+        if (c.srv.usable <= 0 || !c.srv.launched) continue;
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(c.device);
+        (void)pc_server_stop(c);
+        (void)hipSetDevice(prev);
+    }
+}
+}  // namespace
+
+extern "C" {
+
 int qfec_tune(const char* key, int value) {
     if (!key) return QFEC_EINVAL;
-    if (!strcmp(key, "recon_impl") && value >= -1 && value <= 8 && value != 7) { tuning().recon_impl = value; return QFEC_OK; }
-    if (!strcmp(key, "host_chunk") && value >= 0) { tuning().host_chunk = value; return QFEC_OK; }
-    if (!strcmp(key, "encode_impl") && value >= -1 && value <= 2) { tuning().encode_impl = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_store_nt") && value >= 0 && value <= 3) { tuning().wire_store_nt = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_chunk") && value >= 0) { tuning().wire_chunk = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_send_wave") && value >= 0 && value <= 4) { tuning().wire_send_wave = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_line") && (value == 0 || value == 1)) { tuning().wire_line = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_rx_tail") && (value == 0 || value == 1)) { tuning().wire_rx_tail = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_fused_rx") && (value == 0 || value == 1)) { tuning().wire_fused_rx = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_fused") && (value == 0 || value == 1)) { tuning().wire_fused = value; return QFEC_OK; }
-    if (!strcmp(key, "host_zero_copy") && (value == 0 || value == 1)) { tuning().host_zero_copy = value; return QFEC_OK; }
-    if (!strcmp(key, "recon_compact") && value >= 0 && value <= 2) { tuning().recon_compact = value; return QFEC_OK; }
-    if (!strcmp(key, "recon_full_lines") && value >= 0 && value <= 2) { tuning().recon_full_lines = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_rx_lds") && value >= 0 && value <= 2) { tuning().wire_rx_lds = value; return QFEC_OK; }
-    if (!strcmp(key, "frame_rows") && value >= 1 && value <= 4) { tuning().frame_rows = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_rx_split") && value >= 0 && value <= 4) { tuning().wire_rx_split = value; return QFEC_OK; }
-    if (!strcmp(key, "wire_rx_skip_lost") && (value == 0 || value == 1)) { tuning().wire_rx_skip_lost = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_fast") && (value == 0 || value == 1)) { g_percall_fast = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_spin") && (value == 0 || value == 1)) { g_percall_spin = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_in") && (value == 0 || value == 1)) { g_percall_in = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_group") && (value == 0 || value == 1)) { g_percall_group = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_fault") && (value == 0 || value == 1)) { g_percall_fault = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_timeout_us") && value >= 0) { g_percall_timeout_us = value; return QFEC_OK; }
-    if (!strcmp(key, "percall_idle_us") && value >= 0 && value <= 1000000) {
-        // a running block keeps the idle time it was launched with: stop it, the next call
-        // launches one with the new value
-        g_percall_idle_us = value;
-        for (DevCtx& c : g_ctx) {
-            std::lock_guard<std::mutex> lk(c.mu);
-            if (c.srv.usable <= 0 || !c.srv.launched) continue;
-            int prev = 0;
-            (void)hipGetDevice(&prev);
-            (void)hipSetDevice(c.device);
-            (void)pc_server_stop(c);
-            (void)hipSetDevice(prev);
-        }
-        return QFEC_OK;
-    }
-    if (!strcmp(key, "percall_resident") && (value == 0 || value == 1)) {
-        g_percall_resident = value;
-        if (!value)
-            for (DevCtx& c : g_ctx) {
-                std::lock_guard<std::mutex> lk(c.mu);
-                if (c.srv.usable <= 0 || !c.srv.launched) continue;
-                int prev = 0;
-                (void)hipGetDevice(&prev);
-                (void)hipSetDevice(c.device);
-                (void)pc_server_stop(c);
-                (void)hipSetDevice(prev);
-            }
+    for (const Knob& kn : knob_table()) {
+        if (strcmp(key, kn.key)) continue;
+        if (value < kn.lo || value > kn.hi) break;
+        kn.v->store(value);
+        if (!strcmp(key, "percall_idle_us") || (!strcmp(key, "percall_resident") && !value)) stop_percall_servers();
         return QFEC_OK;
     }
     set_error("qfec_tune: unknown key/value %s=%d", key, value);
+    return QFEC_EINVAL;
+}
+
+int qfec_tune_get(const char* key, int* value) {
+    if (!key || !value) return QFEC_EINVAL;
+    for (const Knob& kn : knob_table())
+        if (!strcmp(key, kn.key)) {
+            *value = kn.v->load();
+            return QFEC_OK;
+        }
+    set_error("qfec_tune_get: unknown key %s", key);
     return QFEC_EINVAL;
 }
 
@@ -1089,7 +1126,7 @@ int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char
     const int k = code->k, m = code->m;
     const size_t in_g = (size_t)k * (size_t)pitch, out_g = (size_t)m * (size_t)pitch;
     // chunk: ~32 MiB of data shards (tuning "host_chunk" = groups per chunk overrides)
-    long long gc = tuning().host_chunk > 0 ? tuning().host_chunk
+    long long gc = tuning().host_chunk > 0 ? (long long)tuning().host_chunk
                                            : std::max<long long>(1, (long long)((size_t)32 << 20) / (long long)in_g);
     gc = std::min(gc, groups);
     const bool pin_in = is_pinned_host(h_data), pin_out = is_pinned_host(h_parity);
@@ -1173,7 +1210,7 @@ int qfec_reconstruct_host(qfec_code* code, unsigned char* h_data, const unsigned
     // chunk slot layout, device and pinned alike: data [gc][k][pitch] | parity [gc][m][pitch]
     // | marks [gc*k data marks][gc*m parity marks] | failed counter (8 B)
     const size_t dg = (size_t)k * (size_t)pitch, pg = (size_t)m * (size_t)pitch;
-    long long gc = tuning().host_chunk > 0 ? tuning().host_chunk
+    long long gc = tuning().host_chunk > 0 ? (long long)tuning().host_chunk
                                            : std::max<long long>(1, (long long)((size_t)32 << 20) / (long long)dg);
     gc = std::min(gc, groups);
     const size_t mk_off = (size_t)gc * (dg + pg), cnt_off = round_up(mk_off + (size_t)gc * (k + m), 16);
@@ -1995,13 +2032,14 @@ int qfec_unframe_udp(const unsigned char* d_in, long long in_pitch, const int* d
 // ====================================================================== host-buffer paths
 namespace {
 
-// gather `count` rows of `len` bytes from ptrs[] (host or device) into device rows of
-// `pitch` at dst (device); uses the pinned stage at hst when the rows are host memory.
+// gather `count` rows of `len` bytes from ptrs[] into device rows of `pitch` at dst (device).
+// dev_src: one copy per row, whatever memory each row is in (device, managed or host rows mixed:
+// hipMemcpyDefault); else the rows are host memory, gathered through the pinned stage at h_tmp.
 int gather_rows(DevCtx& c, unsigned char* const* ptrs, size_t count, int len, size_t pitch, uint8_t* d_dst,
                 uint8_t* h_tmp, bool dev_src) {
     if (dev_src) {
         for (size_t i = 0; i < count; ++i)
-            HIP_TRY(hipMemcpyAsync(d_dst + i * pitch, ptrs[i], (size_t)len, hipMemcpyDeviceToDevice, c.stream));
+            HIP_TRY(hipMemcpyAsync(d_dst + i * pitch, ptrs[i], (size_t)len, hipMemcpyDefault, c.stream));
         return QFEC_OK;
     }
     for (size_t i = 0; i < count; ++i) memcpy(h_tmp + i * pitch, ptrs[i], (size_t)len);
@@ -2014,7 +2052,7 @@ int scatter_rows(DevCtx& c, unsigned char* const* ptrs, size_t count, int len, s
     if (dev_dst) {
         for (size_t i = 0; i < count; ++i)
             if (!only || only[i])
-                HIP_TRY(hipMemcpyAsync(ptrs[i], d_src + i * pitch, (size_t)len, hipMemcpyDeviceToDevice, c.stream));
+                HIP_TRY(hipMemcpyAsync(ptrs[i], d_src + i * pitch, (size_t)len, hipMemcpyDefault, c.stream));
         HIP_TRY(hipStreamSynchronize(c.stream));
         return QFEC_OK;
     }
@@ -2033,6 +2071,264 @@ bool contiguous(unsigned char* const* ptrs, size_t count, int len) {
 }
 
 constexpr size_t kChunkBytes = (size_t)256 << 20;  // staging chunk for host-buffer batches
+
+// ---- module/rs.h on arrays of caller shard pointers (round 5)
+//
+// Kinds of caller pointers: device (or managed) memory against host memory.  A device verdict
+// comes only from the runtime (hipPointerGetAttributes), and the whole allocation it belongs to
+// (hipMemGetAddressRange) then answers for later pointers without a probe.  A host verdict is
+// reused for other pointers in the same 64 KiB window, within one call only.  Device allocations
+// are placed in the GPU address apertures the runtime reserves, which host mappings do not share
+// at that granularity; a managed allocation that a reused host verdict covers is still memory
+// the CPU copies can read and write.  So no reused verdict can move a wrong byte.
+struct PtrClass {
+    std::vector<std::pair<uintptr_t, uintptr_t>> dev;  // device allocation ranges [lo, hi)
+    std::vector<uintptr_t> host_win;                   // 64 KiB windows with a host verdict
+    uintptr_t last_win = ~(uintptr_t)0;
+    size_t last_dev = 0;
+    bool is_dev(const void* p) {
+        const uintptr_t u = (uintptr_t)p, w = u >> 16;
+        if (last_dev < dev.size() && u >= dev[last_dev].first && u < dev[last_dev].second) return true;
+        for (size_t i = 0; i < dev.size(); ++i)
+            if (u >= dev[i].first && u < dev[i].second) {
+                last_dev = i;
+                return true;
+            }
+        if (w == last_win) return false;
+        for (uintptr_t x : host_win)
+            if (x == w) {
+                last_win = w;
+                return false;
+            }
+        hipPointerAttribute_t attr;
+        const hipError_t e = hipPointerGetAttributes(&attr, p);
+        if (e == hipSuccess && (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged)) {
+            void* base = nullptr;
+            size_t size = 0;
+            if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) == hipSuccess && base && size) {
+                dev.emplace_back((uintptr_t)base, (uintptr_t)base + size);
+                last_dev = dev.size() - 1;
+            } else {
+                (void)hipGetLastError();
+                dev.emplace_back(u, u + 1);  // this pointer only
+            }
+            return true;
+        }
+        if (e != hipSuccess) (void)hipGetLastError();
+        if (host_win.size() < 4096) host_win.push_back(w);
+        last_win = w;
+        return false;
+    }
+};
+
+// number of device pointers among ptrs[0 .. count), classified on the host pool's threads
+size_t count_device_ptrs(unsigned char* const* ptrs, size_t count, HostPool& pool) {
+    std::atomic<size_t> ndev{0};
+    pool.run(
+        [&](int t, int nt) {
+            PtrClass pc;
+            size_t nd = 0;
+            const size_t a = count * t / nt, b = count * (t + 1) / nt;
+            for (size_t i = a; i < b; ++i) nd += pc.is_dev(ptrs[i]) ? 1 : 0;
+            ndev += nd;
+        },
+        (int)std::max<size_t>(1, count >> 14));
+    return ndev.load();
+}
+
+// bytes of caller shards per pipelined chunk of the host-pointer paths (tuning "host_chunk"
+// overrides with groups per chunk)
+constexpr size_t kRsPipeBytes = (size_t)16 << 20;
+
+// the slot's device view: the pinned staging itself (zero copy) or the slot's device buffer
+uint8_t* rs_slot_dev(DevCtx::HostSlot& h, bool zc) {
+    uint8_t* z = nullptr;
+    if (zc && host_dev(h.h_in, &z)) return z;
+    return nullptr;
+}
+
+// reed_solomon_encode over host shard pointers: chunks of groups alternate between two pinned
+// slots; the host threads gather a chunk's data rows into one slot while the device encodes the
+// previous chunk out of the other (reading and writing the pinned slot in place, or through the
+// slot's device buffer), and scatter each chunk's parity rows once its event has fired.
+int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigned char** data, unsigned char** par,
+                   long long G, int B, bool any_stale) {
+    const int k = c->k, m = c->m;
+    const size_t pitch = round_up((size_t)B, 16), dg = (size_t)k * pitch, pg = (size_t)m * pitch;
+    long long per = tuning().host_chunk > 0 ? (long long)tuning().host_chunk
+                                            : std::max<long long>(1, (long long)(kRsPipeBytes / (dg + pg)));
+    per = std::min(per, G);
+    const size_t slot_bytes = (size_t)per * (dg + pg);
+    std::shared_ptr<HostPool> pool = host_pool();
+    std::lock_guard<std::mutex> lk(ctx.host_mu);
+    int rc = QFEC_OK;
+    for (auto& h : ctx.host)
+        if ((rc = ensure_host_slot(h, slot_bytes, 16))) return rc;
+    const bool zc = tuning().host_zero_copy != 0;
+    long long pending[2] = {-1, -1};
+    auto rows_job = [&](size_t nrows, const std::function<void(size_t)>& row) {
+        pool->run(
+            [&](int t, int nt) {
+                const size_t a = nrows * t / nt, b = nrows * (t + 1) / nt;
+                for (size_t i = a; i < b; ++i) row(i);
+            },
+            (int)std::max<size_t>(1, nrows / 64));
+    };
+    auto drain = [&](int sl) -> int {
+        if (pending[sl] < 0) return QFEC_OK;
+        DevCtx::HostSlot& h = ctx.host[sl];
+        HIP_TRY(hipEventSynchronize(h.done));
+        const long long g0 = pending[sl], gn = std::min(per, G - g0);
+        const uint8_t* hp = h.h_in + (size_t)gn * dg;
+        rows_job((size_t)gn * m, [&](size_t i) { memcpy(par[(size_t)g0 * m + i], hp + i * pitch, (size_t)B); });
+        pending[sl] = -1;
+        return QFEC_OK;
+    };
+    const long long nchunks = (G + per - 1) / per;
+    for (long long i = 0; i < nchunks && !rc; ++i) {
+        const int sl = (int)(i & 1);
+        DevCtx::HostSlot& h = ctx.host[sl];
+        const long long g0 = i * per, gn = std::min(per, G - g0);
+        uint8_t* hd = h.h_in;
+        uint8_t* hp = h.h_in + (size_t)gn * dg;
+        // data rows (and, when a parity row keeps its old bytes -- the rs.c quirk -- the parity rows)
+        const size_t nd = (size_t)gn * k, np = any_stale ? (size_t)gn * m : 0;
+        rows_job(nd + np, [&](size_t r) {
+            if (r < nd) memcpy(hd + r * pitch, data[(size_t)g0 * k + r], (size_t)B);
+            else memcpy(hp + (r - nd) * pitch, par[(size_t)g0 * m + (r - nd)], (size_t)B);
+        });
+        uint8_t* z = rs_slot_dev(h, zc);
+        uint8_t* dd = z ? z : h.d_buf;
+        if (!z) {
+            const hipError_t e = hipMemcpyAsync(dd, hd, (size_t)gn * dg + np * pitch, hipMemcpyHostToDevice, h.stream);
+            if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_encode: H2D"); break; }
+        }
+        if ((rc = run_encode(ctx, c, tab, m, dd, dd + (size_t)gn * dg, gn, B, (long long)pitch, h.stream))) break;
+        if (!z) {
+            const hipError_t e = hipMemcpyAsync(hp, dd + (size_t)gn * dg, (size_t)gn * pg, hipMemcpyDeviceToHost, h.stream);
+            if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_encode: D2H"); break; }
+        }
+        const hipError_t e = hipEventRecord(h.done, h.stream);
+        if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_encode: event"); break; }
+        pending[sl] = g0;
+        if (i > 0 && (rc = drain(sl ^ 1))) break;  // the previous chunk, while this one runs
+    }
+    if (!rc) rc = drain((int)((nchunks - 1) & 1));
+    if (rc) quiesce_host_slots(ctx);  // nothing may still be writing into the slots
+    return rc;
+}
+
+// reed_solomon_reconstruct over host shard pointers (k + m <= QFEC_LUT_MAX_N): the same two-slot
+// pipeline.  Per group only what the decode reads is staged -- the surviving data rows and the
+// first e surviving parity rows (rs.c:611-629), plus the erased rows where the pattern's record
+// seeds a row from its old bytes (the rs.c quirk) -- with the chunk's marks in rs.c layout; the
+// LUT kernel decodes and only the erased data rows of recoverable groups are scattered back.
+// Groups with more erased data than surviving parity are left untouched and counted (*nfail).
+int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uint8_t* seed, unsigned char** data,
+                        unsigned char** par, const uint8_t* mk, long long G, int B, long long* nfail) {
+    const int k = c->k, m = c->m, n = k + m;
+    const size_t pitch = round_up((size_t)B, 16), dg = (size_t)k * pitch, pg = (size_t)m * pitch;
+    long long per = tuning().host_chunk > 0 ? (long long)tuning().host_chunk
+                                            : std::max<long long>(1, (long long)(kRsPipeBytes / (dg + pg)));
+    per = std::min(per, G);
+    const size_t mk_off = (size_t)per * (dg + pg), slot_bytes = round_up(mk_off + (size_t)per * n, 16);
+    std::shared_ptr<HostPool> pool = host_pool();
+    std::lock_guard<std::mutex> lk(ctx.host_mu);
+    int rc = QFEC_OK;
+    for (auto& h : ctx.host)
+        if ((rc = ensure_host_slot(h, slot_bytes, 16))) return rc;
+    const bool zc = tuning().host_zero_copy != 0;
+    std::vector<uint8_t> todo[2];  // per slot, per group: 1 = decoded (scatter its erased data rows)
+    long long pending[2] = {-1, -1};
+    std::atomic<long long> fails{0};
+    auto groups_job = [&](long long gn, const std::function<void(long long, long long)>& span) {
+        pool->run(
+            [&](int t, int nt) { span(gn * t / nt, gn * (t + 1) / nt); }, (int)std::max<long long>(1, gn / 16));
+    };
+    auto drain = [&](int sl) -> int {
+        if (pending[sl] < 0) return QFEC_OK;
+        DevCtx::HostSlot& h = ctx.host[sl];
+        HIP_TRY(hipEventSynchronize(h.done));
+        const long long g0 = pending[sl], gn = std::min(per, G - g0);
+        const uint8_t* todo_s = todo[sl].data();
+        const uint8_t* hd = h.h_in;
+        groups_job(gn, [&](long long a, long long b) {
+            for (long long g = a; g < b; ++g) {
+                if (!todo_s[g]) continue;
+                const uint8_t* dm = mk + (size_t)(g0 + g) * k;
+                for (int i = 0; i < k; ++i)
+                    if (dm[i]) memcpy(data[(size_t)(g0 + g) * k + i], hd + ((size_t)g * k + i) * pitch, (size_t)B);
+            }
+        });
+        pending[sl] = -1;
+        return QFEC_OK;
+    };
+    const long long nchunks = (G + per - 1) / per;
+    for (long long i = 0; i < nchunks && !rc; ++i) {
+        const int sl = (int)(i & 1);
+        DevCtx::HostSlot& h = ctx.host[sl];
+        const long long g0 = i * per, gn = std::min(per, G - g0);
+        uint8_t* hd = h.h_in;
+        uint8_t* hp = h.h_in + (size_t)gn * dg;
+        uint8_t* hm = h.h_in + (size_t)gn * (dg + pg);
+        todo[sl].assign((size_t)gn, 0);
+        uint8_t* todo_s = todo[sl].data();
+        groups_job(gn, [&](long long a, long long b) {
+            long long nf = 0;
+            for (long long g = a; g < b; ++g) {
+                const size_t gg = (size_t)(g0 + g);
+                const uint8_t* dm = mk + gg * k;
+                const uint8_t* pm = mk + (size_t)G * k + gg * m;
+                memcpy(hm + (size_t)g * k, dm, (size_t)k);
+                memcpy(hm + (size_t)gn * k + (size_t)g * m, pm, (size_t)m);
+                uint32_t mask = 0;
+                int e = 0;
+                for (int x = 0; x < k; ++x)
+                    if (dm[x]) { mask |= 1u << x; ++e; }
+                if (!e) continue;
+                for (int j = 0; j < m; ++j)
+                    if (pm[j]) mask |= 1u << (k + j);
+                int got = 0;
+                for (int j = 0; j < m && got < e; ++j)
+                    if (!pm[j]) {
+                        memcpy(hp + ((size_t)g * m + j) * pitch, par[gg * m + j], (size_t)B);
+                        ++got;
+                    }
+                if (got < e) {  // under-determined: left as it is (rs.c:630-634)
+                    ++nf;
+                    continue;
+                }
+                const bool sd = seed[mask] != 0;
+                for (int x = 0; x < k; ++x)
+                    if (!dm[x] || sd) memcpy(hd + ((size_t)g * k + x) * pitch, data[gg * k + x], (size_t)B);
+                todo_s[g] = 1;
+            }
+            fails += nf;
+        });
+        uint8_t* z = rs_slot_dev(h, zc);
+        uint8_t* dd = z ? z : h.d_buf;
+        const size_t used = (size_t)gn * (dg + pg + n);
+        if (!z) {
+            const hipError_t e = hipMemcpyAsync(dd, h.h_in, used, hipMemcpyHostToDevice, h.stream);
+            if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_reconstruct: H2D"); break; }
+        }
+        if ((rc = run_reconstruct(ctx, c, d->d_lut, nullptr, d->d_rec, dd, dd + (size_t)gn * dg,
+                                  dd + (size_t)gn * (dg + pg), gn, B, (long long)pitch, nullptr, h.stream)))
+            break;
+        if (!z) {
+            const hipError_t e = hipMemcpyAsync(h.h_in, dd, (size_t)gn * dg, hipMemcpyDeviceToHost, h.stream);
+            if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_reconstruct: D2H"); break; }
+        }
+        const hipError_t e = hipEventRecord(h.done, h.stream);
+        if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_reconstruct: event"); break; }
+        pending[sl] = g0;
+        if (i > 0 && (rc = drain(sl ^ 1))) break;
+    }
+    if (!rc) rc = drain((int)((nchunks - 1) & 1));
+    if (rc) quiesce_host_slots(ctx);
+    *nfail = fails.load();
+    return rc;
+}
 
 }  // namespace
 
@@ -2145,16 +2441,24 @@ int reed_solomon_encode(reed_solomon* rs, unsigned char** shards, int nr_shards,
     if (rc) { fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error()); return rc; }
     unsigned char** data = shards;
     unsigned char** par = shards + G * k;
-    const bool dev = is_device_ptr(shards[0]);
+    // every shard pointer is classified: all device -> in place (or device gathers), all host ->
+    // the pipelined host path, a mix -> one copy per row, whatever memory each row is in
+    const size_t nptr = (size_t)G * n;
+    const size_t ndev = count_device_ptrs(shards, nptr, *host_pool());
+    if (ndev == 0) {
+        rc = rs_encode_pipe(*ctx, c, tab, data, par, G, block_size, any_stale);
+        if (rc) fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
+        return rc;
+    }
     std::lock_guard<std::mutex> lk(ctx->mu);
-    if (dev && contiguous(data, (size_t)G * k, block_size) && contiguous(par, (size_t)G * m, block_size)) {
+    if (ndev == nptr && contiguous(data, (size_t)G * k, block_size) && contiguous(par, (size_t)G * m, block_size)) {
         rc = run_encode(*ctx, c, tab, m, data[0], par[0], G, block_size, block_size, ctx->stream);
         if (!rc) rc = hipStreamSynchronize(ctx->stream) == hipSuccess ? 0 : QFEC_EHIP;
         if (rc) fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
         return rc;
     }
     const size_t pitch = round_up((size_t)block_size, 16);
-    const long long per = tuning().host_chunk > 0 ? tuning().host_chunk
+    const long long per = tuning().host_chunk > 0 ? (long long)tuning().host_chunk
                                                   : std::max<long long>(1, (long long)(kChunkBytes / ((size_t)n * pitch)));
     for (long long g0 = 0; g0 < G && !rc; g0 += per) {
         const long long gn = std::min(per, G - g0);
@@ -2162,15 +2466,18 @@ int reed_solomon_encode(reed_solomon* rs, unsigned char** shards, int nr_shards,
         if ((rc = ensure_stage(*ctx, dbytes + pbytes, dbytes + pbytes))) break;
         uint8_t* d_d = ctx->d_stage;
         uint8_t* d_p = ctx->d_stage + dbytes;
-        if ((rc = gather_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, ctx->h_stage, dev))) break;
+        if ((rc = gather_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, ctx->h_stage, true))) break;
         if (any_stale &&
-            (rc = gather_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, ctx->h_stage + dbytes, dev)))
+            (rc = gather_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, ctx->h_stage + dbytes, true)))
             break;
         if ((rc = run_encode(*ctx, c, tab, m, d_d, d_p, gn, block_size, (long long)pitch, ctx->stream))) break;
-        rc = scatter_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, ctx->h_stage + dbytes, dev,
+        rc = scatter_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, ctx->h_stage + dbytes, true,
                           nullptr);
     }
-    if (rc) fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
+    if (rc) {
+        (void)hipStreamSynchronize(ctx->stream);
+        fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
+    }
     return rc;
 }
 
@@ -2194,18 +2501,43 @@ int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned 
         }
         mk = hmarks.data();
     }
-    // chunks of ~kChunkBytes of staged shards, each with its own decode records (built from
-    // that chunk's marks), so staging stays bounded whatever the batch size; groups left
-    // under-determined -> -1 (rs.c:631-634), counted on the host by the kernel's rule
     unsigned char** data = shards;
     unsigned char** par = shards + G * k;
-    const size_t pitch = round_up((size_t)block_size, 16);
-    const long long per = tuning().host_chunk > 0 ? tuning().host_chunk  // knob: tests force several chunks
-                                                  : std::max<long long>(1, (long long)(kChunkBytes / ((size_t)n * pitch)));
     DevCtx* ctx = nullptr;
-    bool dev = false;
     long long nfail_all = 0;
     int rc = QFEC_OK;
+    // all shards in host memory and a pattern LUT in reach: the pipelined host path
+    if (n <= QFEC_LUT_MAX_N) {
+        bool any = false;
+        for (size_t i = 0; i < (size_t)G * k && !any; ++i) any = mk[i] != 0;
+        if (!any) return 0;  // nothing erased: nothing to do (rs.c:618-620)
+        if ((rc = current_ctx(&ctx))) {
+            fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error());
+            return rc;
+        }
+        if (count_device_ptrs(shards, (size_t)G * n, *host_pool()) == 0) {
+            DevTables* d = nullptr;
+            std::vector<uint8_t> seed;
+            {
+                std::lock_guard<std::mutex> lk(c->mu);
+                rc = ensure_lut(c, ctx->device, &d);
+                if (!rc) seed = c->lut_seed;
+            }
+            if (!rc) rc = rs_reconstruct_pipe(*ctx, c, d, seed.data(), data, par, mk, G, block_size, &nfail_all);
+            if (rc) {
+                fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error());
+                return rc;
+            }
+            return nfail_all ? -1 : 0;
+        }
+    }
+    // device or mixed pointers (or n > 24): chunks of ~kChunkBytes of staged shards, each with its
+    // own decode records (built from that chunk's marks), so staging stays bounded whatever the
+    // batch size; one copy per row, whatever memory it is in; groups left under-determined -> -1
+    // (rs.c:631-634), counted on the host by the kernel's rule
+    const size_t pitch = round_up((size_t)block_size, 16);
+    const long long per = tuning().host_chunk > 0 ? (long long)tuning().host_chunk  // knob: tests force several chunks
+                                                  : std::max<long long>(1, (long long)(kChunkBytes / ((size_t)n * pitch)));
     std::vector<uint8_t> cmarks, only;
     std::vector<int32_t> grec;
     std::vector<uint32_t> recs;
@@ -2221,10 +2553,7 @@ int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned 
         }
         nfail_all += nfail;
         if (recs.empty()) continue;  // nothing to recover in this chunk
-        if (!ctx) {
-            if ((rc = current_ctx(&ctx))) break;
-            dev = is_device_ptr(shards[0]);
-        }
+        if (!ctx && (rc = current_ctx(&ctx))) break;
         only.resize((size_t)gn * k);
         for (size_t i = 0; i < only.size(); ++i) only[i] = cmarks[i] ? 1 : 0;
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -2240,14 +2569,14 @@ int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned 
         uint8_t* hs = ctx->h_stage;
         memcpy(hs + dbytes + pbytes, grec.data(), (size_t)gn * 4);
         memcpy(hs + dbytes + pbytes + gbytes, recs.data(), recs.size() * 4);
-        rc = gather_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, hs, dev);
-        if (!rc) rc = gather_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, hs + dbytes, dev);
+        rc = gather_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, hs, true);
+        if (!rc) rc = gather_rows(*ctx, par + g0 * m, (size_t)gn * m, block_size, pitch, d_p, hs + dbytes, true);
         if (!rc && hipMemcpyAsync(d_g, hs + dbytes + pbytes, gbytes + rbytes, hipMemcpyHostToDevice, ctx->stream) !=
                        hipSuccess)
             rc = hip_fail(hipGetLastError(), "reed_solomon_reconstruct: H2D");
         if (!rc) rc = run_reconstruct(*ctx, c, nullptr, d_g, d_r, d_d, d_p, nullptr, gn, block_size, (long long)pitch,
                                       nullptr, ctx->stream);
-        if (!rc) rc = scatter_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, hs, dev, only.data());
+        if (!rc) rc = scatter_rows(*ctx, data + g0 * k, (size_t)gn * k, block_size, pitch, d_d, hs, true, only.data());
         if (rc) (void)hipStreamSynchronize(ctx->stream);  // nothing left in flight into the staging
     }
     if (rc) {

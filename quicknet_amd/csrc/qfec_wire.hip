@@ -1050,870 +1050,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WV ? W
     if (ln < N) a.wire_len[g * N + ln] = FP + HDR + (ln < K ? size[ln] + HEAD : gmax);
 }
 
-// A lane's slice of a shard row in one pass: NV16 = 4 -> one 16-B chunk at pos16, then NVT
-// tail dwords at tail + 4 * (lane + 64 t) (coalesced per instruction).  Dword d sits at
-// byte pos(d) of the row.
-template <int NV16, int NVT>
-struct Slice {
-    static constexpr int NV = NV16 + NVT;
-    int pos16, tail, lane;
-    bool act16;
-    int tail_end;  // tail dwords past this byte are inactive
-    __device__ __forceinline__ int pos(int d) const { return d < NV16 ? pos16 + 4 * d : tail + 4 * (lane + 64 * (d - NV16)); }
-    __device__ __forceinline__ bool act(int d) const { return d < NV16 ? act16 : pos(d) < tail_end; }
-    __device__ __forceinline__ void load(uint32_t (&v)[NV], const uint8_t* row) const {
-        if (NV16 && act16) {
-            uint4 w;
-            __builtin_memcpy(&w, row + pos16, 16);
-            v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
-        }
-#pragma unroll
-        for (int d = NV16; d < NV; ++d)
-            if (act(d)) __builtin_memcpy(&v[d], row + pos(d), 4);
-    }
-    __device__ __forceinline__ void store(uint8_t* row, const uint32_t (&v)[NV]) const {
-        if (NV16 && act16) st16(row + pos16, make_uint4(v[0], v[1], v[2], v[3]));
-#pragma unroll
-        for (int d = NV16; d < NV; ++d)
-            if (act(d)) *reinterpret_cast<uint32_t*>(row + pos(d)) = v[d];
-    }
-    // keep the bytes of row positions [lo, hi)
-    __device__ __forceinline__ void mask(uint32_t (&v)[NV], int lo, int hi) const {
-#pragma unroll
-        for (int d = 0; d < NV; ++d) v[d] &= byte_mask(lo - pos(d), hi - pos(d), 0);
-    }
-};
+// The fused receive (qfec_unpack_datagrams / qfec_unpack_frames) is k_rx in qfec_rx.hip.
 
-template <int NV>
-__device__ __forceinline__ uint32_t sum_vec(const uint32_t (&v)[NV]) {
-    uint32_t s = 0;
-#pragma unroll
-    for (int d = 0; d < NV; ++d) s = __builtin_amdgcn_sad_u8(v[d], 0u, s);
-    return s;
-}
-
-// the group's plan, wave-uniform
-template <int K, int M>
-struct UnpackPlan {
-    uint32_t sv_off[K];   // survivor c: datagram row offset + its header length
-    int sv_row[K], sv_size[K];
-    int ns;               // survivors loaded (K when recoverable, else the valid data rows)
-    int lost_row[M], e;   // decoded rows
-    bool dec;             // rows to decode (known from the masks, before the record loads)
-    const uint32_t* tab;
-    uint32_t zero_rows;   // data rows to zero (lost, group not recoverable)
-    uint32_t ex_off[M];   // rows only checksummed (first round)
-    int ex_row[M], ex_size[M], nx;
-};
-
-template <int K, int M, int NV16, int NVT>
-__device__ __forceinline__ void unpack_pass(const UnpackPlan<K, M>& pl, const uint8_t* __restrict__ wire_g,
-                                            uint8_t* __restrict__ out_g, uint64_t pitch,
-                                            const Slice<NV16, NVT>& sl, bool first_pass, int checksum,
-                                            uint32_t (&dsum)[K], uint32_t (&xsum)[M], uint32_t (&ps_s)[K],
-                                            uint32_t (&ps_l)[M], uint32_t (&w0_s)[K], uint32_t (&w0_l)[M]) {
-    constexpr int NV = NV16 + NVT;
-    uint32_t x[K][NV];
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-#pragma unroll
-        for (int d = 0; d < NV; ++d) x[c][d] = 0;
-        if (c < pl.ns) sl.load(x[c], wire_g + pl.sv_off[c]);
-    }
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        sl.mask(x[c], 0, pl.sv_size[c]);
-        dsum[c] += sum_vec<NV>(x[c]);
-    }
-    uint32_t acc[M][NV];
-#pragma unroll
-    for (int j = 0; j < M; ++j)
-#pragma unroll
-        for (int d = 0; d < NV; ++d) acc[j][d] = 0;
-    if (pl.dec) {  // not pl.e: the table loads need not wait for the record header
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            Sel sc[NV];
-#pragma unroll
-            for (int d = 0; d < NV; ++d) sc[d] = gf_sel(x[c][d]);
-            // all M rows, no branch on e: records are padded to M rows (zero tables), and
-            // unconditional scalar loads batch instead of one s_load round trip per entry
-#pragma unroll
-            for (int j = 0; j < M; ++j) {
-                const uint32_t* t = pl.tab + (j * K + c) * QFEC_TAB_STRIDE;
-                const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
-#pragma unroll
-                for (int d = 0; d < NV; ++d)
-                    acc[j][d] = xor3(acc[j][d], pp0(sc[d], t0, t1), pp1(sc[d], t2, t3)) ^ pp2(sc[d], t4);
-            }
-        }
-    }
-    // materialise the rows before the per-row branches below (keeps the selectors short-lived)
-#pragma unroll
-    for (int j = 0; j < M; ++j)
-#pragma unroll
-        for (int d = 0; d < NV; ++d) asm volatile("" : "+v"(acc[j][d]));
-    // the first shard dword of every output row (lane 0, dword 0 of the first pass):
-    // size (bytes 0-1) and payload checksum (2-3)
-    if (first_pass) {
-#pragma unroll
-        for (int c = 0; c < K; ++c) w0_s[c] = (uint32_t)__builtin_amdgcn_readlane((int)x[c][0], 0);
-#pragma unroll
-        for (int j = 0; j < M; ++j) w0_l[j] = (uint32_t)__builtin_amdgcn_readlane((int)acc[j][0], 0);
-    }
-    const int head = checksum ? 4 : 2;
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        if (c < pl.ns && pl.sv_row[c] < K) {
-            sl.store(out_g + (uint64_t)pl.sv_row[c] * pitch, x[c]);
-            sl.mask(x[c], head, head + (int)(w0_s[c] & 0xFFFF));
-            ps_s[c] += sum_vec<NV>(x[c]);
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        if (j < pl.e) {
-            sl.store(out_g + (uint64_t)pl.lost_row[j] * pitch, acc[j]);
-            sl.mask(acc[j], head, head + (int)(w0_l[j] & 0xFFFF));
-            ps_l[j] += sum_vec<NV>(acc[j]);
-        }
-    }
-    if (pl.zero_rows) {
-        uint32_t z[NV];
-#pragma unroll
-        for (int d = 0; d < NV; ++d) z[d] = 0;
-        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) sl.store(out_g + (uint64_t)__builtin_ctz(zr) * pitch, z);
-    }
-#pragma unroll
-    for (int r = 0; r < M; ++r) {
-        if (r < pl.nx) {
-            uint32_t y[NV];
-#pragma unroll
-            for (int d = 0; d < NV; ++d) y[d] = 0;
-            sl.load(y, wire_g + pl.ex_off[r]);
-            sl.mask(y, 0, pl.ex_size[r]);
-            xsum[r] += sum_vec<NV>(y);
-        }
-    }
-}
-
-// all passes over a row of `chunks` 16-B chunks: 16-B passes, <= 16 chunks left over as one
-// dword per lane -- in a pass of its own, or (FUSE_TAIL) riding on the last 16-B pass
-template <int K, int M, bool FUSE_TAIL>
-__device__ __forceinline__ void unpack_row_passes(const UnpackPlan<K, M>& pl, const uint8_t* __restrict__ wire_g,
-                                                  uint8_t* __restrict__ out_g, uint64_t pitch, int lane,
-                                                  int checksum, uint32_t (&dsum)[K], uint32_t (&xsum)[M],
-                                                  uint32_t (&ps_s)[K], uint32_t (&ps_l)[M], uint32_t (&w0_s)[K],
-                                                  uint32_t (&w0_l)[M]) {
-    const int chunks = (int)(pitch / 16);
-    int q0 = 0;
-    for (;;) {
-        const int left = chunks - q0;
-        Slice<4, 0> s0{16 * (q0 + lane), 0, lane, q0 + lane < chunks, 0};
-        if (left <= 0) break;
-        if (left <= 64 && left > 16) {  // a last, partly filled 16-B pass
-            unpack_pass<K, M, 4, 0>(pl, wire_g, out_g, pitch, s0, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
-            break;
-        }
-        const int rest = left - 64;  // chunks after a full 16-B pass
-        if (left <= 16) {  // tail only: 4 bytes per lane
-            Slice<0, 1> st{0, 16 * q0, lane, false, (int)pitch};
-            unpack_pass<K, M, 0, 1>(pl, wire_g, out_g, pitch, st, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
-            break;
-        }
-        if (rest > 0 && rest <= 16 && FUSE_TAIL) {
-            Slice<4, 1> sc{16 * (q0 + lane), 16 * (q0 + 64), lane, true, (int)pitch};
-            unpack_pass<K, M, 4, 1>(pl, wire_g, out_g, pitch, sc, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
-            break;
-        }
-        unpack_pass<K, M, 4, 0>(pl, wire_g, out_g, pitch, s0, q0 == 0, checksum, dsum, xsum, ps_s, ps_l, w0_s, w0_l);
-        q0 += 64;
-    }
-}
-
-template <int K, int M, bool FUSE_TAIL>
-__global__ void __launch_bounds__(256) k_unpack_fused(WireArgs a, const uint8_t* __restrict__ wire,
-                                                      const int32_t* __restrict__ wire_len,
-                                                      const int32_t* __restrict__ lut,
-                                                      const uint32_t* __restrict__ records, uint32_t rec_hdr,
-                                                      uint8_t* __restrict__ shards) {
-    constexpr int N = K + M;
-    const int lane = threadIdx.x & 63;
-    const uint64_t g = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    if (g >= a.groups) return;
-    const uint64_t wp = a.wire_pitch, pitch = a.pitch;
-    const uint8_t* wire_g = wire + g * (uint64_t)N * wp;
-    uint8_t* out_g = shards + g * a.group_stride;
-    // ---- 1. headers
-    int len = 0, hdr = 11, size = 0;
-    uint32_t stated = 0;
-    bool okh = false;
-    if (lane < N) {
-        // the header load does not wait for the length: row starts are always in the buffer
-        len = wire_len[g * N + lane];
-        const uint4 h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
-        const uint32_t tag = get_byte(h, 0);
-        hdr = tag == 0xED ? 13 : 11;
-        const uint32_t ikn = get_byte(h, 9) | (get_byte(h, 10) << 8);
-        okh = len >= 11 && len <= (int)wp && (tag == 0xEC || tag == 0xED) && len >= hdr &&
-              (int)(ikn & 0xF) == N && (int)((ikn >> 4) & 0xF) == K && (int)((ikn >> 8) & 0xF) == lane &&
-              len - hdr <= (int)pitch;
-        size = okh ? len - hdr : 0;
-        stated = get_byte(h, 11) | (get_byte(h, 12) << 8);
-    }
-    const uint32_t rowmask = (1u << N) - 1u;
-    uint32_t good = (uint32_t)__ballot(okh) & rowmask;           // header fine
-    const uint32_t summed13 = (uint32_t)__ballot(okh && hdr == 13) & rowmask;
-    // per-row values for a wave-uniform row r: v_readlane with an SGPR lane index
-    auto r_hdr = [&](int r) { return __builtin_amdgcn_readlane(hdr, r); };
-    auto r_size = [&](int r) { return __builtin_amdgcn_readlane(size, r); };
-    auto r_stated = [&](int r) { return (uint32_t)__builtin_amdgcn_readlane((int)stated, r); };
-    // ---- 2-4, repeated without any survivor whose shard checksum fails
-    uint32_t verified = 0;    // rows whose checksum is known good
-    uint32_t bad = 0;         // rows whose checksum failed
-    uint32_t w0_s[K], w0_l[M], ps_s[K], ps_l[M];
-    UnpackPlan<K, M> pl;
-    bool recoverable = false;
-    uint32_t lost_data = 0;
-    for (int round = 0; round <= N; ++round) {
-        const uint32_t avail = good & ~bad;
-        lost_data = ~avail & ((1u << K) - 1u);
-        recoverable = __builtin_popcount(avail) >= K;
-        pl.ns = 0;
-        pl.e = 0;
-        pl.dec = false;
-        pl.zero_rows = 0;
-        pl.tab = records;
-        uint32_t take = avail;
-        // survivors: the lowest K available rows; unrecoverable: just the available data rows
-        if (!recoverable) {
-            take = avail & ((1u << K) - 1u);
-            pl.zero_rows = lost_data;
-        }
-        uint32_t svmask = 0;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            pl.sv_row[c] = 0;
-            if (take) {
-                pl.sv_row[c] = __builtin_ctz(take);
-                take &= take - 1;
-                pl.ns = c + 1;
-                svmask |= 1u << pl.sv_row[c];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < M; ++j) pl.lost_row[j] = 0;
-        if (recoverable && lost_data) {
-            const int rec = lut[(~avail) & rowmask];
-            pl.tab = records + rec + rec_hdr;
-            pl.e = (int)records[rec];
-            pl.dec = true;
-#pragma unroll
-            for (int j = 0; j < M; ++j) {  // the record header has room for M lost ids
-                const int lr = (int)records[rec + 4 + K + j];
-                pl.lost_row[j] = j < pl.e ? lr : 0;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const int r = pl.sv_row[c];
-            pl.sv_off[c] = (uint32_t)((uint64_t)r * wp + (uint64_t)r_hdr(r));
-            pl.sv_size[c] = c < pl.ns ? r_size(r) : 0;
-        }
-        // rows only checksummed: good headers with a checksum, not loaded as survivors, not yet known
-        uint32_t extra = good & summed13 & ~svmask & ~verified & ~bad;
-        pl.nx = 0;
-#pragma unroll
-        for (int r = 0; r < M; ++r) {
-            pl.ex_row[r] = 0;
-            pl.ex_off[r] = 0;
-            pl.ex_size[r] = 0;
-            if (extra) {
-                const int rr = __builtin_ctz(extra);
-                extra &= extra - 1;
-                pl.ex_row[r] = rr;
-                pl.ex_off[r] = (uint32_t)((uint64_t)rr * wp + 13u);
-                pl.ex_size[r] = r_size(rr);
-                pl.nx = r + 1;
-            }
-        }
-        uint32_t dsum[K], xsum[M];
-#pragma unroll
-        for (int c = 0; c < K; ++c) dsum[c] = ps_s[c] = 0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) xsum[j] = ps_l[j] = 0;
-        unpack_row_passes<K, M, FUSE_TAIL>(pl, wire_g, out_g, pitch, lane, a.checksum, dsum, xsum, ps_s, ps_l, w0_s,
-                                           w0_l);
-        // ---- verdicts
-        uint32_t newbad = 0;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const uint32_t t = wave_total(dsum[c]);
-            ps_s[c] = wave_total(ps_s[c]);
-            if (c < pl.ns) {
-                const int r = pl.sv_row[c];
-                if ((summed13 >> r) & 1u) {
-                    if ((t & 0xFFFFu) != r_stated(r)) newbad |= 1u << r;
-                    else verified |= 1u << r;
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-            const uint32_t t = wave_total(xsum[j]);
-            ps_l[j] = wave_total(ps_l[j]);
-            if (j < pl.nx) {
-                const int r = pl.ex_row[j];
-                if ((t & 0xFFFFu) != r_stated(r)) bad |= 1u << r;
-                else verified |= 1u << r;
-            }
-        }
-        if (!(newbad & svmask)) break;
-        bad |= newbad;
-    }
-    // ---- per-row results
-    const uint32_t okrows = good & ~bad;
-    if (lane < N) {
-        const bool ok = (okrows >> lane) & 1u;
-        if (lane < K) a.marks[g * K + lane] = ok ? 0 : 1;
-        else a.marks[a.groups * K + g * M + (lane - K)] = ok ? 0 : 1;
-        if (a.rx_size) a.rx_size[g * N + lane] = ok ? size : -1;
-    }
-    // dec_src_pkt_info per data row (k_check_payloads' rules)
-    int st = 0, psz = 0;
-    const int head = a.checksum ? 4 : 2;
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        if (c < pl.ns && pl.sv_row[c] < K && lane == pl.sv_row[c]) {
-            psz = (int)(w0_s[c] & 0xFFFF);
-            st = psz >= a.dec_pkt_size || head + psz > (int)pitch ? -1
-                 : a.checksum && (ps_s[c] & 0xFFFFu) != (w0_s[c] >> 16) ? -1 : head;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        if (j < pl.e && lane == pl.lost_row[j]) {
-            psz = (int)(w0_l[j] & 0xFFFF);
-            st = psz >= a.dec_pkt_size || head + psz > (int)pitch ? -1
-                 : a.checksum && (ps_l[j] & 0xFFFFu) != (w0_l[j] >> 16) ? -1 : head;
-        }
-    }
-    if (lane < K && !recoverable && ((lost_data >> lane) & 1u)) {
-        st = -2;
-        psz = 0;
-    }
-    if (lane < K) {
-        a.status[g * K + lane] = st;
-        a.psize[g * K + lane] = psz;
-    }
-}
-
-// ------------------------------------------------------------------ receive, lean single wave
-// k_unpack_v2: k_unpack_fused's rules and layout (one wave per group, the survivors' bytes in
-// register passes), rebuilt after counting what its 675 us go to (rocprofv3 SQ_INSTS_*, r02):
-// ~3 200 VALU and ~1 050 SALU instructions per group, a third of the VALU being v_readlane /
-// v_writelane of 200+ spilled SGPRs (survivor list, sizes, decode tables, checksum words held
-// in SGPR arrays).  The kernel is issue-bound, not HBM-bound.  Here:
-//   * wave-uniform per-row values live in VGPR LANES (v_off, v_rs, v_ss, v_w0), read with one
-//     v_readlane where used; the decode tables are fetched per survivor column next to their
-//     use (an opaque offset keeps them from being hoisted into 150 live SGPRs);
-//   * byte masks only where a pass crosses a boundary (wave-uniform tests), 5 ops per dword;
-//   * a copied row's payload sum is its datagram sum minus its first `head` bytes whenever
-//     the payload reaches the datagram's end (every well-formed datagram); other rows take an
-//     exact slow path.  Decoded rows sum [0, head + size) and subtract the same head bytes.
-// Outputs are identical to k_unpack_fused's.
-__device__ __forceinline__ uint32_t lane_of(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-// v with lane l replaced by the wave-uniform x: one v_writelane_b32 (a `lane == l ? x : v`
-// select makes the compiler hoist a 64-bit lane mask per l into SGPRs, which then spill)
-__device__ __forceinline__ uint32_t set_lane(uint32_t v, int l, uint32_t x) {
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(l));
-    return v;
-}
-
-template <int NVA, int NVT>
-struct RxSl {
-    static constexpr int NV = NVA + NVT;
-    int posa, tail, lane;
-    bool acta;
-    int end;  // row bytes at and past `end` are outside the row
-    __device__ __forceinline__ int pos(int d) const { return d < NVA ? posa + 4 * d : tail + 4 * (lane + 64 * (d - NVA)); }
-    __device__ __forceinline__ bool act(int d) const { return d < NVA ? acta : pos(d) < end; }
-    __device__ __forceinline__ void load(uint32_t (&v)[NV], const uint8_t* row) const {
-        if (acta) {
-            if constexpr (NVA == 4) {
-                uint4 w;
-                __builtin_memcpy(&w, row + posa, 16);
-                v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
-            } else {
-                uint2 w;
-                __builtin_memcpy(&w, row + posa, 8);
-                v[0] = w.x; v[1] = w.y;
-            }
-        }
-#pragma unroll
-        for (int d = NVA; d < NV; ++d)
-            if (act(d)) __builtin_memcpy(&v[d], row + pos(d), 4);
-    }
-    __device__ __forceinline__ void store(uint8_t* row, const uint32_t (&v)[NV]) const {
-        if (acta) {
-            if constexpr (NVA == 4) {
-                st16(row + posa, make_uint4(v[0], v[1], v[2], v[3]));
-            } else {
-                const u32x2 w = {v[0], v[1]};
-                __builtin_nontemporal_store(w, reinterpret_cast<u32x2*>(row + posa));
-            }
-        }
-#pragma unroll
-        for (int d = NVA; d < NV; ++d)
-            if (act(d)) __builtin_nontemporal_store(v[d], reinterpret_cast<uint32_t*>(row + pos(d)));
-    }
-    // keep the row bytes below n: in the NVA part when mask_a, in the tail dwords when mask_t
-    // (wave-uniform flags: a region that lies wholly below n is left alone)
-    __device__ __forceinline__ void keep_below(uint32_t (&v)[NV], int n, bool mask_a, bool mask_t) const {
-        if (mask_a) {
-#pragma unroll
-            for (int d = 0; d < NVA; ++d) v[d] = keep_dw(v[d], n - pos(d));
-        }
-        if (NVT && mask_t) {
-#pragma unroll
-            for (int d = NVA; d < NV; ++d) v[d] = keep_dw(v[d], n - pos(d));
-        }
-    }
-    // un-XOR the dwords this lane loaded (ProtocolUdp frames); the others stay 0
-    __device__ __forceinline__ void xor_act(uint32_t (&v)[NV], uint32_t mm) const {
-#pragma unroll
-        for (int d = 0; d < NV; ++d) v[d] ^= act(d) ? mm : 0u;
-    }
-    __device__ __forceinline__ static uint32_t keep_dw(uint32_t x, int nb) {  // the low nb bytes of x
-        const int c = min(max(nb, 0), 4);
-        return c >= 4 ? x : x & ((1u << (8 * c)) - 1u);
-    }
-};
-
-// the round's plan; wave-uniform per-row values in VGPR lanes
-//   v_off  lane c < K: survivor c's shard bytes (offset from the group's first datagram);
-//          lane K + r: checksum-only row r's
-//   v_rs   lane c < K: survivor row | size << 16; lane K + r: checksum-only row | size << 16;
-//          lane K + M + j: decoded (lost) row j
-template <int K, int M>
-struct RxP {
-    uint32_t v_off, v_rs;
-    uint32_t v_mm;  // frames: lane c survivor c's XOR word, lane K + r checksum-only row r's
-    int ns, e, nx;
-    bool dec, recoverable;
-    uint32_t zero_rows, svmask, lost_data;
-    int min_size, min_xsize;
-    const uint32_t* tab;
-};
-
-template <int K, int M, int NVA, int NVT, int FP = 0>
-__device__ __forceinline__ void rx2_pass(RxP<K, M>& pl, const uint8_t* __restrict__ wire_g, uint8_t* __restrict__ out_g,
-                                         uint64_t pitch, const RxSl<NVA, NVT>& sl, bool first, int head, int end_a,
-                                         int end_t,
-                                         uint32_t& v_w0, uint32_t (&dsum)[K], uint32_t (&xsum)[M], uint32_t (&psl)[M]) {
-    constexpr int NV = NVA + NVT;
-    // opaque per pass: the v_readlane results below are not carried across passes in SGPRs
-    asm volatile("" : "+v"(pl.v_off), "+v"(pl.v_rs), "+v"(v_w0));
-    if constexpr (FP != 0) asm volatile("" : "+v"(pl.v_mm));
-    uint32_t x[K][NV];
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-#pragma unroll
-        for (int d = 0; d < NV; ++d) x[c][d] = 0;
-        if (c < pl.ns) sl.load(x[c], wire_g + lane_of(pl.v_off, c));
-    }
-    if constexpr (FP != 0) {
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-            if (c < pl.ns) sl.xor_act(x[c], lane_of(pl.v_mm, c));
-    }
-    // some survivor's datagram ends inside this pass: keep [0, size) (end_a / end_t: where the
-    // pass's NVA part and tail dwords end)
-    if (end_a > pl.min_size || (NVT && end_t > pl.min_size)) {
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-            sl.keep_below(x[c], (int)(lane_of(pl.v_rs, c) >> 16), end_a > pl.min_size, end_t > pl.min_size);
-    }
-#pragma unroll
-    for (int c = 0; c < K; ++c) dsum[c] += sum_vec<NV>(x[c]);
-    uint32_t acc[M][NV];
-#pragma unroll
-    for (int j = 0; j < M; ++j)
-#pragma unroll
-        for (int d = 0; d < NV; ++d) acc[j][d] = 0;
-    if (pl.dec) {
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            Sel sc[NV];
-#pragma unroll
-            for (int d = 0; d < NV; ++d) sc[d] = gf_sel(x[c][d]);
-            uint32_t toff = (uint32_t)(c * QFEC_TAB_STRIDE);
-            asm volatile("" : "+s"(toff));  // fetch this column's tables here, not all 5 K M up front
-#pragma unroll
-            for (int j = 0; j < M; ++j) {
-                if (j >= pl.e) continue;  // only the group's e decoded rows (wave-uniform)
-                const uint32_t* t = pl.tab + toff + j * K * QFEC_TAB_STRIDE;
-                const uint32_t t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4];
-#pragma unroll
-                for (int d = 0; d < NV; ++d)
-                    acc[j][d] = xor3(acc[j][d], pp0(sc[d], t0, t1), pp1(sc[d], t2, t3)) ^ pp2(sc[d], t4);
-            }
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < M; ++j)
-#pragma unroll
-        for (int d = 0; d < NV; ++d) asm volatile("" : "+v"(acc[j][d]));
-    if (first) {  // lane 0, dword 0 of the first pass: bytes 0-3 of every output row
-#pragma unroll
-        for (int c = 0; c < K; ++c) v_w0 = set_lane(v_w0, c, (uint32_t)__builtin_amdgcn_readlane((int)x[c][0], 0));
-#pragma unroll
-        for (int j = 0; j < M; ++j) v_w0 = set_lane(v_w0, K + j, (uint32_t)__builtin_amdgcn_readlane((int)acc[j][0], 0));
-    }
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        const uint32_t r = lane_of(pl.v_rs, c) & 0xFFFF;
-        if (c < pl.ns && (int)r < K) sl.store(out_g + (uint64_t)r * pitch, x[c]);
-    }
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        if (j < pl.e) {
-            sl.store(out_g + (uint64_t)lane_of(pl.v_rs, K + M + j) * pitch, acc[j]);
-            const int hi = head + (int)(lane_of(v_w0, K + j) & 0xFFFF);  // payload end of decoded row j
-            sl.keep_below(acc[j], hi, end_a > hi, end_t > hi);
-            psl[j] += sum_vec<NV>(acc[j]);
-        }
-    }
-    if (pl.zero_rows) {
-        uint32_t z[NV];
-#pragma unroll
-        for (int d = 0; d < NV; ++d) z[d] = 0;
-        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1)
-            sl.store(out_g + (uint64_t)__builtin_ctz(zr) * pitch, z);
-    }
-#pragma unroll
-    for (int r = 0; r < M; ++r) {
-        if (r < pl.nx) {
-            uint32_t y[NV];
-#pragma unroll
-            for (int d = 0; d < NV; ++d) y[d] = 0;
-            sl.load(y, wire_g + lane_of(pl.v_off, K + r));
-            if constexpr (FP != 0) sl.xor_act(y, lane_of(pl.v_mm, K + r));
-            const int xs = (int)(lane_of(pl.v_rs, K + r) >> 16);
-            sl.keep_below(y, xs, end_a > xs, end_t > xs);
-            xsum[r] += sum_vec<NV>(y);
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t head_bytes_sum(uint32_t w0, int head) {
-    return __builtin_amdgcn_sad_u8(head == 4 ? w0 : (w0 & 0xFFFFu), 0u, 0u);
-}
-
-// LDSW (tuning "wire_rx_lds"; one wave per block, K * pitch bytes of LDS): the passes write the
-// group's K data rows into LDS, and the wave then stores them as one flat byte range, 1 KiB per
-// instruction, so no 64-B line is written in two parts where a row ends mid-line (pitch 1040)
+// frames built in LDS and stored flat (k_frame_udp_rows<.., true>)
 extern __shared__ uint4 rx_stage[];
-
-// FP (frame prefix 4 or 12, qfec_unpack_frames): the rows are ProtocolUdp frames of the
-// datagrams.  Lanes j < n read frame j's mask byte and un-XOR its first 32 bytes: RecvPacket's
-// length and cmd tests (network/ProtocolBasic.cpp:155-199) join the FEC header tests, every
-// survivor / checksum-only load is un-XORed with its row's word, and a row whose frame checksum
-// (prefix bytes + datagram header + the shard sum the passes produce) fails is dropped like a
-// datagram with a bad shard checksum -- RecvPacket returns it before the FEC layer sees it.  In
-// frame mode every good non-survivor row is read and checked (the frame checksum covers rows
-// the datagram checksum does not), and rows whose FEC header is rejected get their checksum
-// from a last per-row pass, so fr.status is RecvPacket's verdict for every row: 0 ok, 1 short,
-// 2 checksum, 3 cmd, 4 too long (as qfec_unframe_udp).
-// TT: tail dwords per lane a row's remainder after the full passes may ride on the last one
-// (1: up to 256 bytes; 2, tuning "wire_rx_split" 4: up to 512, e.g. 1 408 = 1 024 + 384 in one pass
-// on 16-B lanes)
-template <int K, int M, int NVA, bool LDSW = false, int FP = 0, int TT = 1>
-__global__ void __launch_bounds__(LDSW ? 64 : 256) k_unpack_v2(WireArgs a, const uint8_t* __restrict__ wire,
-                                                   const int32_t* __restrict__ wire_len,
-                                                   const int32_t* __restrict__ lut,
-                                                   const uint32_t* __restrict__ records, uint32_t rec_hdr,
-                                                   uint8_t* __restrict__ shards, FrameRecv fr) {
-    constexpr int N = K + M;
-    constexpr int A = 256 * NVA;  // row bytes per full pass
-    const int lane = threadIdx.x & 63;
-    const uint64_t g = __builtin_amdgcn_readfirstlane(LDSW ? blockIdx.x : blockIdx.x * 4u + (threadIdx.x >> 6));
-    if (g >= a.groups) return;
-    const int pitch = (int)a.pitch;
-    const uint64_t wp = a.wire_pitch;
-    const uint8_t* wire_g = wire + g * (uint64_t)N * wp;
-    uint8_t* const out_hbm = shards + g * a.group_stride;
-    uint8_t* out_g = LDSW ? reinterpret_cast<uint8_t*>(rx_stage) : out_hbm;
-    // ---- headers (unpack_fec_head's checks, FecCodecBuf.cpp:334-411)
-    int len = 0, hdr = 11, size = 0;
-    uint32_t stated = 0;
-    bool okh = false;
-    uint32_t v_fx = 0, v_fs = 0;  // frames, lane r: row r's XOR byte; its prefix + header byte sum | check << 24
-    int fst = 0;                  // frames, lane r: RecvPacket's verdict before the checksum
-    if (lane < N) {
-        len = wire_len[g * N + lane];
-        int dlen = len;
-        uint4 h = make_uint4(0u, 0u, 0u, 0u);
-        // rx_skip_lost: a row not received (length <= 0) is not read -- its first line is otherwise
-        // fetched for nothing (3 of 13 rows: ~4 % of the receive's reads), at the price of the
-        // header load waiting for the length
-        const bool rd = !a.rx_skip_lost || len > 0;
-        if constexpr (FP != 0) {
-            const uint8_t* frow = wire_g + (uint64_t)lane * wp;
-            uint4 f0 = make_uint4(0u, 0u, 0u, 0u), f1 = f0;
-            if (rd) {
-                f0 = *reinterpret_cast<const uint4*>(frow);
-                f1 = *reinterpret_cast<const uint4*>(frow + 16);
-            }
-            v_fx = (get_byte(f0, 0) ^ fr.gmask ^ 0x5Au) & 0xFFu;
-            const uint32_t mmx = v_fx * 0x01010101u;
-            const uint4 u0 = xor16(f0, mmx), u1 = xor16(f1, mmx);
-            h = window(u0, u1, FP);
-            dlen = len - FP;
-            const uint32_t cmd = get_byte(u0, 2);
-            fst = len < FP ? 1 : len > (int)wp ? 4 : (cmd & 0xE0u) != 0xA0u ? 3 : 0;
-            uint32_t pre = cmd + get_byte(u0, 3);  // frame bytes 2 .. FP - 1
-            if (FP == 12) {
-                pre = __builtin_amdgcn_sad_u8(u0.y, 0u, __builtin_amdgcn_sad_u8(u0.z, 0u, pre));
-                if (fr.conv_hid && fst == 0) {
-                    fr.conv_hid[2 * (g * N + lane)] = u0.y;
-                    fr.conv_hid[2 * (g * N + lane) + 1] = u0.z;
-                }
-            }
-            v_fs = pre | (get_byte(u0, 1) << 24);
-        } else {
-            if (rd) h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
-        }
-        const uint32_t tag = get_byte(h, 0);
-        hdr = tag == 0xED ? 13 : 11;
-        const uint32_t ikn = get_byte(h, 9) | (get_byte(h, 10) << 8);
-        okh = fst == 0 && dlen >= 11 && dlen <= (int)wp && (tag == 0xEC || tag == 0xED) && dlen >= hdr &&
-              (int)(ikn & 0xF) == N && (int)((ikn >> 4) & 0xF) == K && (int)((ikn >> 8) & 0xF) == lane &&
-              dlen - hdr <= pitch;
-        size = okh ? dlen - hdr : 0;
-        stated = get_byte(h, 11) | (get_byte(h, 12) << 8);
-        if constexpr (FP != 0) v_fs += sum16(mask16(h, 0, hdr), 0);  // the datagram header's bytes
-    }
-    const uint32_t rowmask = (1u << N) - 1u, kmask = (1u << K) - 1u;
-    const uint32_t good = (uint32_t)__ballot(okh) & rowmask;
-    const uint32_t summed = (uint32_t)__ballot(okh && hdr == 13) & rowmask;
-    const uint32_t v_ss = (uint32_t)size | (stated << 16);  // lane r: row r's size | stated checksum
-    // the first round's record, requested before the loads (used unless a survivor fails)
-    const bool rec0_needed = __builtin_popcount(good) >= K && (~good & kmask);
-    const int rec0 = rec0_needed ? __builtin_amdgcn_readfirstlane(lut[~good & rowmask]) : 0;
-    const int head = a.checksum ? 4 : 2;
-    // passes: full passes of A bytes; a remainder of <= 256 bytes rides on the last one as
-    // one tail dword per lane, a longer one is a partial pass of its own
-    const int P = pitch / A, rem = pitch % A;
-    const bool fuse_tail = P > 0 && rem > 0 && rem <= 256 * TT;
-    const int passes = P + ((rem > 0 && !fuse_tail) ? 1 : 0);
-    uint32_t bad = 0, verified = 0, fbad = 0;
-    RxP<K, M> pl;
-    pl.v_mm = 0;
-    uint32_t v_w0 = 0, v_dt = 0;  // lane c: survivor c's dword 0 / datagram total; K + j: decoded row j's
-    for (int round = 0; round <= N; ++round) {
-        // ---- plan: survivors = the lowest K good rows (or the good data rows if too few)
-        const uint32_t avail = good & ~bad;
-        pl.lost_data = ~avail & kmask;
-        pl.recoverable = __builtin_popcount(avail) >= K;
-        pl.zero_rows = pl.recoverable ? 0u : pl.lost_data;
-        pl.v_off = pl.v_rs = 0;
-        pl.ns = 0;
-        pl.min_size = pitch;
-        pl.svmask = 0;
-        uint32_t take = pl.recoverable ? avail : (avail & kmask);
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            if (take) {
-                const int r = __builtin_ctz(take);
-                take &= take - 1;
-                const int sz = __builtin_amdgcn_readlane((int)v_ss, r) & 0xFFFF;
-                pl.v_off = set_lane(pl.v_off, c, (uint32_t)((uint64_t)r * wp + FP + (((summed >> r) & 1u) ? 13u : 11u)));
-                pl.v_rs = set_lane(pl.v_rs, c, (uint32_t)(r | (sz << 16)));
-                if constexpr (FP != 0) pl.v_mm = set_lane(pl.v_mm, c, lane_of(v_fx, r) * 0x01010101u);
-                pl.min_size = min(pl.min_size, sz);
-                pl.ns = c + 1;
-                pl.svmask |= 1u << r;
-            }
-        }
-        pl.dec = pl.recoverable && pl.lost_data;
-        pl.e = 0;
-        pl.tab = records;
-        if (pl.dec) {
-            const int rec = round == 0 ? rec0 : __builtin_amdgcn_readfirstlane(lut[~avail & rowmask]);
-            pl.tab = records + rec + rec_hdr;
-            pl.e = (int)records[rec];
-#pragma unroll
-            for (int j = 0; j < M; ++j)
-                if (j < pl.e) pl.v_rs = set_lane(pl.v_rs, K + M + j, records[rec + 4 + K + j]);
-        }
-        // rows only checksummed (frames: every good row, for its frame checksum)
-        uint32_t extra = good & (FP ? rowmask : summed) & ~pl.svmask & ~verified & ~bad;
-        pl.nx = 0;
-        pl.min_xsize = pitch;
-#pragma unroll
-        for (int r = 0; r < M; ++r) {
-            if (extra) {
-                const int rr = __builtin_ctz(extra);
-                extra &= extra - 1;
-                const int sz = __builtin_amdgcn_readlane((int)v_ss, rr) & 0xFFFF;
-                pl.v_off = set_lane(pl.v_off, K + r, (uint32_t)((uint64_t)rr * wp + FP + (((summed >> rr) & 1u) ? 13u : 11u)));
-                pl.v_rs = set_lane(pl.v_rs, K + r, (uint32_t)(rr | (sz << 16)));
-                if constexpr (FP != 0) pl.v_mm = set_lane(pl.v_mm, K + r, lane_of(v_fx, rr) * 0x01010101u);
-                pl.min_xsize = min(pl.min_xsize, sz);
-                pl.nx = r + 1;
-            }
-        }
-        // ---- the byte passes
-        uint32_t dsum[K], xsum[M], psl[M];
-#pragma unroll
-        for (int c = 0; c < K; ++c) dsum[c] = 0;
-#pragma unroll
-        for (int j = 0; j < M; ++j) xsum[j] = psl[j] = 0;
-        for (int q = 0; q < passes; ++q) {
-            const int base = A * q;
-            if (fuse_tail && q == passes - 1) {
-                RxSl<NVA, TT> sl{base + 4 * NVA * lane, base + A, lane, true, pitch};
-                rx2_pass<K, M, NVA, TT, FP>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, base + A, pitch, v_w0,
-                                              dsum, xsum, psl);
-            } else {
-                RxSl<NVA, 0> sl{base + 4 * NVA * lane, 0, lane, base + 4 * NVA * lane < pitch, pitch};
-                rx2_pass<K, M, NVA, 0, FP>(pl, wire_g, out_g, (uint64_t)pitch, sl, q == 0, head, min(pitch, base + A), 0,
-                                              v_w0, dsum, xsum, psl);
-            }
-        }
-        // ---- verdicts (k_unpack_fused's rules)
-        uint32_t newbad = 0;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const uint32_t t = wave_total(dsum[c]);
-            v_dt = set_lane(v_dt, c, t);
-            if (c < pl.ns) {
-                const int r = (int)(lane_of(pl.v_rs, c) & 0xFFFF);
-                bool rb = false, rv = false;
-                if ((summed >> r) & 1u) {
-                    if ((t & 0xFFFFu) != (lane_of(v_ss, r) >> 16)) rb = true;
-                    else rv = true;
-                }
-                if constexpr (FP != 0) {  // ProtocolUdp::CheckSum over frame bytes 2.. (ProtocolBasic.cpp:80-87)
-                    const uint32_t fs = lane_of(v_fs, r), s = (fs & 0xFFFFFFu) + t;
-                    if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (fs >> 24)) {
-                        rb = true;
-                        fbad |= 1u << r;
-                    } else {
-                        rv = true;
-                    }
-                }
-                if (rb) newbad |= 1u << r;
-                else if (rv) verified |= 1u << r;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-            const uint32_t t = wave_total(xsum[j]);
-            if (j < pl.nx) {
-                const int r = (int)(lane_of(pl.v_rs, K + j) & 0xFFFF);
-                bool rb = ((summed >> r) & 1u) && (t & 0xFFFFu) != (lane_of(v_ss, r) >> 16);
-                if constexpr (FP != 0) {
-                    const uint32_t fs = lane_of(v_fs, r), s = (fs & 0xFFFFFFu) + t;
-                    if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (fs >> 24)) {
-                        rb = true;
-                        fbad |= 1u << r;
-                    }
-                }
-                if (rb) bad |= 1u << r;
-                else verified |= 1u << r;
-            }
-        }
-        if (!(newbad & pl.svmask)) {
-#pragma unroll
-            for (int j = 0; j < M; ++j) v_dt = set_lane(v_dt, K + j, wave_total(psl[j]));
-            break;
-        }
-        bad |= newbad;
-    }
-    if constexpr (LDSW) {  // the K data rows, staged whole, as one flat range
-        wave_lds_sync();
-        const int total = K * pitch;
-        for (int o = 16 * lane; o < total; o += 1024) st16(out_hbm + o, rx_stage[o >> 4]);
-    }
-    // ---- per-row results (k_unpack_fused's)
-    const uint32_t okrows = good & ~bad;
-    if (lane < N) {
-        const bool ok = (okrows >> lane) & 1u;
-        if (lane < K) a.marks[g * K + lane] = ok ? 0 : 1;
-        else a.marks[a.groups * K + g * M + (lane - K)] = ok ? 0 : 1;
-        if (a.rx_size) a.rx_size[g * N + lane] = ok ? size : -1;
-    }
-    int st = 0, psz = 0;
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        const uint32_t rs = lane_of(pl.v_rs, c);
-        const int r = (int)(rs & 0xFFFF), sz = (int)(rs >> 16);
-        if (c < pl.ns && r < K) {
-            const uint32_t w0 = lane_of(v_w0, c);
-            const int p = (int)(w0 & 0xFFFF);
-            uint32_t ps = lane_of(v_dt, c) - head_bytes_sum(w0, head);
-            if (a.checksum && head + p < sz) {  // bytes after the payload inside the datagram: exact sum
-                uint32_t s = 0;
-                const uint8_t* row = wire_g + lane_of(pl.v_off, c);
-                for (int p0 = 0; p0 < sz; p0 += 1024) {
-                    const int pos = p0 + 16 * lane;
-                    if (pos < sz) {
-                        uint4 v = ldu16(row + pos);
-                        if constexpr (FP != 0) v = xor16(v, lane_of(v_fx, r) * 0x01010101u);
-                        v = mask16(v, head - pos, min(sz, head + p) - pos);
-                        s = sum16(v, s);
-                    }
-                }
-                ps = wave_total(s);
-            }
-            if (lane == r) {
-                psz = p;
-                st = psz >= a.dec_pkt_size || head + psz > pitch ? -1
-                     : a.checksum && (ps & 0xFFFFu) != (w0 >> 16) ? -1 : head;
-            }
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        if (j < pl.e && lane == (int)lane_of(pl.v_rs, K + M + j)) {
-            const uint32_t w0 = lane_of(v_w0, K + j);
-            const uint32_t ps = lane_of(v_dt, K + j) - head_bytes_sum(w0, head);
-            psz = (int)(w0 & 0xFFFF);
-            st = psz >= a.dec_pkt_size || head + psz > pitch ? -1
-                 : a.checksum && (ps & 0xFFFFu) != (w0 >> 16) ? -1 : head;
-        }
-    }
-    if (lane < K && !pl.recoverable && ((pl.lost_data >> lane) & 1u)) {
-        st = -2;
-        psz = 0;
-    }
-    if constexpr (FP != 0) {
-        // frames the FEC header rejected were not read by the passes: their RecvPacket checksum,
-        // one row at a time over the wave (only malformed rows come here).  A bad cmd is judged
-        // after the checksum, as RecvPacket does (ProtocolBasic.cpp:167-196), so those rows too.
-        uint32_t chk = (uint32_t)__ballot(lane < N && (fst == 0 || fst == 3) && !okh) & rowmask;
-        while (chk) {
-            const int r = __builtin_ctz(chk);
-            chk &= chk - 1;
-            const int flen = __builtin_amdgcn_readlane(len, r);
-            const uint32_t mmr = lane_of(v_fx, r) * 0x01010101u;
-            const uint8_t* row = wire_g + (uint64_t)r * wp;
-            uint32_t s = 0;
-            for (int pos = 16 * lane; pos < flen; pos += 1024)
-                s = sum16(mask16(xor16(*reinterpret_cast<const uint4*>(row + pos), mmr), 2 - pos, flen - pos), s);
-            s = wave_total(s);
-            if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (lane_of(v_fs, r) >> 24)) fbad |= 1u << r;
-        }
-        if (fr.status && lane < N)
-            fr.status[g * N + lane] = fst == 1 || fst == 4 ? fst : ((fbad >> lane) & 1u) ? 2 : fst;
-    }
-    if (lane < K) {
-        a.status[g * K + lane] = st;
-        a.psize[g * K + lane] = psz;
-    }
-}
 
 // ------------------------------------------------------------------ ProtocolUdp framing
 // The byte stage below FEC on every datagram:
@@ -2430,119 +1570,6 @@ hipError_t launch_pack_frames(const WireArgs& a, const FrameSend& fs, int fp, co
     QFEC_PFC(7, 1)
     QFEC_PFC(8, 4)
 #undef QFEC_PFC
-    return hipSuccess;
-}
-
-#define QFEC_UNPACK_CASE(KK, MM)                                                                        \
-    if (a.k == KK && a.m == MM) {                                                                       \
-        *launched = true;                                                                               \
-        if (rx) return unpack_v2_shape<KK, MM>(a, lut, records, rec_hdr, s, nva);                       \
-        if (tuning().wire_rx_tail)                                                                      \
-            hipLaunchKernelGGL((k_unpack_fused<KK, MM, true>), dim3(waves_grid(a.groups)), dim3(256), 0, s, a, \
-                               a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);    \
-        else                                                                                            \
-            hipLaunchKernelGGL((k_unpack_fused<KK, MM, false>), dim3(waves_grid(a.groups)), dim3(256), 0, s, a, \
-                               a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards);    \
-        *launched = true;                                                                               \
-        return hipGetLastError();                                                                       \
-    }
-
-// the lean single-wave receive for one (K, M): 16-B lanes (NVA 4) or 8-B lanes (NVA 2); fp 4 / 12
-// reads ProtocolUdp frames (qfec_unpack_frames)
-template <int K, int M, int FP>
-hipError_t unpack_v2_launch(const WireArgs& a0, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
-                            hipStream_t s, int nva, const FrameRecv& fr) {
-    WireArgs a = a0;
-    a.rx_skip_lost = tuning().wire_rx_skip_lost;
-    const dim3 grid((unsigned)((a.groups + 3) / 4)), block(256);
-    // the K rows staged in LDS and stored flat (tuning "wire_rx_lds"): 1 where the staging leaves
-    // at least 3/4 of the waves per CU the registers allow (16 on 16-B lanes, 24 on 8-B lanes;
-    // 160 KiB of LDS per CU), 2 whenever the rows fit 16 KiB (A/B).  RS(10,13), 100k groups:
-    // 1 KiB 520 -> 465 us, 512 B 339 -> 291 us; 1400 B on 8-B lanes (11 waves) 691 -> 769 us
-    const size_t stage = (size_t)K * a.pitch;
-    const int lds = tuning().wire_rx_lds;
-    const size_t lds_waves = stage ? (size_t)(160 * 1024) / stage : 0, reg_waves = nva == 4 ? 16 : 24;
-    const uint8_t* w = a.wire;
-    const int32_t* wl = a.wire_len;
-    if (stage <= 16384 && (lds == 2 || (lds == 1 && 4 * lds_waves >= 3 * reg_waves))) {
-        if (nva == 4)
-            hipLaunchKernelGGL((k_unpack_v2<K, M, 4, true, FP>), dim3((unsigned)a.groups), dim3(64), stage, s, a, w, wl,
-                               lut, records, rec_hdr, a.shards, fr);
-        else
-            hipLaunchKernelGGL((k_unpack_v2<K, M, 2, true, FP>), dim3((unsigned)a.groups), dim3(64), stage, s, a, w, wl,
-                               lut, records, rec_hdr, a.shards, fr);
-        return hipGetLastError();
-    }
-    const uint32_t rem16 = (uint32_t)(a.pitch % 1024);
-    if (nva == 4 && tuning().wire_rx_split == 4 && a.pitch > 1024 && rem16 > 256 && rem16 <= 512)
-        hipLaunchKernelGGL((k_unpack_v2<K, M, 4, false, FP, 2>), grid, block, 0, s, a, w, wl, lut, records, rec_hdr,
-                           a.shards, fr);
-    else if (nva == 4)
-        hipLaunchKernelGGL((k_unpack_v2<K, M, 4, false, FP>), grid, block, 0, s, a, w, wl, lut, records, rec_hdr,
-                           a.shards, fr);
-    else
-        hipLaunchKernelGGL((k_unpack_v2<K, M, 2, false, FP>), grid, block, 0, s, a, w, wl, lut, records, rec_hdr,
-                           a.shards, fr);
-    return hipGetLastError();
-}
-
-template <int K, int M>
-hipError_t unpack_v2_shape(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
-                           hipStream_t s, int nva, int fp = 0, const FrameRecv& fr = FrameRecv{}) {
-    if (fp == 4) return unpack_v2_launch<K, M, 4>(a, lut, records, rec_hdr, s, nva, fr);
-    if (fp == 12) return unpack_v2_launch<K, M, 12>(a, lut, records, rec_hdr, s, nva, fr);
-    return unpack_v2_launch<K, M, 0>(a, lut, records, rec_hdr, s, nva, fr);
-}
-
-hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
-                               hipStream_t s, bool* launched) {
-    *launched = false;
-    if (!a.groups) return hipSuccess;
-    // the workgroup-per-group path covers shard pitches up to 768 * kRxMaxWaves bytes
-    // 0: k_unpack_fused; k_unpack_v2 with 1: 16-B lanes when one pass covers the row with most
-    // lanes busy (768 < pitch <= 1280), else 8-B lanes (fewer VGPRs: 85 vs 119); 2: 16-B lanes;
-    // 3: 8-B lanes.  RS(10,13) x 100k, A/B on one box (r02n): 1 KiB payloads 520 us on 16-B
-    // lanes / 566 on 8-B; 1400 B 690 on 8-B / 725 on 16-B; 512 B 337 on 8-B / 411 on 16-B
-    const int rx = tuning().wire_rx_split;
-    const int nva = (rx == 2 || rx == 4) ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
-    QFEC_UNPACK_CASE(10, 3)
-    QFEC_UNPACK_CASE(4, 1)
-    QFEC_UNPACK_CASE(4, 2)
-    QFEC_UNPACK_CASE(2, 2)
-    QFEC_UNPACK_CASE(3, 1)
-    QFEC_UNPACK_CASE(3, 2)
-    QFEC_UNPACK_CASE(5, 1)
-    QFEC_UNPACK_CASE(5, 3)
-    QFEC_UNPACK_CASE(7, 1)
-    QFEC_UNPACK_CASE(8, 4)
-    return hipSuccess;
-}
-#undef QFEC_UNPACK_CASE
-
-// qfec_unpack_frames: unframe + unpack in one pass (k_unpack_v2 with a frame prefix) for the
-// templated shapes; *launched = false otherwise
-hipError_t launch_unpack_frames(const WireArgs& a, const FrameRecv& fr, int fp, const int32_t* lut,
-                                const uint32_t* records, uint32_t rec_hdr, hipStream_t s, bool* launched) {
-    *launched = false;
-    if (!a.groups) return hipSuccess;
-    const int rx = tuning().wire_rx_split;
-    const int nva = (rx == 2 || rx == 4) ? 4 : rx == 3 ? 2 : (a.pitch > 768 && a.pitch <= 1280 ? 4 : 2);
-#define QFEC_UFC(KK, MM)                                                               \
-    if (a.k == KK && a.m == MM) {                                                      \
-        *launched = true;                                                              \
-        return unpack_v2_shape<KK, MM>(a, lut, records, rec_hdr, s, nva, fp, fr);     \
-    }
-    QFEC_UFC(10, 3)
-    QFEC_UFC(4, 1)
-    QFEC_UFC(4, 2)
-    QFEC_UFC(2, 2)
-    QFEC_UFC(3, 1)
-    QFEC_UFC(3, 2)
-    QFEC_UFC(5, 1)
-    QFEC_UFC(5, 3)
-    QFEC_UFC(7, 1)
-    QFEC_UFC(8, 4)
-#undef QFEC_UFC
     return hipSuccess;
 }
 

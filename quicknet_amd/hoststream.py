@@ -197,3 +197,73 @@ def host_encode_leg(code, data, parity, B):
                         "parity in host memory over PCIe)"}
     except Exception as exc:  # report, never fake
         return {"value": None, "verified": False, "error": repr(exc)}
+
+
+def rs_abi_host_leg(G=100_000, k=10, m=3, B=1024, E=3, reps=3, sample_groups=384, seed=0x5EED0005):
+    """module/rs.h unchanged on host memory: reed_solomon_encode then reed_solomon_reconstruct
+    (E random erasures per group) through libqfec.so on arrays of per-shard pointers into pageable
+    numpy buffers (rs.c's own calling convention, module/rs.c:574-643), the config-2 shape.  The
+    same metric as cpu_baseline (data GiB/s of encode + decode).  Verified in full afterwards (the
+    restored rows equal the originals; the parity equals the device encode's); `_sample` carries
+    groups for the cpu_baseline leg's reference rs.c check."""
+    import ctypes as C
+
+    import numpy as np
+
+    from .codec import ReedSolomon, lib
+    n = k + m
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d = torch.empty((G, k, B), dtype=torch.uint8, device=dev)
+    synth_fill(d, seed)
+    p = torch.empty((G, m, B), dtype=torch.uint8, device=dev)
+    Code.cauchy(k, m).encode(d, p)
+    data0 = d.cpu().numpy()
+    par_want = p.cpu().numpy()
+    del d, p
+    data = data0.copy()                      # pageable, as a socket buffer pool would be
+    par = np.zeros((G, m, B), np.uint8)
+    ptr = np.concatenate([data.ctypes.data + np.arange(G * k, dtype=np.uint64) * B,
+                          par.ctypes.data + np.arange(G * m, dtype=np.uint64) * B]).astype(np.uint64)
+    ptrs = (C.c_void_p * (G * n)).from_buffer(ptr)
+    gm = erasure_marks(seed ^ 0xD, G, n, E)
+    marks = np.ascontiguousarray(marks_to_rs_layout(gm, k))
+    lost = gm[:, :k].astype(bool)
+    dec_groups = int(lost.any(1).sum())
+    rs = ReedSolomon(k, m)
+    L = lib()
+    enc_s, rec_s = [], []
+    rc_enc = rc_rec = 0
+    for rep in range(reps + 1):  # the first pass warms the pool, the pinned slots and the tables
+        t0 = time.perf_counter()
+        rc_enc |= L.reed_solomon_encode(rs._h, ptrs, G * n, B)
+        t1 = time.perf_counter()
+        data[lost] = 0x5A                    # the erased rows as the receive buffers hold them
+        t2 = time.perf_counter()
+        rc_rec |= L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(marks.ctypes.data), G * n, B)
+        t3 = time.perf_counter()
+        if rep:
+            enc_s.append(t1 - t0)
+            rec_s.append(t3 - t2)
+    ok = rc_enc == 0 and rc_rec == 0 and np.array_equal(par, par_want) and np.array_equal(data, data0)
+    te, tr = float(np.median(enc_s)), float(np.median(rec_s))
+    idx = np.linspace(0, G - 1, sample_groups).astype(np.int64)
+    out = {"what": f"reed_solomon_encode + reed_solomon_reconstruct ({E} random erasures/group) on per-shard "
+                   f"pointers into pageable host memory, RS({k},{m}) B={B}, {G:,} groups (config 2's shape), "
+                   f"median of {reps} passes after one warm pass",
+           "value": round((G + dec_groups) * k * B / (te + tr) / GIB, 3), "unit": "GiB/s",
+           "encode_gibs": round(G * k * B / te / GIB, 3), "reconstruct_gibs": round(dec_groups * k * B / tr / GIB, 3),
+           "encode_ms": round(te * 1e3, 2), "reconstruct_ms": round(tr * 1e3, 2),
+           "host_threads": _tune_get("host_threads"), "verified": bool(ok),
+           "_sample": {"k": k, "m": m, "B": B, "data": data0[idx].copy(), "par": par[idx].copy(),
+                       "marks_gn": gm[idx].copy(), "restored": data[idx].copy()}}
+    rs.close()
+    del data, par, data0, par_want
+    return out
+
+
+def _tune_get(key):
+    from .codec import tune_get
+    try:
+        return tune_get(key)
+    except Exception:  # an older build (QFEC_LIB_COMPAT A/B) without the knob
+        return None

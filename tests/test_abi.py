@@ -182,17 +182,70 @@ def test_tune_keys_documented_and_accepted():
     keys = re.findall(r'^ \*   "(\w+)"\s+(-?\d+)?', block, re.M)
     assert len(keys) >= 20, keys
     L = lib()
-    for key, first in keys:
-        value = int(first) if first else 0
-        assert L.qfec_tune(key.encode(), value) == 0, (key, value)
-    assert L.qfec_tune(b"no_such_knob", 1) != 0
-    assert L.qfec_tune(b"percall_in", 7) != 0
-    assert L.qfec_tune(b"recon_impl", 99) != 0
-    # back to the defaults the rest of this process expects
-    for key, value in (("recon_impl", -1), ("wire_store_nt", 3), ("percall_resident", 1), ("percall_in", 0),
-                       ("percall_idle_us", 1000), ("percall_timeout_us", 2000000), ("percall_fault", 0),
-                       ("percall_group", 1), ("wire_rx_skip_lost", 0)):
-        assert L.qfec_tune(key.encode(), value) == 0
+    before = {key: qa.tune_get(key) for key, _ in keys}
+    try:
+        for key, first in keys:
+            value = int(first) if first else 0
+            assert L.qfec_tune(key.encode(), value) == 0, (key, value)
+            assert qa.tune_get(key) == value
+        assert L.qfec_tune(b"no_such_knob", 1) != 0
+        assert L.qfec_tune(b"percall_in", 7) != 0
+        assert L.qfec_tune(b"recon_impl", 99) != 0
+        v = C.c_int(0)
+        assert L.qfec_tune_get(b"no_such_knob", C.byref(v)) != 0
+    finally:
+        # back to the values the rest of this process runs with
+        for key, value in before.items():
+            assert L.qfec_tune(key.encode(), value) == 0
+    assert {key: qa.tune_get(key) for key, _ in keys} == before
+
+
+def test_tune_while_encoding_threads():
+    """qfec_tune / qfec_tune_get from one thread while others call the codec (knobs are atomics
+    read per launch decision, SURVEY 8(b) threading).  Without a device the codec calls fail with
+    QFEC_ENODEV every time; on a GPU box they run (tests/test_gpu_rs_host.py checks the bytes)."""
+    import threading
+    L = lib()
+    keys = ("host_chunk", "host_threads", "host_zero_copy", "recon_impl", "encode_impl")
+    before = {k: qa.tune_get(k) for k in keys}
+    stop = threading.Event()
+    errors = []
+
+    def tuner():
+        i = 0
+        while not stop.is_set():
+            for k, vals in (("host_chunk", (0, 3, 17)), ("host_threads", (0, 1, 2)), ("host_zero_copy", (0, 1)),
+                            ("recon_impl", (-1, 3)), ("encode_impl", (-1, 0))):
+                if L.qfec_tune(k.encode(), vals[i % len(vals)]) != 0:
+                    errors.append(k)
+                qa.tune_get(k)
+            i += 1
+
+    def coder(seed):
+        rs = qa.ReedSolomon(4, 2)
+        data = np.zeros((3, 4, 64), np.uint8)
+        par = np.zeros((3, 2, 64), np.uint8)
+        marks = np.zeros(18, np.uint8)
+        for _ in range(200):
+            rc = rs.encode(data, par, 64)
+            if rc not in (0, -2):
+                errors.append(("encode", rc))
+            if rs.reconstruct(data, par, marks, 64) != 0:  # nothing erased: 0 with or without a device
+                errors.append("reconstruct")
+        rs.close()
+
+    t = threading.Thread(target=tuner)
+    coders = [threading.Thread(target=coder, args=(i,)) for i in range(3)]
+    t.start()
+    for c in coders:
+        c.start()
+    for c in coders:
+        c.join()
+    stop.set()
+    t.join()
+    for k, v in before.items():
+        qa.tune(k, v)
+    assert not errors, errors[:5]
 
 
 def test_fec_decode_shuffle_and_pattern_cache(oracle):

@@ -1,0 +1,233 @@
+"""module/rs.h on arrays of caller shard pointers (reed_solomon_encode / reed_solomon_reconstruct,
+module/rs.c:574-643) through libqfec.so: the pipelined host path over many chunks, arrays that mix
+host and device shards, and shards scattered in memory -- all against the CPU oracle, return code
+for return code (unrecoverable groups included).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import quicknet_amd as qa
+from quicknet_amd.synth import erasure_marks, marks_to_rs_layout, synth_bytes
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture
+def knobs():
+    """Set knobs for one test and put back what was there before (qfec_tune_get)."""
+    saved = {}
+
+    def set_(key, value):
+        if key not in saved:
+            saved[key] = qa.tune_get(key)
+        qa.tune(key, value)
+
+    yield set_
+    for key, value in saved.items():
+        qa.tune(key, value)
+
+
+def scattered_rows(G, n, B, seed):
+    """G * n separately allocated host rows of B bytes (not one contiguous batch), in a random order
+    in memory; returns (rows, keepalive)."""
+    rng = np.random.default_rng(seed)
+    pool = np.zeros((G * n + 8, B + 24), np.uint8)
+    order = rng.permutation(G * n)
+    rows = [pool[order[i], 8 + (i % 3) * 8:8 + (i % 3) * 8 + B] for i in range(G * n)]
+    return rows, pool
+
+
+def ptr_array(rows):
+    return (C.c_void_p * len(rows))(*[r.ctypes.data if isinstance(r, np.ndarray) else r.data_ptr() for r in rows])
+
+
+def mixed_marks(G, k, m, seed):
+    """Per group 0..m+1 erasures: some groups lose nothing, some more than the parity can cover."""
+    rng = np.random.default_rng(seed)
+    gm = np.zeros((G, k + m), np.uint8)
+    for g in range(G):
+        e = int(rng.integers(0, m + 2))
+        gm[g, rng.choice(k + m, e, replace=False)] = 1
+    gm[0, :] = 0  # nothing erased
+    gm[1, :m + 1] = 1  # m + 1 data rows erased: unrecoverable
+    return gm
+
+
+@pytest.mark.parametrize("k,m,B", [(10, 3, 1000), (4, 2, 1024), (16, 4, 1400)])
+@pytest.mark.parametrize("zero_copy", [1, 0])
+@pytest.mark.parametrize("chunk,threads", [(7, 4), (0, 0), (1, 1)])
+def test_rs_host_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_copy, chunk, threads):
+    """Many pipelined chunks (host_chunk groups each, two slots alternating), 1 to 4 copy threads,
+    zero copy or staged through the slot's device buffer; shard rows scattered in memory."""
+    knobs("host_zero_copy", zero_copy)
+    knobs("host_chunk", chunk)
+    knobs("host_threads", threads)
+    G, n = 61, k + m
+    rows, _keep = scattered_rows(G, n, B, 5)
+    data0 = synth_bytes(0xA11CE + k, G * k * B).reshape(G, k, B)
+    for i in range(G * k):
+        rows[i][:] = data0.reshape(G * k, B)[i]
+    for i in range(G * k, G * n):
+        rows[i][:] = 0x33
+    rs = qa.ReedSolomon(k, m)
+    L = qa.lib()
+    ptrs = ptr_array(rows)
+    assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == 0
+    want = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(oracle.cauchy(k, m), data0, want, B)
+    got = np.stack(rows[G * k:]).reshape(G, m, B)
+    assert np.array_equal(got, want)
+    # reconstruct with inconsistent parity (pins the survivor rule byte for byte) and erased rows
+    # pre-filled with 0x5A
+    par = synth_bytes(0xBEEF + k, G * m * B).reshape(G, m, B)
+    gm = mixed_marks(G, k, m, 11 + k)
+    marks = marks_to_rs_layout(gm, k)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+    for i in range(G * k):
+        rows[i][:] = d.reshape(G * k, B)[i]
+    for i in range(G * m):
+        rows[G * k + i][:] = par.reshape(G * m, B)[i]
+    rc = L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(marks.ctypes.data), G * n, B)
+    exp = d.copy()
+    rc_o = oracle.rs_reconstruct(oracle.cauchy(k, m), exp, par.copy(), marks, B)
+    assert rc == rc_o == -1
+    assert np.array_equal(np.stack(rows[:G * k]).reshape(G, k, B), exp)
+    assert np.array_equal(np.stack(rows[G * k:]).reshape(G, m, B), par)  # parity never written
+    rs.close()
+
+
+def test_rs_host_pipeline_recoverable_rc0(oracle, knobs):
+    """Every group recoverable -> 0; many chunks."""
+    knobs("host_chunk", 5)
+    k, m, B, G = 10, 3, 1024, 40
+    data0 = synth_bytes(7, G * k * B).reshape(G, k, B)
+    par = np.zeros((G, m, B), np.uint8)
+    rs = qa.ReedSolomon(k, m)
+    assert rs.encode(data0, par, B) == 0
+    gm = erasure_marks(9, G, k + m, 3)
+    marks = marks_to_rs_layout(gm, k)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[:G * k] == 1] = 0
+    assert rs.reconstruct(d, par, marks, B) == 0
+    assert np.array_equal(d, data0)
+    rs.close()
+
+
+@pytest.mark.parametrize("pattern", ["alternate", "data_dev", "parity_dev", "one_dev"])
+def test_rs_mixed_host_device_pointers(oracle, pattern):
+    """A pointer array mixing host and device shards (module/rs.h promises either kind per shard):
+    every pointer is classified, and the mixed array takes a copy per row of whatever kind."""
+    k, m, B, G = 10, 3, 1000, 12
+    n = k + m
+    data0 = synth_bytes(0x31337, G * k * B).reshape(G, k, B)
+    host_rows, _keep = scattered_rows(G, n, B, 3)
+    dev_rows = [torch.zeros(B, dtype=torch.uint8, device=DEV) for _ in range(G * n)]
+
+    def on_dev(i):
+        if pattern == "alternate":
+            return i % 2 == 0
+        if pattern == "data_dev":
+            return i < G * k
+        if pattern == "parity_dev":
+            return i >= G * k
+        return i == 5
+
+    rows = [dev_rows[i] if on_dev(i) else host_rows[i] for i in range(G * n)]
+
+    def put(i, a):
+        if isinstance(rows[i], np.ndarray):
+            rows[i][:] = a
+        else:
+            rows[i].copy_(torch.from_numpy(np.ascontiguousarray(a)).to(DEV))
+
+    def get(i):
+        return rows[i].copy() if isinstance(rows[i], np.ndarray) else rows[i].cpu().numpy()
+
+    for i in range(G * k):
+        put(i, data0.reshape(G * k, B)[i])
+    torch.cuda.synchronize()
+    rs = qa.ReedSolomon(k, m)
+    L = qa.lib()
+    ptrs = ptr_array(rows)
+    assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == 0
+    torch.cuda.synchronize()
+    want = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(oracle.cauchy(k, m), data0, want, B)
+    assert np.array_equal(np.stack([get(G * k + i) for i in range(G * m)]).reshape(G, m, B), want)
+    par = synth_bytes(0x5150, G * m * B).reshape(G, m, B)
+    gm = mixed_marks(G, k, m, 4)
+    marks = marks_to_rs_layout(gm, k)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+    for i in range(G * k):
+        put(i, d.reshape(G * k, B)[i])
+    for i in range(G * m):
+        put(G * k + i, par.reshape(G * m, B)[i])
+    torch.cuda.synchronize()
+    rc = L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(marks.ctypes.data), G * n, B)
+    torch.cuda.synchronize()
+    exp = d.copy()
+    rc_o = oracle.rs_reconstruct(oracle.cauchy(k, m), exp, par.copy(), marks, B)
+    assert rc == rc_o
+    assert np.array_equal(np.stack([get(i) for i in range(G * k)]).reshape(G, k, B), exp)
+    rs.close()
+
+
+def test_rs_host_while_tuning(oracle):
+    """Encodes and reconstructs on host pointers from two threads while a third flips the host
+    knobs (chunking, copy threads, zero copy): every result still equals the oracle's."""
+    import threading
+    keys = ("host_chunk", "host_threads", "host_zero_copy")
+    before = {k: qa.tune_get(k) for k in keys}
+    stop = threading.Event()
+    errors = []
+
+    def tuner():
+        i = 0
+        while not stop.is_set():
+            qa.tune("host_chunk", (0, 3, 17)[i % 3])
+            qa.tune("host_threads", (0, 1, 3)[i % 3])
+            qa.tune("host_zero_copy", i & 1)
+            i += 1
+
+    def coder(seed):
+        k, m, B, G = 10, 3, 512, 23
+        rs = qa.ReedSolomon(k, m)
+        want_p = None
+        for it in range(6):
+            data0 = synth_bytes(seed * 100 + it, G * k * B).reshape(G, k, B)
+            par = np.zeros((G, m, B), np.uint8)
+            if rs.encode(data0, par, B) != 0:
+                errors.append("encode rc")
+            want_p = np.zeros((G, m, B), np.uint8)
+            oracle.rs_encode(oracle.cauchy(k, m), data0, want_p, B)
+            if not np.array_equal(par, want_p):
+                errors.append(("encode", seed, it))
+            marks = marks_to_rs_layout(erasure_marks(seed + it, G, k + m, 3), k)
+            d = data0.copy()
+            d.reshape(G * k, B)[marks[:G * k] == 1] = 0
+            if rs.reconstruct(d, par, marks, B) != 0 or not np.array_equal(d, data0):
+                errors.append(("reconstruct", seed, it))
+        rs.close()
+
+    t = threading.Thread(target=tuner)
+    coders = [threading.Thread(target=coder, args=(s,)) for s in (1, 2)]
+    t.start()
+    for c in coders:
+        c.start()
+    for c in coders:
+        c.join()
+    stop.set()
+    t.join()
+    for k, v in before.items():
+        qa.tune(k, v)
+    assert not errors, errors[:5]

@@ -219,6 +219,7 @@ def test_unpack_row_tails(k, n, checksum, pitch):
     # 16-B lanes with / without LDS-staged rows, 8-B lanes, 16-B lanes with a remainder of up to
     # 512 B on the last pass (1408 = 1024 + 384, 1536, 1296)
     # (the last: rows not received are not read at all, wire_rx_skip_lost 1)
+    saved = {k: qa.tune_get(k) for k in ("wire_rx_split", "wire_rx_lds", "wire_rx_skip_lost")}
     for split, lds, skip in ((2, 1, 0), (2, 0, 0), (3, 1, 0), (4, 0, 0), (1, 1, 1)):
         qa.tune("wire_rx_split", split)
         qa.tune("wire_rx_lds", lds)
@@ -227,9 +228,8 @@ def test_unpack_row_tails(k, n, checksum, pitch):
             sh, status, psize, rx = code.unpack_datagrams(dev(w), dev(rx_len), checksum=bool(checksum), shard_pitch=pitch)
             torch.cuda.synchronize()
         finally:
-            qa.tune("wire_rx_split", 1)
-            qa.tune("wire_rx_lds", 1)
-            qa.tune("wire_rx_skip_lost", 0)
+            for k, v in saved.items():
+                qa.tune(k, v)
         outs.append([t.cpu().numpy() for t in (sh, status, psize, rx)])
     sh, status, psize, rx = outs[0]
     for sh0, status0, psize0, rx0 in outs[1:]:

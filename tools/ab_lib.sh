@@ -10,6 +10,6 @@ NAMES=${@:-before}
 for i in 1 2 3; do
   for n in $NAMES; do
     echo "== $n ($i)"
-    QFEC_LIB=$PWD/tools/_abl/libqfec_$n.so timeout -k 10 120 $CMD 2>&1 | grep -v amdgpu.ids || exit 1
+    QFEC_LIB_COMPAT=1 QFEC_LIB=$PWD/tools/_abl/libqfec_$n.so timeout -k 10 120 $CMD 2>&1 | grep -v amdgpu.ids || exit 1
   done
 done
