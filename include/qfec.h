@@ -243,9 +243,9 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *   "host_threads"     host threads that gather / scatter module/rs.h host shard pointers (0: the
  *                      CPUs this process may use -- affinity and cgroup quota -- at most 32)
  *   "wire_fused"       1 fused datagram send where a (k, m) instance exists | 0 staged build -> encode -> emit
- *   "wire_fused_rx"    1 fused datagram receive | 0 staged parse -> reconstruct -> check
- *   "wire_rx_split"    1 k_unpack_v2, lanes by pitch | 2 16-B | 3 8-B | 4 16-B with a remainder of up
- *                      to 512 B riding on the last pass (2 tail dwords) | 0 the round-1 k_unpack_fused
+ *   "wire_rx"          1 fused datagram receive (k_rx, one wave per group), lanes and LDS staging by
+ *                      pitch | 2 / 3 16-B lanes with / without the K rows staged in LDS | 4 / 5 8-B
+ *                      lanes likewise | 0 staged parse -> reconstruct -> check (3 launches)
  *   "wire_store_nt"    0-3 non-temporal datagram stores (bit 0 body, bit 1 head)
  *   "wire_chunk"       groups per fused send launch pair (0: as many as fit)
  *   "wire_line"        1 the fused send writes whole 64-B lines when the wire pitch is the 64-B
@@ -256,13 +256,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *                      group at 592..1072 B, and on 16-B lanes in two passes at 1104..2112 B (A/B:
  *                      slower) | 3 8-B lanes at 592..1600 B | 4 (A/B) 8-B lanes at 5 waves/SIMD above
  *                      1088 B | 0 body + k_pack_line0
- *   "wire_rx_tail"     1 (k_unpack_fused) tail dwords ride on the last 16-B pass | 0 their own pass
  *   "frame_rows"       2 framing kernels run two rows per wave, loads first, frames built in LDS and
  *                      stored flat (rows <= 2 KiB) | 3 the same, stored directly | 1 | 4
- *   "wire_rx_skip_lost" 1 k_unpack_v2 does not read rows whose length is 0 (not received) | 0 it reads
- *                      every row's header (A/B)
- *   "wire_rx_lds"      1 k_unpack_v2 stages the K data rows in LDS and stores them flat where that
- *                      keeps 3/4 of the waves | 2 whenever they fit 16 KiB | 0 row by row
  *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged
  *   "percall_spin"     1 a per-call launch of one block is waited for by spinning on the completion
  *                      word the kernel stores in coherent pinned memory | 0 hipStreamSynchronize

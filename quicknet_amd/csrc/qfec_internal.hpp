@@ -147,8 +147,8 @@ struct Tuning {
     std::atomic<int> recon_impl{-1};  // -1 auto (per shape), 0 row loop, 1 all rows
     std::atomic<int> encode_impl{-1};   // -1 auto (inputs in halves for k >= 16), 0 all rows, 1 row loop, 2 halves
     std::atomic<int> wire_fused{1};     // fused datagram send where a (k, m) instance exists (0: staged)
-    std::atomic<int> wire_fused_rx{1};  // fused datagram receive likewise
-    std::atomic<int> wire_rx_tail{1};   // fused receive: 1 = tail dwords ride on the last 16-B pass (0: own pass)
+    std::atomic<int> wire_rx{1};        // datagram receive: 1 fused k_rx, lanes and LDS staging by pitch; 2 / 3 16-B lanes
+                                        // with / without LDS staging, 4 / 5 8-B lanes likewise; 0 staged (3 launches)
     std::atomic<int> wire_store_nt{3};  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
     std::atomic<int> wire_line{1};      // fused send writes whole 64-B lines when the wire pitch allows it
     std::atomic<int> wire_send_wave{1}; // fused send, 1088-B wire pitch: one wave per group finishes line 0 itself (k_pack_wave64)
@@ -158,10 +158,7 @@ struct Tuning {
     std::atomic<int> recon_full_lines{1};  // 8-/12-B reconstruct lanes cover the 16-B columns' span (no partial 64-B lines)
     std::atomic<int> recon_compact{1};  // LUT reconstruct reads coefficient tables via the record's offsets + t256
     std::atomic<int> host_zero_copy{1}; // pinned host batches: kernels read/write them directly (0: staged copies)
-    std::atomic<int> wire_rx_lds{1};    // fused receive: K rows staged in LDS, stored flat (one wave per block)
     std::atomic<int> frame_rows{2};     // ProtocolUdp framing: rows per wave, loads issued first (2 or 4; 1: one row per wave)
-    std::atomic<int> wire_rx_split{1};  // fused receive: k_unpack_v2 (1 auto lanes, 2 16-B, 3 8-B); 0 k_unpack_fused
-    std::atomic<int> wire_rx_skip_lost{1};  // k_unpack_v2: rows not received are not read (r04b: 479 vs 483 us)
 };
 Tuning& tuning();
 

@@ -949,16 +949,12 @@ const std::vector<Knob>& knob_table() {
         {"wire_chunk", &tuning().wire_chunk, 0, 0x7FFFFFFF},
         {"wire_send_wave", &tuning().wire_send_wave, 0, 4},
         {"wire_line", &tuning().wire_line, 0, 1},
-        {"wire_rx_tail", &tuning().wire_rx_tail, 0, 1},
-        {"wire_fused_rx", &tuning().wire_fused_rx, 0, 1},
         {"wire_fused", &tuning().wire_fused, 0, 1},
+        {"wire_rx", &tuning().wire_rx, 0, 5},
         {"host_zero_copy", &tuning().host_zero_copy, 0, 1},
         {"recon_compact", &tuning().recon_compact, 0, 2},
         {"recon_full_lines", &tuning().recon_full_lines, 0, 2},
-        {"wire_rx_lds", &tuning().wire_rx_lds, 0, 2},
         {"frame_rows", &tuning().frame_rows, 1, 4},
-        {"wire_rx_split", &tuning().wire_rx_split, 0, 4},
-        {"wire_rx_skip_lost", &tuning().wire_rx_skip_lost, 0, 1},
         {"percall_fast", &g_percall_fast, 0, 1},
         {"percall_spin", &g_percall_spin, 0, 1},
         {"percall_in", &g_percall_in, 0, 1},
@@ -1807,7 +1803,7 @@ int qfec_unpack_datagrams(qfec_code* code, const unsigned char* d_wire, long lon
     a.m = m;
     a.checksum = checksum;
     a.dec_pkt_size = dec_pkt_size;
-    if (tuning().wire_fused_rx && d->d_lut) {
+    if (tuning().wire_rx && d->d_lut) {
         bool launched = false;
         const hipError_t ef =
             launch_unpack_fused(a, d->d_lut, d->d_rec, (uint32_t)record_layout(k, m).hdr, s, &launched);
@@ -1906,7 +1902,7 @@ int qfec_unpack_frames(qfec_code* code, const unsigned char* d_frames, long long
     if (rc) return rc;
     const int k = code->k, m = code->m, n = k + m;
     hipStream_t s = (hipStream_t)stream;
-    if (tuning().wire_fused_rx && d->d_lut) {
+    if (tuning().wire_rx && d->d_lut) {
         WireArgs a{};
         a.shards = d_shards;
         a.pitch = (uint64_t)shard_pitch;

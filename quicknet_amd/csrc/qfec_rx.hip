@@ -193,6 +193,30 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
     return rlane(v, 0) | rlane(v, 32);
 }
 
+// where a row chunk goes: LDSW stages the K data rows in LDS (row r byte b at stage offset
+// r * P + b - X) and stores them flat afterwards, except bytes [0, X) of row 0, which go to HBM
+// directly -- X ends on a 64-B line of HBM, so the split costs no partial line, and the stage is
+// 976 B or more smaller than K * P: RS(10,13) with 1 KiB payloads then fits 16 groups per CU (LDS)
+// instead of 15.  Without LDSW every row goes straight to HBM.
+template <bool LDSW>
+struct RowOut {
+    uint8_t* hbm;  // the group's first data row
+    int P, X;
+    template <int NV>
+    __device__ __forceinline__ void chunk(uint32_t r, int pos, const Chunk<NV>& x) const {
+        if constexpr (LDSW) {
+            if (r == 0 && pos < X) store_chunk<NV, false>(hbm + pos, x);
+            else store_chunk<NV, true>(reinterpret_cast<uint8_t*>(rx_stage) + ((int)r * P + pos - X), x);
+        } else {
+            store_chunk<NV, false>(hbm + r * P + pos, x);
+        }
+    }
+    __device__ __forceinline__ void dw(uint32_t r, int pos, uint32_t x) const {  // pos >= X
+        if constexpr (LDSW) store_dw<true>(reinterpret_cast<uint8_t*>(rx_stage) + ((int)r * P + pos - X), x);
+        else store_dw<false>(hbm + r * P + pos, x);
+    }
+};
+
 // the round's plan: wave-uniform scalars, and per survivor c the values lane c of three VGPRs holds
 template <int K, int M>
 struct Plan {
@@ -212,10 +236,9 @@ struct Plan {
 // the E decoded rows' chunks by the MAC; data survivors and decoded chunks stored; decoded sums.
 // On the first pass, dword 0 of every survivor (lane c of v_w0) and decoded row (dw0[j]).
 template <int K, int M, int NV, bool FR, bool LDSW, int E>
-__device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __restrict__ wire_g, uint8_t* out,
+__device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __restrict__ wire_g, const RowOut<LDSW>& out,
                                         int P, int base, bool first, int head, uint32_t (&dsum)[K],
-                                        uint32_t (&psl)[M], uint32_t& v_w0, uint32_t (&dw0)[M]) {
-    const int lane = threadIdx.x;
+                                        uint32_t (&psl)[M], uint32_t& v_w0, uint32_t (&dw0)[M], int lane) {
     const int pos = base + 4 * NV * lane;
     const bool act = pos < P;
     const int pend = min(P, base + 256 * NV);
@@ -292,15 +315,15 @@ __device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __r
 #pragma unroll
         for (int c = 0; c < K; ++c) {
             const uint32_t r = rlane(pl.v_srow, c) & 0xFFFFu;
-            if (c < pl.ns && r < (uint32_t)K) store_chunk<NV, LDSW>(out + r * P + pos, x[c]);
+            if (c < pl.ns && r < (uint32_t)K) out.chunk(r, pos, x[c]);
         }
 #pragma unroll
-        for (int j = 0; j < E; ++j) store_chunk<NV, LDSW>(out + ((pl.lostw >> (4 * j)) & 0xFu) * P + pos, acc[j]);
+        for (int j = 0; j < E; ++j) out.chunk((pl.lostw >> (4 * j)) & 0xFu, pos, acc[j]);
         if (pl.zero_rows) {
             Chunk<NV> z;
 #pragma unroll
             for (int d = 0; d < NV; ++d) z.d[d] = 0;
-            for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) store_chunk<NV, LDSW>(out + __builtin_ctz(zr) * P + pos, z);
+            for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) out.chunk(__builtin_ctz(zr), pos, z);
         }
     }
 #pragma unroll
@@ -323,9 +346,9 @@ __device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __r
 // L2-resident) and an XOR over the survivor lanes.  Returns the survivors' tail sums in tsum
 // (lanes 4c..4c+3) and the decoded rows' in tpsl (lanes 4j..4j+3)
 template <int K, int M, int NV, bool FR, bool LDSW, int E>
-__device__ __forceinline__ void rx_tail(const Plan<K, M>& pl, const uint8_t* __restrict__ wire_g, uint8_t* out, int P,
-                                        int tb, int head, const uint32_t (&dw0)[M], uint32_t& tsum, uint32_t& tpsl) {
-    const int lane = threadIdx.x;
+__device__ __forceinline__ void rx_tail(const Plan<K, M>& pl, const uint8_t* __restrict__ wire_g, const RowOut<LDSW>& out, int P,
+                                        int tb, int head, const uint32_t (&dw0)[M], uint32_t& tsum, uint32_t& tpsl,
+                                        int lane) {
     const int tc = lane >> 2, td = lane & 3;
     // survivor tc's offset, row | size << 16 and XOR word, from lane tc
     const uint32_t off = (uint32_t)__builtin_amdgcn_ds_bpermute(tc * 4, (int)pl.v_soff);
@@ -340,7 +363,7 @@ __device__ __forceinline__ void rx_tail(const Plan<K, M>& pl, const uint8_t* __r
     }
     x = keep_dw(x, (int)(srw >> 16) - pos);
     tsum = sad(x, 0u);
-    if (tact && (srw & 0xFFFFu) < (uint32_t)K) store_dw<LDSW>(out + (srw & 0xFFFFu) * P + pos, x);
+    if (tact && (srw & 0xFFFFu) < (uint32_t)K) out.dw(srw & 0xFFFFu, pos, x);
     tpsl = 0;
     if constexpr (E > 0) {
         uint32_t res = 0, hi_lane = 0;
@@ -357,12 +380,12 @@ __device__ __forceinline__ void rx_tail(const Plan<K, M>& pl, const uint8_t* __r
             hi_lane = tc == j ? (uint32_t)(head + (int)(dw0[j] & 0xFFFFu)) : hi_lane;
         }
         if (tc < E) {
-            store_dw<LDSW>(out + ((pl.lostw >> (4 * tc)) & 0xFu) * P + pos, res);
+            out.dw((pl.lostw >> (4 * tc)) & 0xFu, pos, res);
             tpsl = sad(keep_dw(res, (int)hi_lane - pos), 0u);
         }
     }
     if (pl.zero_rows && lane < 4)
-        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) store_dw<LDSW>(out + __builtin_ctz(zr) * P + pos, 0u);
+        for (uint32_t zr = pl.zero_rows; zr; zr &= zr - 1) out.dw(__builtin_ctz(zr), pos, 0u);
 }
 
 }  // namespace
@@ -371,7 +394,7 @@ __device__ __forceinline__ void rx_tail(const Plan<K, M>& pl, const uint8_t* __r
 // ProtocolUdp frames with an fp-byte prefix (4, or 12 with the Session's conv/hid), LDSW: the K
 // data rows staged in LDS (K * pitch bytes of dynamic LDS) and stored as one flat range
 template <int K, int M, int NV, bool FR, bool LDSW>
-__global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict__ wire, const int32_t* __restrict__ wire_len,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NV == 4 ? 4 : 5))) k_rx(WireArgs a, const uint8_t* __restrict__ wire, const int32_t* __restrict__ wire_len,
                                            const int32_t* __restrict__ lut, const uint32_t* __restrict__ records,
                                            uint32_t rec_hdr, uint8_t* __restrict__ shards, FrameRecv fr, int fp) {
     static_assert(M >= 1 && K + M <= 15 && K + M <= 32, "datagram groups: n <= 15");
@@ -383,13 +406,18 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
     const uint32_t wp = (uint32_t)a.wire_pitch;
     const uint8_t* wire_g = wire + g * (uint64_t)N * wp;
     uint8_t* const out_hbm = shards + g * a.group_stride;
-    uint8_t* const out = LDSW ? reinterpret_cast<uint8_t*>(rx_stage) : out_hbm;
+    // bytes [0, X) of row 0 straight to HBM, up to a 64-B line of HBM (16-B lanes, rows >= 1 KiB)
+    const int X = (LDSW && NV == 4 && P >= 1024) ? 1024 - (int)(((uintptr_t)out_hbm + 1024) & 63) : 0;
+    const RowOut<LDSW> out{out_hbm, P, X};
     if (!FR) fp = 0;
     // ---- headers (unpack_fec_head's checks, FecCodecBuf.cpp:334-411), one row per lane
     int len = 0, hdr = 11, size = 0;
     uint32_t stated = 0;
     bool okh = false;
-    uint32_t v_fx = 0, v_fs = 0;  // frames, lane r: row r's XOR byte; prefix + header byte sum | check << 24
+    // frames, lane r, packed so little stays live through the passes: bits 0-12 the prefix and
+    // header byte sum, 13-15 RecvPacket's verdict before the checksum, 16-23 the XOR byte, 24-31 the
+    // stated frame check byte
+    uint32_t v_fs = 0, v_fx = 0;
     int fst = 0;                  // frames, lane r: RecvPacket's verdict before the checksum
     if (lane < N) {
         len = wire_len[g * N + lane];
@@ -419,7 +447,7 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
                     fr.conv_hid[2 * (g * N + lane) + 1] = u0.z;
                 }
             }
-            v_fs = pre | (get_byte4(u0, 1) << 24);
+            v_fs = pre | ((uint32_t)fst << 13) | (v_fx << 16) | (get_byte4(u0, 1) << 24);
         } else {
             if (rd) h = *reinterpret_cast<const uint4*>(wire_g + (uint64_t)lane * wp);
         }
@@ -441,6 +469,8 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
     const uint32_t rowmask = (1u << N) - 1u, kmask = (1u << K) - 1u;
     const uint32_t good = (uint32_t)__ballot(okh) & rowmask;
     const uint32_t summed = (uint32_t)__ballot(okh && hdr == 13) & rowmask;
+    // frames: rows the FEC header rejected whose RecvPacket checksum still decides their verdict
+    const uint32_t chk_rows = FR ? (uint32_t)__ballot(lane < N && (fst == 0 || fst == 3) && !okh) & rowmask : 0u;
     const uint32_t v_ss = (uint32_t)size | (stated << 16);  // lane r: row r's size | stated checksum
     // the first round's record, requested before the loads (used unless a survivor fails)
     const bool rec0_needed = __builtin_popcount(good) >= K && (~good & kmask);
@@ -454,6 +484,13 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
     uint32_t v_w0 = 0, v_dt = 0;  // lane c: survivor c's dword 0, shard byte total; lane K + j: decoded row j's
     uint32_t dw0[M];
     for (int round = 0;; ++round) {
+        // the lane id and the group's row base made opaque per round: nothing lane- or
+        // address-derived is hoisted out of this (nearly always single-trip) loop to stay live in
+        // registers across it
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint8_t* wg = wire_g;
+        asm volatile("" : "+s"(wg));
         // ---- plan: survivors = the lowest K good rows (or the good data rows if too few)
         const uint32_t avail = good & ~bad;
         const uint32_t lost_data = ~avail & kmask;
@@ -461,20 +498,20 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
         pl.zero_rows = recoverable ? 0u : lost_data;
         uint32_t take = recoverable ? avail : (avail & kmask);
         pl.ns = min(__builtin_popcount(take), K);
-        // lane c < ns: the c-th set bit of take (its rank among the set bits below it)
-        const uint32_t myrow_bits = lane < N ? (take & ((1u << lane) - 1u)) : 0u;
+        // ln c < ns: the c-th set bit of take (its rank among the set bits below it)
+        const uint32_t myrow_bits = ln < N ? (take & ((1u << ln) - 1u)) : 0u;
         const int rank = __builtin_popcount(myrow_bits);
-        const bool mine = lane < N && ((take >> lane) & 1u) && rank < K;
-        // push row r's (offset, row | size, XOR word) to lane rank (ds_permute: lane rank receives)
-        const uint32_t my_off = (uint32_t)lane * wp + (uint32_t)fp + (((summed >> lane) & 1u) ? 13u : 11u);
-        const uint32_t my_srow = (uint32_t)lane | ((uint32_t)size << 16);
-        const int dst = mine ? rank * 4 : 63 * 4;  // lanes not sending write lane 63 (never a survivor)
+        const bool mine = ln < N && ((take >> ln) & 1u) && rank < K;
+        // push row r's (offset, row | size, XOR word) to ln rank (ds_permute: ln rank receives)
+        const uint32_t my_off = (uint32_t)ln * wp + (uint32_t)fp + (((summed >> ln) & 1u) ? 13u : 11u);
+        const uint32_t my_srow = (uint32_t)ln | ((uint32_t)size << 16);
+        const int dst = mine ? rank * 4 : 63 * 4;  // lanes not sending write ln 63 (never a survivor)
         pl.v_soff = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(mine ? my_off : 0u));
         pl.v_srow = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(mine ? my_srow : 0u));
-        pl.v_smm = FR ? (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(mine ? v_fx * 0x01010101u : 0u)) : 0u;
+        pl.v_smm = FR ? (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(mine ? ((v_fs >> 16) & 0xFFu) * 0x01010101u : 0u)) : 0u;
         const uint32_t sv = (uint32_t)__ballot(mine);  // the survivors' rows
         {  // smallest survivor size (lanes c < ns of v_srow)
-            uint32_t msz = lane < pl.ns ? (pl.v_srow >> 16) : (uint32_t)P;
+            uint32_t msz = ln < pl.ns ? (pl.v_srow >> 16) : (uint32_t)P;
             msz = min(msz, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)msz, 0xB1, 0xF, 0xF, false));
             msz = min(msz, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)msz, 0x4E, 0xF, 0xF, false));
             msz = min(msz, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)msz, 0x124, 0xF, 0xF, false));
@@ -503,8 +540,8 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
         auto run = [&](auto ec) {
             constexpr int E = decltype(ec)::value;
             for (int q = 0; q < passes; ++q)
-                rx_pass<K, M, NV, FR, LDSW, E>(pl, wire_g, out, P, A * q, q == 0, head, dsum, psl, v_w0, dw0);
-            if (tail) rx_tail<K, M, NV, FR, LDSW, E>(pl, wire_g, out, P, A * F, head, dw0, tsum, tpsl);
+                rx_pass<K, M, NV, FR, LDSW, E>(pl, wg, out, P, A * q, q == 0, head, dsum, psl, v_w0, dw0, ln);
+            if (tail) rx_tail<K, M, NV, FR, LDSW, E>(pl, wg, out, P, A * F, head, dw0, tsum, tpsl, ln);
         };
         switch (pl.e) {
             case 0: run(std::integral_constant<int, 0>{}); break;
@@ -513,8 +550,8 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
             case 3: if constexpr (M >= 3) run(std::integral_constant<int, 3>{}); break;
             default: if constexpr (M >= 4) run(std::integral_constant<int, M>{}); break;
         }
-        // ---- totals: survivors' shard sums (lane c of v_dt), decoded rows' payload-prefix sums
-        // (lane K + j)
+        // ---- totals: survivors' shard sums (ln c of v_dt), decoded rows' payload-prefix sums
+        // (ln K + j)
         {
             uint32_t v[K + M], o[K + M];
 #pragma unroll
@@ -525,32 +562,32 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
             uint32_t t = 0;
 #pragma unroll
             for (int i = 0; i < K + M; ++i) t = wlanei(t, i, o[i]);
-            if (tail) {  // plus the lane-mapped tails: lane 4c (4j) holds survivor c's (decoded j's) quad
+            if (tail) {  // plus the ln-mapped tails: ln 4c (4j) holds survivor c's (decoded j's) quad
                 tsum += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tsum, 0xB1, 0xF, 0xF, false);
                 tsum += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tsum, 0x4E, 0xF, 0xF, false);
                 tpsl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tpsl, 0xB1, 0xF, 0xF, false);
                 tpsl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tpsl, 0x4E, 0xF, 0xF, false);
-                const uint32_t ts = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (4 * lane), (int)tsum);
-                const uint32_t tp = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (4 * (lane - K)), (int)tpsl);
-                t += lane < K ? ts : (lane < K + M ? tp : 0u);
+                const uint32_t ts = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (4 * ln), (int)tsum);
+                const uint32_t tp = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (4 * (ln - K)), (int)tpsl);
+                t += ln < K ? ts : (ln < K + M ? tp : 0u);
             }
             v_dt = t;
         }
-        // ---- verdicts on the survivors (k_unpack_fused's rules), lane c for survivor c
-        uint32_t nb = 0, vr = 0, fb = 0;  // lane c: row bit if bad / verified / frame-checksum bad
+        // ---- verdicts on the survivors (k_unpack_fused's rules), ln c for survivor c
+        uint32_t nb = 0, vr = 0, fb = 0;  // ln c: row bit if bad / verified / frame-checksum bad
         {
             const uint32_t r = pl.v_srow & 0xFu, rb_bit = 1u << r;
-            // row r's stated checksum and frame sum, to lane c (every lane takes part in the permutes)
+            // row r's stated checksum and frame sum, to ln c (every ln takes part in the permutes)
             const uint32_t sr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * r), (int)v_ss);
             const uint32_t fs = FR ? (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * r), (int)v_fs) : 0u;
-            if (lane < pl.ns) {
+            if (ln < pl.ns) {
                 bool rb = false, rv = false;
                 if ((summed >> r) & 1u) {
                     if ((v_dt & 0xFFFFu) != (sr >> 16)) rb = true;
                     else rv = true;
                 }
                 if constexpr (FR) {  // ProtocolUdp::CheckSum over frame bytes 2.. (ProtocolBasic.cpp:80-87)
-                    const uint32_t s = (fs & 0xFFFFFFu) + v_dt;
+                    const uint32_t s = (fs & 0x1FFFu) + v_dt;
                     if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (fs >> 24)) {
                         rb = true;
                         fb = rb_bit;
@@ -573,11 +610,11 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
                 const int r = __builtin_ctz(extra);
                 extra &= extra - 1;
                 const int xs = (int)(rlane(v_ss, r) & 0xFFFFu);
-                const uint32_t mm = FR ? rlane(v_fx, r) * 0x01010101u : 0u;
-                const uint8_t* row = wire_g + (uint64_t)r * wp + fp + (((summed >> r) & 1u) ? 13u : 11u);
+                const uint32_t mm = FR ? ((rlane(v_fs, r) >> 16) & 0xFFu) * 0x01010101u : 0u;
+                const uint8_t* row = wg + (uint64_t)r * wp + fp + (((summed >> r) & 1u) ? 13u : 11u);
                 uint32_t s = 0;
                 for (int p0 = 0; p0 < P; p0 += 1024) {
-                    const int pos = p0 + 16 * lane;
+                    const int pos = p0 + 16 * ln;
                     if (pos < P) {
                         uint4 w;
                         __builtin_memcpy(&w, row + pos, 16);
@@ -590,7 +627,7 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
                 const uint32_t t = wave_total(s);
                 bool rb = ((summed >> r) & 1u) && (t & 0xFFFFu) != (rlane(v_ss, r) >> 16);
                 if constexpr (FR) {
-                    const uint32_t fs = rlane(v_fs, r), s2 = (fs & 0xFFFFFFu) + t;
+                    const uint32_t fs = rlane(v_fs, r), s2 = (fs & 0x1FFFu) + t;
                     if ((~((s2 >> 16) + (s2 & 0xFFFFu)) & 0xFFu) != (fs >> 24)) {
                         rb = true;
                         fbad |= 1u << r;
@@ -606,7 +643,7 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
     if constexpr (LDSW) {  // the K data rows, staged whole, as one flat range
         wave_lds_sync();
         const int total = K * P;
-        for (int o = 16 * lane; o < total; o += 1024) st16(out_hbm + o, rx_stage[o >> 4]);
+        for (int o = X + 16 * lane; o < total; o += 1024) st16(out_hbm + o, rx_stage[(o - X) >> 4]);
     }
     // ---- per-row results
     const uint32_t okrows = good & ~bad;
@@ -614,7 +651,7 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
         const bool ok = (okrows >> lane) & 1u;
         if (lane < K) a.marks[g * K + lane] = ok ? 0 : 1;
         else a.marks[a.groups * K + g * M + (lane - K)] = ok ? 0 : 1;
-        if (a.rx_size) a.rx_size[g * N + lane] = ok ? size : -1;
+        if (a.rx_size) a.rx_size[g * N + lane] = ok ? (int)(v_ss & 0xFFFFu) : -1;
     }
     // dec_src_pkt_info (FecCodecBuf.cpp:109-133): lane c < ns for survivor c (when a data row),
     // lane K + j for decoded row j; each writes its own row's status
@@ -677,12 +714,12 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
         // frames the FEC header rejected were not read by the passes: their RecvPacket checksum,
         // one row at a time over the wave (only malformed rows come here).  A bad cmd is judged
         // after the checksum, as RecvPacket does (ProtocolBasic.cpp:167-196), so those rows too.
-        uint32_t chk = (uint32_t)__ballot(lane < N && (fst == 0 || fst == 3) && !okh) & rowmask;
+        uint32_t chk = chk_rows;
         while (chk) {
             const int r = __builtin_ctz(chk);
             chk &= chk - 1;
-            const int flen = __builtin_amdgcn_readlane(len, r);
-            const uint32_t mmr = rlane(v_fx, r) * 0x01010101u;
+            const int flen = wire_len[g * N + r];
+            const uint32_t mmr = ((rlane(v_fs, r) >> 16) & 0xFFu) * 0x01010101u;
             const uint8_t* row = wire_g + (uint64_t)r * wp;
             uint32_t s = 0;
             for (int pos = 16 * lane; pos < flen; pos += 1024) {
@@ -698,7 +735,10 @@ __global__ void __launch_bounds__(64) k_rx(WireArgs a, const uint8_t* __restrict
             if ((~((s >> 16) + (s & 0xFFFFu)) & 0xFFu) != (rlane(v_fs, r) >> 24)) fbad |= 1u << r;
         }
         if (fr.status && lane < N)
-            fr.status[g * N + lane] = fst == 1 || fst == 4 ? fst : ((fbad >> lane) & 1u) ? 2 : fst;
+        {
+            const int fs0 = (int)((v_fs >> 13) & 7u);
+            fr.status[g * N + lane] = fs0 == 1 || fs0 == 4 ? fs0 : ((fbad >> lane) & 1u) ? 2 : fs0;
+        }
     }
     // data rows no survivor or decoded row wrote: 0, or -2 where lost and not recoverable
     const uint32_t written = wave_or(orow >= 0 ? 1u << orow : 0u);
@@ -717,13 +757,20 @@ hipError_t rx_launch(const WireArgs& a, const int32_t* lut, const uint32_t* reco
     // lanes: 16 B where one pass covers most of the row (768 < pitch <= 1280), else 8 B.  The K
     // data rows are staged in LDS where that leaves at least 3/4 of the waves per CU the registers
     // allow (16 on 16-B lanes, 24 on 8-B lanes; 160 KiB of LDS per CU): RS(10,13) 1 KiB payloads
-    // yes, 1 400-B payloads (14 KB per group) no
-    const bool lanes16 = a.pitch > 768 && a.pitch <= 1280;
+    // yes, 1 400-B payloads (14 KB per group) no.  Tuning "wire_rx" 2..5 forces a lane width and
+    // staging (tests hold every form to the same outputs)
+    const int rx = tuning().wire_rx;
     const size_t stage = (size_t)K * a.pitch;
+    bool lanes16 = a.pitch > 768 && a.pitch <= 1280;
     const size_t lds_waves = (size_t)(160 * 1024) / stage, reg_waves = lanes16 ? 16 : 24;
-    const bool ldsw = stage <= 16384 && 4 * lds_waves >= 3 * reg_waves;
+    bool ldsw = stage <= 16384 && 4 * lds_waves >= 3 * reg_waves;
+    if (rx >= 2) {
+        lanes16 = rx <= 3;
+        ldsw = (rx == 2 || rx == 4) && stage <= 65536;
+    }
     const dim3 grid((unsigned)a.groups), block(64);
-    const size_t sh = ldsw ? stage : 0;
+    // (the first 976..1024 bytes of row 0 bypass the stage on 16-B lanes, rows >= 1 KiB)
+    const size_t sh = ldsw ? stage - (lanes16 && a.pitch >= 1024 ? 976 : 0) : 0;
     if (lanes16) {
         if (ldsw) hipLaunchKernelGGL((k_rx<K, M, 4, FR, true>), grid, block, sh, s, a, a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards, fr, fp);
         else hipLaunchKernelGGL((k_rx<K, M, 4, FR, false>), grid, block, sh, s, a, a.wire, (const int32_t*)a.wire_len, lut, records, rec_hdr, a.shards, fr, fp);

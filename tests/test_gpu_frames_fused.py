@@ -182,17 +182,15 @@ def test_unpack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session):
     torch.cuda.synchronize()
     want = [t.cpu().numpy() for t in want]
     outs = []
-    saved = {k: qa.tune_get(k) for k in ("wire_fused_rx", "wire_rx_skip_lost")}
-    for fused, skip in ((1, 0), (0, 0), (1, 1)):  # one pass, two calls, one pass not reading lost rows
-        qa.tune("wire_fused_rx", fused)
-        qa.tune("wire_rx_skip_lost", skip)
+    saved = qa.tune_get("wire_rx")
+    for rxk in (1, 0, 3, 4):  # one pass (auto, 16-B lanes unstaged, 8-B lanes staged), two calls
+        qa.tune("wire_rx", rxk)
         try:
             got = code.unpack_frames(dev(f), dev(fl), gmask=GMASK, session=session, checksum=bool(checksum),
                                      shard_pitch=sp)
             torch.cuda.synchronize()
         finally:
-            for k, v in saved.items():
-                qa.tune(k, v)
+            qa.tune("wire_rx", saved)
         outs.append([t.cpu().numpy() if t is not None else None for t in got])
     for sh, status, psize, rx, fst, cho in outs:
         assert np.array_equal(fst, st_ref)

@@ -30,11 +30,12 @@ def wire_fused(request):
     """Both datagram paths: fused (send: body + head launches; receive: one launch; templated
     (k, m)) and staged (build -> encode -> emit, parse -> reconstruct -> check), which every
     shape can take."""
+    saved = {kk: qa.tune_get(kk) for kk in ("wire_fused", "wire_rx")}
     qa.tune("wire_fused", request.param[0])
-    qa.tune("wire_fused_rx", request.param[0])
+    qa.tune("wire_rx", request.param[0])
     yield request.param
-    qa.tune("wire_fused", 1)
-    qa.tune("wire_fused_rx", 1)
+    for kk, v in saved.items():
+        qa.tune(kk, v)
 
 
 @pytest.fixture(params=[64, 16], ids=["wire64", "wire16"])
@@ -186,11 +187,11 @@ def test_pack_oversize_group(wire_fused):
                                                 (10, 13, 1, 528), (7, 8, 1, 544), (3, 5, 1, 1280), (10, 13, 1, 1408),
                                                 (4, 6, 0, 1408), (5, 8, 1, 1536), (10, 13, 1, 1296)])
 def test_unpack_row_tails(k, n, checksum, pitch):
-    """Shard pitches whose last pass leaves a short row tail (1040 = 1024 + 16, 1056, 1088, 528,
-    544, 1280; k_unpack_v2 runs it as tail dwords on the last pass; 1408, 1536, 1296 with two tail
-    dwords under wire_rx_split 4): every data packet of a
-    recoverable group comes back exactly, on 16-B lanes with and without the LDS-staged flat row
-    stores (wire_rx_lds) and on 8-B lanes (all give the same shard rows, verdicts and sizes).  Losses up to m + 1 per group, some datagrams corrupted
+    """Shard pitches whose passes leave a short row tail (1040 = 1024 + 16 and 528 = 512 + 16: k_rx
+    runs the tail lane-mapped; 1056, 1088, 544, 1280, 1408, 1536, 1296: a partial last pass): every
+    data packet of a recoverable group comes back exactly, and every form of the receive -- 16-B and
+    8-B lanes, with and without the rows staged in LDS, and the staged three-launch path -- gives
+    the same shard rows, verdicts and sizes.  Losses up to m + 1 per group, some datagrams corrupted
     inside the row tail, half the rows full to the pitch's limit."""
     rng = np.random.default_rng(pitch * 31 + k)
     G, m = 300, n - k
@@ -216,20 +217,16 @@ def test_unpack_row_tails(k, n, checksum, pitch):
                 w[g, j, wl[g, j] - 1] ^= 0x10  # a byte inside the row tail
     rx_len = np.where(drop, 0, wl).astype(np.int32)
     outs = []
-    # 16-B lanes with / without LDS-staged rows, 8-B lanes, 16-B lanes with a remainder of up to
-    # 512 B on the last pass (1408 = 1024 + 384, 1536, 1296)
-    # (the last: rows not received are not read at all, wire_rx_skip_lost 1)
-    saved = {k: qa.tune_get(k) for k in ("wire_rx_split", "wire_rx_lds", "wire_rx_skip_lost")}
-    for split, lds, skip in ((2, 1, 0), (2, 0, 0), (3, 1, 0), (4, 0, 0), (1, 1, 1)):
-        qa.tune("wire_rx_split", split)
-        qa.tune("wire_rx_lds", lds)
-        qa.tune("wire_rx_skip_lost", skip)
+    # every form of the fused receive (tuning "wire_rx": 1 auto, 2 / 3 16-B lanes with / without
+    # the rows staged in LDS, 4 / 5 8-B lanes likewise) and the staged three-launch path (0)
+    saved = qa.tune_get("wire_rx")
+    for rxk in (1, 2, 3, 4, 5, 0):
+        qa.tune("wire_rx", rxk)
         try:
             sh, status, psize, rx = code.unpack_datagrams(dev(w), dev(rx_len), checksum=bool(checksum), shard_pitch=pitch)
             torch.cuda.synchronize()
         finally:
-            for k, v in saved.items():
-                qa.tune(k, v)
+            qa.tune("wire_rx", saved)
         outs.append([t.cpu().numpy() for t in (sh, status, psize, rx)])
     sh, status, psize, rx = outs[0]
     for sh0, status0, psize0, rx0 in outs[1:]:

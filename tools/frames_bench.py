@@ -98,7 +98,7 @@ def main():
     def recv2():
         ok(L.qfec_unframe_udp(fr1.data_ptr(), fpitch, rx_len.data_ptr(), G * n, 0x3C, int(a.session), dgr.data_ptr(),
                               fpitch, dlen.data_ptr(), fst.data_ptr(), None, None, st))
-        qa.lib().qfec_tune(b"wire_fused_rx", 1)
+        qa.lib().qfec_tune(b"wire_rx", 1)
         ok(L.qfec_unpack_datagrams(code._h, dgr.data_ptr(), fpitch, dlen.data_ptr(), G, 1, 2068, osh.data_ptr(), sp,
                                    marks.data_ptr(), rxs.data_ptr(), status.data_ptr(), psize.data_ptr(), st))
 

@@ -16,8 +16,7 @@ import torch  # noqa: E402
 
 import quicknet_amd as qa  # noqa: E402
 
-KNOBS = {"wire_fused": 1, "wire_store_nt": 3, "wire_fused_rx": 1, "wire_rx_tail": 1, "wire_chunk": 0, "wire_rx_split": 1, "wire_rx_lds": 1, "wire_send_wave": 1,
-         "wire_line": 1, "wire_rx_skip_lost": 0}
+KNOBS = {"wire_fused": 1, "wire_store_nt": 3, "wire_rx": 1, "wire_chunk": 0, "wire_send_wave": 1, "wire_line": 1}
 
 
 def main():
