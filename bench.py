@@ -63,7 +63,7 @@ GIB = float(1 << 30)
 KERNEL_SOURCES = ("quicknet_amd/csrc/qfec_kernels.hip", "quicknet_amd/csrc/qfec_internal.hpp",
                   "quicknet_amd/csrc/qfec_device.hpp")
 # ... and those of the datagram / framing legs (their own traffic.json entry)
-WIRE_KERNEL_SOURCES = KERNEL_SOURCES + ("quicknet_amd/csrc/qfec_wire.hip",)
+WIRE_KERNEL_SOURCES = KERNEL_SOURCES + ("quicknet_amd/csrc/qfec_wire.hip", "quicknet_amd/csrc/qfec_rx.hip")
 TRAFFIC_PATH = os.path.join(ROOT, "profiles", "traffic.json")
 
 
@@ -925,11 +925,10 @@ def load_traffic(path, workload_key, sources=KERNEL_SOURCES):
     if ent.get("kernel_sources_sha256") != want:
         return None, f"stale: measured on kernel sources {ent.get('kernel_sources_sha256')}, now {want}"
     run = ent.get("run", "PMC run")
-    # the counter CSVs behind the entry: profiles/<run>_pmc/ or profiles/<run>/pmc/ (tracked)
-    csv = next((d for d in (f"profiles/{run}_pmc", f"profiles/{run}/pmc") if os.path.isdir(os.path.join(ROOT, d))),
-               None)
-    return ent, (f"{os.path.relpath(path, ROOT)} ({run}, kernel sources {want}; counter CSVs "
-                 f"{csv or 'not found under profiles/'})")
+    # the counter CSVs behind the entry, as tracked in the repository (the entry names them; they
+    # are not shipped to the GPU box, so their presence here says nothing)
+    csv = ent.get("csv") or f"profiles/{run}/pmc"
+    return ent, f"{os.path.relpath(path, ROOT)} ({run}, kernel sources {want}; counter CSVs {csv}/)"
 
 
 def kernel_sources_hash(sources=KERNEL_SOURCES):

@@ -23,8 +23,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"encode": "k_encode_perm<{k}, {m}>", "reconstruct": "k_reconstruct_perm<{k}, {m},", "probe": "k_probe_xor"}
 # --workload wire: bench.py's `wire` leg (tools/side_legs.py), RS(10,13) 1 KiB payloads
-WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0, 1, 16, 0>", "unpack": "k_unpack_v2<10, 3, 4, true, 0, 1>",
-                "pack_frames": "k_pack_wave64<10, 3, 1, 4, 1, 16, 0>", "unpack_frames": "k_unpack_v2<10, 3, 4, true, 4, 1>"}
+WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0, 1, 16, 0>", "unpack": "k_rx<10, 3, 4, false, true>",
+                "pack_frames": "k_pack_wave64<10, 3, 1, 4, 1, 16, 0>", "unpack_frames": "k_rx<10, 3, 4, true, true>"}
 
 
 def run_pass(counter, out, bench_args, k, m, kernels=KERNELS, script="bench.py"):
@@ -62,6 +62,9 @@ def main():
     p.add_argument("--groups", type=int, default=100_000)
     p.add_argument("--tag", default="PMC run", help="which run produced the numbers (recorded in the JSON)")
     p.add_argument("--workload", choices=["headline", "wire"], default="headline")
+    p.add_argument("--csv-home", default=None,
+                   help="where the counter CSVs are kept in the repository (default profiles/<tag>/pmc): recorded "
+                        "in the JSON so the bench line names tracked files whether or not they travel to the box")
     a = p.parse_args()
     if a.workload == "wire":
         return wire_main(a)
@@ -97,6 +100,7 @@ def main():
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; bytes = 2*FETCH_SIZE*1024 "
                   "+ WRITE_SIZE*1024 (gfx950 corrections, MI355X_MICROARCH.md HBM section)",
         "raw": res,
+        "csv": a.csv_home or f"profiles/{a.tag}/pmc",
     }
     os.makedirs(os.path.dirname(a.json), exist_ok=True)
     with open(a.json, "w") as fh:
@@ -131,7 +135,7 @@ def wire_main(a):
     doc[key] = {"kernel_sources_sha256": kernel_sources_hash(WIRE_KERNEL_SOURCES), "run": a.tag,
                 "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over tools/side_legs.py; "
                           "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 corrections)",
-                "raw": res}
+                "raw": res, "csv": a.csv_home or f"profiles/{a.tag}/pmc"}
     for k2, v in res.items():
         doc[key][k2] = v["bytes_per_launch"]
     with open(a.json, "w") as fh:
