@@ -230,55 +230,45 @@ int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long s
 int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long long groups, int k, int m,
                       int block_size, long long pitch, void *stream);
 
-/* Experiment knobs for interleaved A/B timing (tools/ab.py, tools/wire_ab.py).  Defaults are
- * the measured best; results are identical either way.
- *   "encode_impl"      -1 auto (2 for k >= 16, else 0) | 0 all rows | 1 row loop | 2 all rows, the inputs
- *                      loaded in two halves (fewer registers, more waves per SIMD)
- *   "recon_impl"       -1 auto | 0 row loop | 1 all rows | 2 exact-e rows on 16-B lanes | 3 on 8-B | 4 on 12-B | 5 one wave per group on 8-B slabs | 6 = 3 at 8 waves/SIMD | 8 = 3 with one group per block (auto picks it for 3 where a group is <= 4 waves)
- *   "recon_compact"    1 tables via the 256-entry table at the record header's offsets | 0 from the record
- *   "recon_full_lines" 1 8-/12-B lanes cover the 16-B columns' span for k < 14 | 2 always | 0 stop at B
+/* Knobs.  Integration settings: host chunking, host copy threads, zero copy, the per-call
+ * server's footprint.  Plus one A/B switch per kernel family (tools/ab.py, tools/wire_ab.py)
+ * and one test hook.  Defaults are the measured best; outputs are identical either way.
  *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies
  *   "host_chunk"       groups per staged host chunk (0: by bytes: ~32 MiB for qfec_*_host, ~16 MiB of
  *                      caller shards for module/rs.h on host pointers)
  *   "host_threads"     host threads that gather / scatter module/rs.h host shard pointers (0: the
  *                      CPUs this process may use -- affinity and cgroup quota -- at most 32)
- *   "wire_fused"       1 fused datagram send where a (k, m) instance exists | 0 staged build -> encode -> emit
- *   "wire_rx"          1 fused datagram receive (k_rx, one wave per group), lanes and LDS staging by
- *                      pitch | 2 / 3 16-B lanes with / without the K rows staged in LDS | 4 / 5 8-B
- *                      lanes likewise | 0 staged parse -> reconstruct -> check (3 launches)
- *   "wire_store_nt"    0-3 non-temporal datagram stores (bit 0 body, bit 1 head)
- *   "wire_chunk"       groups per fused send launch pair (0: as many as fit)
- *   "wire_line"        1 the fused send writes whole 64-B lines when the wire pitch is the 64-B
- *                      multiple above 13 + shard pitch (body + k_pack_line0) | 0 body + k_pack_head
- *   "wire_send_wave"   1 at a 1088-B (576-B) wire pitch one wave holds one (two) groups and writes
- *                      their rows' first lines itself (k_pack_wave64); at 1104..1600 B (e.g. 1472 for
- *                      1400-B payloads) the same on 8-byte lanes in three passes | 2 also one wave per
- *                      group at 592..1072 B, and on 16-B lanes in two passes at 1104..2112 B (A/B:
- *                      slower) | 3 8-B lanes at 592..1600 B | 4 (A/B) 8-B lanes at 5 waves/SIMD above
- *                      1088 B | 0 body + k_pack_line0
- *   "frame_rows"       2 framing kernels run two rows per wave, loads first, frames built in LDS and
- *                      stored flat (rows <= 2 KiB) | 3 the same, stored directly | 1 | 4
- *   "percall_fast"     1 fec_encode / fec_decode through the one-launch per-call kernel | 0 staged
- *   "percall_spin"     1 a per-call launch of one block is waited for by spinning on the completion
- *                      word the kernel stores in coherent pinned memory | 0 hipStreamSynchronize
  *   "percall_resident" 1 fec_encode / fec_decode of packets up to 4 KiB with k <= 16 and k * e <= 64
  *                      go to a resident one-block server that polls a request word in device memory
- *                      and exits by itself after 1 ms without a request | 0 one launch per call
- *                      (setting 0 stops the servers)
- *   "percall_in"       0 the server's input rows in device memory | 1 in write-combined pinned host
- *                      memory (A/B: 0.9 us slower per call)
+ *                      and exits by itself after percall_idle_us without a request | 0 one launch per
+ *                      call (setting 0 stops the servers)
  *   "percall_idle_us"  how long the resident server's block stays on the device after its last
  *                      request, 0 .. 1 000 000 us (default 1 000); 0 = it exits right after each
  *                      call (every call then pays a launch).  A hipDeviceSynchronize issued while it
  *                      is resident waits for it: at most this long after the last call.
  *   "percall_timeout_us" how long a call spins for the server before it stops the block and waits
  *                      for it (the block serves the pending request first), or, if the request was
- *                      never taken, runs it through one launch (default 2 000 000)
+ *                      never taken, runs it through one launch (default 2 000 000).  The wait after
+ *                      the timeout is NOT bounded: it lasts until the block gets a CU and exits (a
+ *                      device whose every CU is held by other persistent kernels keeps the call
+ *                      waiting)
+ *   "percall_fast"     1 per-packet calls on host packets through the server / one launch on mapped
+ *                      pinned staging | 0 the staged DMA path (the one device-pointer packets take)
+ * A/B, one per kernel family:
+ *   "encode_impl"      -1 auto (2 for k >= 16, else 0) | 0 all rows | 2 all rows, the inputs loaded in
+ *                      two halves (fewer registers, more waves per SIMD)
+ *   "recon_impl"       -1 auto | exact-e rows on 2 16-B lanes | 3 8-B lanes | 4 12-B lanes | 8 = 3 with
+ *                      one group per block (auto picks it for 3 where a group is <= 4 waves)
+ *   "wire_fused"       1 fused datagram send where a (k, m) instance exists | 0 staged build -> encode -> emit
+ *   "wire_rx"          1 fused datagram receive (k_rx, one wave per group), lanes and LDS staging by
+ *                      pitch | 2 / 3 16-B lanes with / without the K rows staged in LDS | 4 / 5 8-B
+ *                      lanes likewise | 0 staged parse -> reconstruct -> check (3 launches)
  *   "percall_group"    1 fec_encode of a parity index computes the group's n - k rows in one request
  *                      and serves the group's other indices from a per-handle copy while src[], sz and
  *                      every input byte are unchanged | 0 one request per index
- *   "percall_fault"    (tests) 1 requests are never handed to a server, so every call takes the
- *                      timeout branch */
+ * Test hook:
+ *   "percall_fault"    1 requests are never handed to a server, so every call takes the timeout
+ *                      branch */
 int qfec_tune(const char *key, int value);
 /* The current value of a knob of qfec_tune (*value); QFEC_EINVAL for an unknown key. */
 int qfec_tune_get(const char *key, int *value);

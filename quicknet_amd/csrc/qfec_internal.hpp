@@ -64,10 +64,9 @@ struct ReconArgs {
     int surv_off, lost_off, hdr;
     int coff;                 // record word of the coefficient-table byte offsets (RecordLayout::coff)
     const uint32_t* t256;     // [256][QFEC_TAB_STRIDE] perm tables of every coefficient value (compact mode)
-    int compact;              // tuning "recon_compact": tables via t256 + the record's offsets
     int vec16;
-    int impl;                 // tuning "recon_impl": -1 auto, 0 row loop, 1 all rows at once,
-                              // 2 exact-e rows (16-B lanes), 3 exact-e rows (8-B lanes)
+    int impl;                 // tuning "recon_impl": -1 auto, exact-e rows on 2 16-B lanes, 3 8-B lanes,
+                              // 4 12-B lanes, 8 8-B lanes with one group per block
     uint32_t wpg;             // waves per group = ceil(cols / 64) (vec16 LUT kernels)
     uint32_t cols8, wpg8;     // the same at 8-B columns: ceil(B / 8), ceil(cols8 / 64)
     uint32_t cols12, wpg12;   // the same at 12-B columns (recon_impl 4)
@@ -144,21 +143,14 @@ hipError_t launch_check_payloads(const WireArgs& a, hipStream_t s);
 // runtime tuning knobs (qfec_tune); defaults are the measured best.  Atomic: qfec_tune may
 // write a knob while launches on other threads read it (each read is one atomic load)
 struct Tuning {
-    std::atomic<int> recon_impl{-1};  // -1 auto (per shape), 0 row loop, 1 all rows
-    std::atomic<int> encode_impl{-1};   // -1 auto (inputs in halves for k >= 16), 0 all rows, 1 row loop, 2 halves
+    std::atomic<int> recon_impl{-1};  // -1 auto (per shape); 2, 3, 4: exact-e rows on 16-, 8-, 12-B lanes; 8: 3 one group per block
+    std::atomic<int> encode_impl{-1};   // -1 auto (inputs in halves for k >= 16), 0 all rows, 2 halves
     std::atomic<int> wire_fused{1};     // fused datagram send where a (k, m) instance exists (0: staged)
     std::atomic<int> wire_rx{1};        // datagram receive: 1 fused k_rx, lanes and LDS staging by pitch; 2 / 3 16-B lanes
                                         // with / without LDS staging, 4 / 5 8-B lanes likewise; 0 staged (3 launches)
-    std::atomic<int> wire_store_nt{3};  // fused send datagram stores: bit 0 body, bit 1 head non-temporal
-    std::atomic<int> wire_line{1};      // fused send writes whole 64-B lines when the wire pitch allows it
-    std::atomic<int> wire_send_wave{1}; // fused send, 1088-B wire pitch: one wave per group finishes line 0 itself (k_pack_wave64)
-    std::atomic<int> wire_chunk{0};     // fused send: groups per body + head launch pair (0: as many as fit)
     std::atomic<int> host_chunk{0};     // host-buffer paths: groups per pipelined chunk (0: by bytes)
     std::atomic<int> host_threads{0};   // host copy threads for module/rs.h on host pointers (0: usable CPUs, <= 32)
-    std::atomic<int> recon_full_lines{1};  // 8-/12-B reconstruct lanes cover the 16-B columns' span (no partial 64-B lines)
-    std::atomic<int> recon_compact{1};  // LUT reconstruct reads coefficient tables via the record's offsets + t256
     std::atomic<int> host_zero_copy{1}; // pinned host batches: kernels read/write them directly (0: staged copies)
-    std::atomic<int> frame_rows{2};     // ProtocolUdp framing: rows per wave, loads issued first (2 or 4; 1: one row per wave)
 };
 Tuning& tuning();
 

@@ -134,43 +134,6 @@ __global__ void __launch_bounds__(256) k_encode_perm_halves(EncodeArgs a) {
     for (int r = 0; r < M; ++r) st16(dst + (uint64_t)r * a.pitch, acc[r]);
 }
 
-// Variant (tuning "encode_impl" = 1): one output row at a time, selectors re-formed per
-// row (pinned against LICM) -- fewer registers, more VALU.
-template <int K, int M>
-__global__ void __launch_bounds__(256) k_encode_perm_rows(EncodeArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (t >= a.work) return;
-    const uint64_t g = fast_div(t, a.cols_div);
-    const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
-    const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
-    uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
-    const uint32_t* __restrict__ tab = a.tab;
-    uint4 x[K];
-#pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = ld16(src + (uint64_t)c * a.pitch);
-    for (int r = 0; r < M; ++r) {
-        const uint32_t* tr = tab + r * K * QFEC_TAB_STRIDE;
-        uint4 acc = make_uint4(0, 0, 0, 0);
-        if (tr[5]) acc = *reinterpret_cast<const uint4*>(dst + (uint64_t)r * a.pitch);
-#pragma unroll
-        for (int c = 0; c + 1 < K; c += 2) {
-            pin16(x[c]);
-            pin16(x[c + 1]);
-            Sel sa[4], sb[4];
-            sel16(sa, x[c]);
-            sel16(sb, x[c + 1]);
-            gf_mac16x2(acc, sa, sb, tr + c * QFEC_TAB_STRIDE, tr + (c + 1) * QFEC_TAB_STRIDE);
-        }
-        if (K & 1) {
-            pin16(x[K - 1]);
-            Sel sl[4];
-            sel16(sl, x[K - 1]);
-            gf_mac16(acc, sl, tr + (K - 1) * QFEC_TAB_STRIDE);
-        }
-        st16(dst + (uint64_t)r * a.pitch, acc);
-    }
-}
-
 // runtime k, m: output rows in chunks of RCH; the k input rows are re-read per chunk
 // (L1/L2 hits).  Used for uncommon shapes and for the single-row fec_encode calls.
 constexpr int RCH = 4;
@@ -310,93 +273,9 @@ __device__ __forceinline__ int group_record(const ReconArgs& a, uint64_t g, int 
     return __builtin_amdgcn_readfirstlane(rec);
 }
 
-// One 16-B column of a group's reconstruct.  The K survivor loads are issued together;
-// the e output rows are then produced one at a time (runtime, wave-uniform loop), so only
-// one accumulator and one pair of selector sets are live: ~90 VGPRs, and no work is spent
-// on the M - e rows a group does not need.  The row's coefficient tables are scalar loads.
-template <int K, int M>
-__device__ __forceinline__ void recon_column(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                             uint64_t lost_bits, const uint32_t* __restrict__ tab, int e,
-                                             uint64_t pitch, uint64_t off) {
-    uint4 x[K];
-#pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = ld16(src[c] + off);
-    for (int j = 0; j < e; ++j) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(lost_bits);
-        lost_bits &= lost_bits - 1;
-        uint8_t* dst = data_g + (uint64_t)l * pitch + off;
-        const uint32_t* tj = tab + j * K * QFEC_TAB_STRIDE;
-        uint4 acc = make_uint4(0, 0, 0, 0);
-        if (tj[5]) acc = *reinterpret_cast<const uint4*>(dst);  // rs.c column-0 quirk
-#pragma unroll
-        for (int c = 0; c + 1 < K; c += 2) {
-            // opaque to LICM: re-form the selectors per row instead of keeping all K
-            // inputs' selector words (3x the input registers) live across the row loop
-            pin16(x[c]);
-            pin16(x[c + 1]);
-            Sel sa[4], sb[4];
-            sel16(sa, x[c]);
-            sel16(sb, x[c + 1]);
-            gf_mac16x2(acc, sa, sb, tj + c * QFEC_TAB_STRIDE, tj + (c + 1) * QFEC_TAB_STRIDE);
-        }
-        if (K & 1) {
-            pin16(x[K - 1]);
-            Sel sl[4];
-            sel16(sl, x[K - 1]);
-            gf_mac16(acc, sl, tj + (K - 1) * QFEC_TAB_STRIDE);
-        }
-        st16(dst, acc);
-    }
-}
-
-// Variant (tuning "recon_impl" = 1): all M rows computed at once, selectors formed once
-// per input and shared by the rows; more registers (2-3 waves/SIMD), fewer VALU ops.
-template <int K, int M>
-__device__ __forceinline__ void recon_column_allrows(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                                     uint64_t lost_bits, const uint32_t* __restrict__ tab, int e,
-                                                     uint64_t pitch, uint64_t off) {
-    uint4 x[K];
-#pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = ld16(src[c] + off);
-    uint8_t* dst[M];
-    uint4 acc[M];
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-        uint32_t l = 0;
-        if (j < e) {
-            l = (uint32_t)__builtin_ctzll(lost_bits);
-            lost_bits &= lost_bits - 1;
-        }
-        dst[j] = data_g + (uint64_t)l * pitch + off;
-        acc[j] = make_uint4(0, 0, 0, 0);
-        if (j < e && tab[(j * K) * QFEC_TAB_STRIDE + 5]) acc[j] = *reinterpret_cast<const uint4*>(dst[j]);
-    }
-#pragma unroll
-    for (int c = 0; c + 1 < K; c += 2) {
-        Sel sa[4], sb[4];
-        sel16(sa, x[c]);
-        sel16(sb, x[c + 1]);
-#pragma unroll
-        for (int j = 0; j < M; ++j)
-            gf_mac16x2(acc[j], sa, sb, tab + (j * K + c) * QFEC_TAB_STRIDE, tab + (j * K + c + 1) * QFEC_TAB_STRIDE);
-    }
-    if (K & 1) {
-        Sel sl[4];
-        sel16(sl, x[K - 1]);
-#pragma unroll
-        for (int j = 0; j < M; ++j) gf_mac16(acc[j], sl, tab + (j * K + K - 1) * QFEC_TAB_STRIDE);
-    }
-    // materialise every row here: left alone, the compiler sinks each row's MAC into its
-    // `j < e` store branch, which keeps all K inputs' selector words live across the rows
-#pragma unroll
-    for (int j = 0; j < M; ++j) pin16(acc[j]);
-#pragma unroll
-    for (int j = 0; j < M; ++j)
-        if (j < e) st16(dst[j], acc[j]);
-}
-
-// Exactly E rows (E = the group's erased-data count, wave-uniform): the ALLROWS schedule
-// without the M - E rows a group does not need.  3 random erasures of 13 give e = 1, 2, 3
+// Exactly E rows (E = the group's erased-data count, wave-uniform): all E rows at once,
+// selectors formed once per input and shared by the rows, no work on the M - E rows a group
+// does not need.  3 random erasures of 13 give e = 1, 2, 3
 // with probability 0.10, 0.47, 0.42, so RS(10,3) does 77 % of the all-rows VALU work.
 // D = dwords per lane (4: 16-B columns, 2: 8-B columns for rows whose 16-B column count
 // leaves a wave mostly idle, e.g. B = 1400: 88 16-B columns on 2 waves, 175 8-B on 3).
@@ -437,31 +316,14 @@ __device__ __forceinline__ void ldv_plain(uint32_t (&v)[D], const uint8_t* p) {
     for (int d = 0; d < D; ++d) v[d] = reinterpret_cast<const uint32_t*>(p)[d];
 }
 
-// where a decode record's coefficient tables are: in the record itself (the tables follow
-// its header), or -- compact -- in the 256-entry table of every coefficient value, at the
-// byte offsets the record's header lists (RecordLayout::coff).  The compact form reads only
-// the record's header, so the records of all patterns stay cache-resident (RS(16,4): 4 844
-// records of 2.4 KB would not fit the 4 MB L2; their headers do).
-// The tables are read through the constant address space: loads from it are scalar (SMEM)
-// whatever stores the kernel makes, also inside a loop over items (recon_impl 9), where the
-// clobber analysis would turn global-address loads into per-lane vector loads.
+// where a decode record's coefficient tables are: in the 256-entry table of every coefficient
+// value, at the byte offsets the record's header lists (RecordLayout::coff).  Reading only the
+// record's header keeps the records of all patterns cache-resident (RS(16,4): 4 844 records of
+// 2.4 KB would not fit the 4 MB L2; their headers do).  The tables are read through the
+// constant address space: loads from it are scalar (SMEM) whatever stores the kernel makes.
 typedef const __attribute__((address_space(4))) uint32_t* cptr32;
 typedef const __attribute__((address_space(4))) uint8_t* cptr8;
-template <int CT>
-struct RTab;
-template <>
-struct RTab<0> {
-    cptr32 tab;
-    __device__ RTab(const uint32_t* t) : tab((cptr32)t) {}
-    __device__ __forceinline__ cptr32 at(int j, int c, int K) const { return tab + (j * K + c) * QFEC_TAB_STRIDE; }
-    __device__ __forceinline__ bool quirk(int j, int K) const { return tab[(j * K) * QFEC_TAB_STRIDE + 5] != 0; }
-    __device__ __forceinline__ void load5(int j, int c, int K, uint32_t (&t5)[5]) const {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) t5[i] = at(j, c, K)[i];
-    }
-};
-template <>
-struct RTab<1> {
+struct RTab {
     cptr32 rec;  // the record: [1] quirk flags, [coff + j*K + c] table byte offsets
     cptr32 offs;
     cptr32 t256;
@@ -476,9 +338,9 @@ struct RTab<1> {
         for (int i = 0; i < 5; ++i) t5[i] = at(j, c, K)[i];
     }
 };
-template <int K, int E, int D, class TT>
+template <int K, int E, int D>
 __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                               uint64_t lost_bits, const TT& T, uint64_t pitch, uint64_t off) {
+                                               uint64_t lost_bits, const RTab& T, uint64_t pitch, uint64_t off) {
     uint32_t x[K][D];
 #pragma unroll
     for (int c = 0; c < K; ++c) ldv<D>(x[c], src[c] + off);
@@ -525,12 +387,12 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
 }
 
 // wave-uniform dispatch on e to the exact-row-count body
-template <int K, int M, int D, class TT, int E = M>
+template <int K, int M, int D, int E = M>
 __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                                  uint64_t lost_bits, const TT& T, int e, uint64_t pitch, uint64_t off) {
+                                                  uint64_t lost_bits, const RTab& T, int e, uint64_t pitch, uint64_t off) {
     if constexpr (E > 1) {
         if (e < E) {
-            recon_column_by_e<K, M, D, TT, E - 1>(src, data_g, lost_bits, T, e, pitch, off);
+            recon_column_by_e<K, M, D, E - 1>(src, data_g, lost_bits, T, e, pitch, off);
             return;
         }
     }
@@ -541,18 +403,18 @@ __device__ __forceinline__ void recon_column_by_e(const uint8_t* const (&src)[K]
 // it is the lowest K non-erased shard ids (all surviving data, then the first e surviving
 // parity rows: module/rs.c:620-629) -- so the shard loads issue right after the ballot,
 // while the decode record (coefficients only) is still in flight.
-// One wave per 64 16-B columns of a group: a group of `cols` columns gets
-// wpg = ceil(cols / 64) waves (B = 1400 -> 2), all in flight together, no column loop.
-// IMPL 6: IMPL 3 compiled for 8 waves per SIMD (register caps; 7 otherwise: 106 SGPRs)
-// IMPL 8: IMPL 3 launched with one group per block (blocks of wpg8 waves), so a group's slab
-// waves share a CU and its scalar data (marks, LUT entry, record header, tables)
-template <int K, int M, int IMPL, int CT>
+// One wave per 64 columns of a group: a group of `cols` columns gets wpg = ceil(cols / 64)
+// waves, all in flight together, no column loop.  IMPL: 2 exact-e rows on 16-B lanes, 3 on
+// 8-B lanes, 4 on 12-B lanes; 8 = 3 launched with one group per block (blocks of wpg8 waves),
+// so a group's slab waves share a CU and its scalar data (marks, LUT entry, record header,
+// tables)
+template <int K, int M, int IMPL>
 __device__ __forceinline__ void recon_item(const ReconArgs& a, uint8_t* __restrict__ data,
                                            const uint8_t* __restrict__ parity, const uint8_t* __restrict__ marks,
                                            const int32_t* __restrict__ lut, const uint32_t* __restrict__ records,
                                            uint32_t wid, int lane) {
     constexpr int N = K + M;
-    const uint32_t wpg = IMPL == 5 ? 1u : IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
+    const uint32_t wpg = IMPL == 3 ? a.wpg8 : IMPL == 4 ? a.wpg12 : a.wpg;
     const uint64_t g = wid / wpg;
     const uint32_t part = wid - (uint32_t)g * wpg;
     if (g >= a.groups) return;
@@ -569,9 +431,7 @@ __device__ __forceinline__ void recon_item(const ReconArgs& a, uint8_t* __restri
         return;
     }
     const int rec = ((const __attribute__((address_space(4))) int32_t*)lut)[mask];
-    const uint32_t* tab = records + rec + a.hdr;
-    const RTab<0> TD{tab};
-    const RTab<1> TC{records + rec, a.coff, a.t256};
+    const RTab T{records + rec, a.coff, a.t256};
     const uint64_t pitch = a.pitch;
     uint8_t* data_g = data + g * a.dgs;
     const uint8_t* par_g = parity + g * a.pgs;
@@ -582,40 +442,26 @@ __device__ __forceinline__ void recon_item(const ReconArgs& a, uint8_t* __restri
         avail &= avail - 1;
         src[c] = s < (uint32_t)K ? data_g + (uint64_t)s * pitch : par_g + (uint64_t)(s - K) * pitch;
     }
-    if constexpr (IMPL == 5) {  // one wave per group: the scalar setup above once, then the 8-B slabs
-        for (uint32_t col = lane; col < a.cols8; col += 64u) {
-            if constexpr (CT != 0) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 8u);
-            else recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 8u);
-        }
-        return;
-    }
     const uint32_t col = part * 64u + lane;
     if (col < (IMPL == 3 ? a.cols8 : IMPL == 4 ? a.cols12 : a.cols)) {
-        if constexpr (CT != 0) {
-            if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 16u);
-            else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 8u);
-            else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, TC, e, pitch, (uint64_t)col * 12u);
-        } else if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 16u);
-        else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 8u);
-        else if (IMPL == 4) recon_column_by_e<K, M, 3>(src, data_g, lost_bits, TD, e, pitch, (uint64_t)col * 12u);
-        else if (IMPL == 1) recon_column_allrows<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
-        else recon_column<K, M>(src, data_g, lost_bits, tab, e, pitch, (uint64_t)col * 16u);
+        if (IMPL == 2) recon_column_by_e<K, M, 4>(src, data_g, lost_bits, T, e, pitch, (uint64_t)col * 16u);
+        else if (IMPL == 3) recon_column_by_e<K, M, 2>(src, data_g, lost_bits, T, e, pitch, (uint64_t)col * 8u);
+        else recon_column_by_e<K, M, 3>(src, data_g, lost_bits, T, e, pitch, (uint64_t)col * 12u);
     }
 }
 
-template <int K, int M, int IMPL_, int CT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMPL_ == 6 ? 8 : 1)))
-k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
+template <int K, int M, int IMPL_>
+__global__ void __launch_bounds__(256) k_reconstruct_perm(ReconArgs a, uint8_t* __restrict__ data,
                                                           const uint8_t* __restrict__ parity,
                                                           const uint8_t* __restrict__ marks,
                                                           const int32_t* __restrict__ lut,
                                                           const uint32_t* __restrict__ records) {
     // __restrict__ parameters: the LUT and records are provably not written by this
     // launch, so their loads stay scalar (SGPR) even across the row loop's stores.
-    constexpr int IMPL = (IMPL_ == 6 || IMPL_ == 8) ? 3 : IMPL_;
+    constexpr int IMPL = IMPL_ == 8 ? 3 : IMPL_;
     const int lane = threadIdx.x & 63;
     const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * (IMPL_ == 8 ? a.wpg8 : 4u) + (threadIdx.x >> 6));
-    recon_item<K, M, IMPL, CT>(a, data, parity, marks, lut, records, wid, lane);
+    recon_item<K, M, IMPL>(a, data, parity, marks, lut, records, wid, lane);
 }
 
 // runtime k, e; any vector width via the byte path when the layout is not 16-B aligned
@@ -736,9 +582,7 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
 #define QFEC_ENC_CASE(KK, MM)                                                                 \
     if (a.k == KK && a.m == MM) {                                                             \
         const int im = a.impl < 0 ? (KK >= 16 ? 2 : 0) : a.impl;                              \
-        if (im == 1)                                                                          \
-            hipLaunchKernelGGL((k_encode_perm_rows<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
-        else if (im == 2)                                                                     \
+        if (im == 2)                                                                          \
             hipLaunchKernelGGL((k_encode_perm_halves<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
         else                                                                                  \
             hipLaunchKernelGGL((k_encode_perm<KK, MM>), dim3(grid), dim3(256), 0, stream, a);  \
@@ -779,35 +623,27 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream) {
 #define QFEC_REC_LAUNCH(KK, MM, AR)                                                                        \
     do {                                                                                                   \
         const dim3 blk(AR == 8 ? 64u * a.wpg8 : 256u), grd(AR == 8 ? (unsigned)a.groups : pgrid);          \
-        if (AR >= 2 && a.compact && a.t256)                                                                \
-            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, (AR >= 2) * 1>), grd, blk, 0, stream, a,   \
-                               a.data, a.parity, a.marks, a.lut, a.records);                               \
-        else                                                                                               \
-            hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR, 0>), grd, blk, 0, stream, a,               \
-                               a.data, a.parity, a.marks, a.lut, a.records);                               \
+        hipLaunchKernelGGL((k_reconstruct_perm<KK, MM, AR>), grd, blk, 0, stream, a, a.data, a.parity, a.marks, \
+                           a.lut, a.records);                                                              \
     } while (0)
 
 #define QFEC_REC_CASE(KK, MM)                                                      \
     if (a.k == KK && a.m == MM) {                                                  \
-        /* auto: exact-e rows up to k*m = 64 (8-B or 12-B lanes when they fill   */ \
-        /* the waves better, e.g. B = 1400, 8-B for k >= 10), else the row loop    */ \
+        /* auto: exact-e rows on 12-B lanes for k*m <= 30 where they fill the waves */ \
+        /* best, on 8-B lanes where those fill better than 16-B lanes or for k >= 10 */ \
+        /* (one group per block where a group is at most 4 waves), else 16-B lanes   */ \
         const bool wide8 = KK >= 10 && fill8 >= fill16 - 0.01;                     \
-        int im = a.impl < 0 ? (KK * MM <= 64 ? (KK * MM <= 30 && lanes12 ? 4 : (lanes8 || wide8) ? 3 : 2) : 0) \
-                            : a.impl;                                              \
+        int im = a.impl < 0 ? (KK * MM <= 30 && lanes12 ? 4 : (lanes8 || wide8) ? 3 : 2) : a.impl; \
         if (im == 4 && !lanes12_ok) im = 2;                                        \
-        const unsigned pgrid = im == 5 ? grid : (im == 3 || im == 6) ? pgrid8 : im == 4 ? pgrid12 : pgrid16; \
+        const unsigned pgrid = im == 3 ? pgrid8 : im == 4 ? pgrid12 : pgrid16;     \
         /* 8-B lanes run one group per block where a group is at most 4 waves: its slab */ \
         /* waves share a CU (RS(16,4) B=1400: 1 218 against 1 224 us, r03blk)            */ \
         if (im == 3 && a.impl < 0) im = 8;                                         \
         if (im == 8 && (a.wpg8 < 1 || a.wpg8 > 4)) im = 3;                         \
         if (im == 8) QFEC_REC_LAUNCH(KK, MM, 8);                                   \
-        else if (im == 6) QFEC_REC_LAUNCH(KK, MM, 6);                              \
-        else if (im == 5) QFEC_REC_LAUNCH(KK, MM, 5);                              \
         else if (im == 4) QFEC_REC_LAUNCH(KK, MM, 4);                              \
         else if (im == 3) QFEC_REC_LAUNCH(KK, MM, 3);                              \
-        else if (im == 2) QFEC_REC_LAUNCH(KK, MM, 2);                              \
-        else if (im == 1) QFEC_REC_LAUNCH(KK, MM, 1);                              \
-        else QFEC_REC_LAUNCH(KK, MM, 0);                                           \
+        else QFEC_REC_LAUNCH(KK, MM, 2);                                           \
         return hipGetLastError();                                                  \
     }
 

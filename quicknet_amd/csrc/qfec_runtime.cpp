@@ -70,7 +70,6 @@ int hip_fail(hipError_t e, const char* what) {
 
 std::atomic<int> g_variant{QFEC_VARIANT_PERM};
 std::atomic<int> g_percall_fast{1};  // qfec_tune "percall_fast": fec_encode / fec_decode via k_percall
-std::atomic<int> g_percall_spin{1};  // qfec_tune "percall_spin": wait on k_percall's completion word
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -106,9 +105,6 @@ struct DevCtx {
         hipStream_t stream = nullptr;
         PcBell* bell = nullptr;      // fine-grained device memory the CPU stores into
         uint8_t* in = nullptr;       // ditto: kPcMaxCoef rows of kPcMaxChunks * 16 bytes
-        uint8_t* h_in = nullptr;     // the same in write-combined pinned host memory ("percall_in" 1)
-        uint8_t* d_in = nullptr;     //   and its device address
-        int in_mode = 0;             // where the running server reads its inputs: 0 device, 1 host
         uint8_t* h_out = nullptr;    // coherent pinned host memory, same shape
         uint8_t* d_out = nullptr;
         PcStatus* h_st = nullptr;    // coherent pinned host memory
@@ -225,7 +221,6 @@ int ensure_pc(DevCtx& c, size_t bytes) {
 
 // ---- the resident per-call server (qfec_percall.hpp)
 std::atomic<int> g_percall_resident{1};  // qfec_tune "percall_resident"
-std::atomic<int> g_percall_in{0};        // qfec_tune "percall_in": server inputs 0 in device memory, 1 in host memory
 std::atomic<int> g_percall_idle_us{(int)kPcIdleUsDefault};  // qfec_tune "percall_idle_us": the block's idle exit
 std::atomic<int> g_percall_timeout_us{2000000};  // qfec_tune "percall_timeout_us": give up spinning, wait instead
 std::atomic<int> g_percall_fault{0};     // qfec_tune "percall_fault" (tests): 1 = requests are never handed to a server
@@ -265,12 +260,11 @@ int pc_server_setup(DevCtx& c) {
         if (s.stream) (void)hipStreamDestroy(s.stream);
         if (s.bell) (void)hipFree(s.bell);
         if (s.in) (void)hipFree(s.in);
-        if (s.h_in) (void)hipHostFree(s.h_in);
         if (s.h_out) (void)hipHostFree(s.h_out);
         if (s.h_st) (void)hipHostFree(s.h_st);
         s.stream = nullptr;
         s.bell = nullptr;
-        s.in = s.h_in = s.d_in = s.h_out = s.d_out = nullptr;
+        s.in = s.h_out = s.d_out = nullptr;
         s.h_st = s.d_st = nullptr;
         (void)hipGetLastError();
     };
@@ -287,10 +281,6 @@ int pc_server_setup(DevCtx& c) {
         return fail(e, "bell");
     if ((e = hipExtMallocWithFlags((void**)&s.in, kPcSrvBytes, hipDeviceMallocFinegrained)) != hipSuccess)
         return fail(e, "input rows");
-    if ((e = hipHostMalloc((void**)&s.h_in, kPcSrvBytes, hipHostMallocMapped | hipHostMallocWriteCombined)) !=
-            hipSuccess ||
-        (e = hipHostGetDevicePointer((void**)&s.d_in, s.h_in, 0)) != hipSuccess)
-        return fail(e, "host input rows");
     if ((e = hipHostMalloc((void**)&s.h_out, kPcSrvBytes, hipHostMallocMapped | hipHostMallocCoherent)) !=
             hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&s.d_out, s.h_out, 0)) != hipSuccess)
@@ -352,12 +342,8 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
                    unsigned char* const* out, int sz, size_t pitch, Overlap* ov = nullptr) {
     DevCtx::PcServer& s = c.srv;
     PcBell* b = s.bell;
-    const int mode = g_percall_in.load();
-    if (mode != s.in_mode) {  // the running server reads the other buffer: restart it
-        (void)pc_server_stop(c);
-        s.in_mode = mode;
-    }
-    uint8_t* rows = mode ? s.h_in : s.in;
+    uint8_t* rows = s.in;  // fine-grained device memory the CPU stores into (reading the rows from
+                           // write-combined host memory instead cost 0.9 us more per call, r03)
     for (int r = 0; r < k; ++r) memcpy(rows + (size_t)r * pitch, in[r], (size_t)sz);
     // the tables go out only when they differ from the last call's (fec_encode of one parity
     // index, or a repeated loss pattern, sends none)
@@ -388,7 +374,7 @@ int pc_server_call(DevCtx& c, const std::vector<uint32_t>& tab, int k, int e, un
         static const uint32_t trace = getenv("QFEC_PERCALL_TRACE") && atoi(getenv("QFEC_PERCALL_TRACE")) ? 1u : 0u;
         const uint64_t idle = (uint64_t)std::max(0, g_percall_idle_us.load()) * 100u;  // 100 MHz wall clock
         const uint32_t flags = trace;  // bit 0: QFEC_PERCALL_TRACE (qfec_percall.hip)
-        return launch_percall_server(b, s.in_mode ? s.d_in : s.in, s.d_out, s.d_st, prev, s.gen, flags, idle,
+        return launch_percall_server(b, s.in, s.d_out, s.d_st, prev, s.gen, flags, idle,
                                      s.stream);
     };
     hipError_t he = hipSuccess;
@@ -776,7 +762,6 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.hdr = L.hdr;
     a.coff = L.coff;
     a.t256 = ctx.d_t256;
-    a.compact = tuning().recon_compact;
     a.dgs = dgs >= 0 ? (uint64_t)dgs : (uint64_t)c->k * pitch;
     a.pgs = pgs >= 0 ? (uint64_t)pgs : (uint64_t)c->m * pitch;
     a.vec16 = vec16_ok(d_data, d_par, block, pitch) && !((a.dgs | a.pgs) & 15) ? 1 : 0;
@@ -785,9 +770,7 @@ int run_reconstruct(DevCtx& ctx, const qfec_code* c, const int32_t* lut, const i
     a.wpg = (a.cols + 63) / 64;
     a.cols8 = (uint32_t)((block + 7) / 8);
     a.cols12 = (uint32_t)((block + 11) / 12);
-    // recon_full_lines 1 (auto): for k < 14; 2: always; 0: never
-    const int fl = tuning().recon_full_lines;
-    if (a.vec16 && (fl == 2 || (fl == 1 && c->k < 14))) {
+    if (a.vec16 && c->k < 14) {
         // cover the 16-B columns' span, which the 16-B body writes anyway (it stays inside
         // the pitch): a row that ends part-way into a 64-B line costs a partial-line write
         // (B = 1400: 175 -> 176 8-B columns, rows end on 1408 = 22 lines).  It also reads the
@@ -945,19 +928,10 @@ const std::vector<Knob>& knob_table() {
         {"host_chunk", &tuning().host_chunk, 0, 0x7FFFFFFF},
         {"host_threads", &tuning().host_threads, 0, 64},
         {"encode_impl", &tuning().encode_impl, -1, 2},
-        {"wire_store_nt", &tuning().wire_store_nt, 0, 3},
-        {"wire_chunk", &tuning().wire_chunk, 0, 0x7FFFFFFF},
-        {"wire_send_wave", &tuning().wire_send_wave, 0, 4},
-        {"wire_line", &tuning().wire_line, 0, 1},
         {"wire_fused", &tuning().wire_fused, 0, 1},
         {"wire_rx", &tuning().wire_rx, 0, 5},
         {"host_zero_copy", &tuning().host_zero_copy, 0, 1},
-        {"recon_compact", &tuning().recon_compact, 0, 2},
-        {"recon_full_lines", &tuning().recon_full_lines, 0, 2},
-        {"frame_rows", &tuning().frame_rows, 1, 4},
         {"percall_fast", &g_percall_fast, 0, 1},
-        {"percall_spin", &g_percall_spin, 0, 1},
-        {"percall_in", &g_percall_in, 0, 1},
         {"percall_group", &g_percall_group, 0, 1},
         {"percall_fault", &g_percall_fault, 0, 1},
         {"percall_timeout_us", &g_percall_timeout_us, 0, 0x7FFFFFFF},
@@ -989,6 +963,8 @@ int qfec_tune(const char* key, int value) {
     for (const Knob& kn : knob_table()) {
         if (strcmp(key, kn.key)) continue;
         if (value < kn.lo || value > kn.hi) break;
+        if (!strcmp(key, "recon_impl") && value != -1 && value != 2 && value != 3 && value != 4 && value != 8) break;
+        if (!strcmp(key, "encode_impl") && value == 1) break;
         kn.v->store(value);
         if (!strcmp(key, "percall_idle_us") || (!strcmp(key, "percall_resident") && !value)) stop_percall_servers();
         return QFEC_OK;
@@ -1749,7 +1725,7 @@ int qfec_pack_datagrams(qfec_code* code, const unsigned char* d_payload, const l
     a.k = k;
     a.m = m;
     a.checksum = checksum;
-    a.store_nt = tuning().wire_store_nt;
+    a.store_nt = 3;  // non-temporal datagram stores, body and head
     if (tuning().wire_fused) {
         bool launched = false;
         // the fused path never materialises shards; their buffer holds its partial sums
@@ -1859,7 +1835,7 @@ int qfec_pack_frames(qfec_code* code, const unsigned char* d_payload, const long
         a.k = k;
         a.m = m;
         a.checksum = checksum;
-        a.store_nt = tuning().wire_store_nt;
+        a.store_nt = 3;  // non-temporal datagram stores, body and head
         FrameSend fs{d_mask, d_conv_hid, (uint32_t)gmask & 0xFFu, (uint32_t)cmd, (uint32_t)protocol};
         bool launched = false;
         const hipError_t e = launch_pack_frames(a, fs, fp, tab, s, &launched);
@@ -2652,7 +2628,7 @@ int apply_rows(const std::vector<uint32_t>& tab, int k, int e, unsigned char* co
         for (int i = 0; i < k * e; ++i) memcpy(&a.tab[i * 5], &tab[(size_t)i * QFEC_TAB_STRIDE], 5 * sizeof(uint32_t));
         // one block: wait on the kernel's completion word (its outputs are visible in host
         // memory once it is stored), not on the runtime's completion signal
-        const bool spin = a.chunks <= 256 && g_percall_spin.load();
+        const bool spin = a.chunks <= 256;
         a.done = spin ? ctx->d_pc_done : nullptr;
         a.seq = spin ? ++ctx->pc_seq : 0;
         if (spin && a.seq == 0) a.seq = ++ctx->pc_seq;  // 0 is the word's initial value

@@ -1397,17 +1397,11 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s) {
 // 2 only: at 1472 B, RS(10,13) x 100k 1400-B payloads, it ran 841 us against 782 for the body +
 // line-0 pair -- the second pass keeps 24 of 64 lanes busy; profiles/r03_wire/r03n_mtu_ab.txt); 0 none
 static int send_wave_gpw(uint64_t wire_pitch) {
-    const int sw = tuning().wire_send_wave;
-    if (!sw) return 0;
-    if (sw == 4 && wire_pitch > 1088 && wire_pitch <= 1600) return 11;  // A/B: 8-B lanes at 5 waves/SIMD
-    if (sw == 3 && wire_pitch > 576 && wire_pitch <= 1600)  // 8-B lanes: 2 passes to 1088 B, 3 to 1600
-        return wire_pitch <= 1088 ? 9 : 10;
-    // the default above 1088 B: 8-B lanes in three passes (1472 B, RS(10,13) x 100k: 737 against
-    // 781 us for the body + line-0 pair; at 1088 B the 16-B lanes stay: 497 against 545 us)
+    // above 1088 B: 8-B lanes in three passes (1472 B, RS(10,13) x 100k: 737 against 781 us for
+    // the body + line-0 pair); at 1088 B 16-B lanes, one pass (497 against 545 us on 8-B lanes)
     if (wire_pitch > 1088 && wire_pitch <= 1600) return 10;
     if (wire_pitch == 576) return 2;
-    if (wire_pitch == 1088 || (sw == 2 && wire_pitch > 576 && wire_pitch < 1088)) return 1;
-    if (sw == 2 && wire_pitch > 1088 && wire_pitch <= 2112) return 5;
+    if (wire_pitch == 1088) return 1;
     return 0;
 }
 
@@ -1419,7 +1413,7 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
     // pitch): chunks [TS, wire_pitch / 16), so lanes per group is a multiple of 4 and every
     // 64-B line of a row is one store instruction (a line written in two parts costs the
     // memory a read-modify-write: tools/wrskel.hip, profiles/r02zn_wrskel.txt)
-    const bool line = tuning().wire_line && a.wire_pitch % 64 == 0 &&
+    const bool line = a.wire_pitch % 64 == 0 &&
                       a.wire_pitch == (HDR + a.pitch + 63) / 64 * 64 && a.wire_pitch / 16 >= (HDR == 13 ? 20u : 16u);
     // one wave per group (k_pack_wave64): the body's chunks 4.. are 64 lanes at a 1088-B wire
     // pitch (one pass), 32 at 576 B (two groups per wave), up to 128 in two passes above 1088 B
@@ -1435,17 +1429,8 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
             if (gpw == 1)
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 1>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
                                    a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
-            else if (gpw == 5)
-                hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
-                                   a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
-            else if (gpw == 9)
-                hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 2, 8>), grid, dim3(256), 0, s, b, a.payload,
-                                   a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
             else if (gpw == 10)
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 3, 8>), grid, dim3(256), 0, s, b, a.payload,
-                                   a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
-            else if (gpw == 11)
-                hipLaunchKernelGGL((k_pack_wave64<K, M, 1, 0, 3, 8, 5>), grid, dim3(256), 0, s, b, a.payload,
                                    a.offsets + g0 * K, a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, FrameSend{});
             else
                 hipLaunchKernelGGL((k_pack_wave64<K, M, 2>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K,
@@ -1457,10 +1442,8 @@ hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* pa
     const uint32_t tn = line ? (uint32_t)(a.wire_pitch / 16) : (uint32_t)((HDR + a.pitch + 15) / 16);
     const uint32_t lpg = std::max(16u, tn - TS);
     const DivMagic lpg_div = make_div_magic(lpg);
-    // groups per body + head launch pair (keeps g0 * lpg % 16 == 0); tuning "wire_chunk"
-    // bounds it so that a head launch rewrites lines its body launch wrote only just before
+    // groups per body + head launch pair (keeps g0 * lpg % 16 == 0)
     uint64_t per = (((uint64_t)1 << 30) / lpg) & ~(uint64_t)15;
-    if (tuning().wire_chunk > 0) per = std::min(per, (uint64_t)tuning().wire_chunk & ~(uint64_t)15);
     per = std::max(per, (uint64_t)16);
     for (uint64_t g0 = 0; g0 < a.groups; g0 += per) {
         const uint64_t gn = std::min(per, a.groups - g0);
@@ -1518,7 +1501,7 @@ hipError_t pack_frames_shape(const WireArgs& a, const FrameSend& fs, int fp, con
     // frames above 1088 B take the two-pass wave whenever the one-wave send is on: the other way
     // is two calls (datagrams, then frames), 1 577 against 851 us at 1472 B (r03n)
     int gpw = send_wave_gpw(fpitch);
-    if (!gpw && tuning().wire_send_wave && fpitch > 1088 && fpitch <= 2112) gpw = 5;
+    if (!gpw && fpitch > 1088 && fpitch <= 2112) gpw = 5;
     if (!a.checksum || !gpw || fpitch != (fp + 13 + a.pitch + 63) / 64 * 64) return hipSuccess;
     *launched = true;
     for (uint64_t g0 = 0; g0 < a.groups; g0 += ((uint64_t)1 << 28)) {
@@ -1536,10 +1519,7 @@ hipError_t pack_frames_shape(const WireArgs& a, const FrameSend& fs, int fp, con
 #define QFEC_PF8(FP, NP)                                                                                          \
     hipLaunchKernelGGL((k_pack_wave64<K, M, 1, FP, NP, 8>), grid, dim3(256), 0, s, b, a.payload, a.offsets + g0 * K, \
                        a.sizes + g0 * K, a.seq + 2 * g0, tab, gn, f)
-        if (gpw == 11) gpw = 10;  // (the 5-wave A/B build is for datagrams only)
-        if (gpw == 9 && fp == 4) QFEC_PF8(4, 2);
-        else if (gpw == 9) QFEC_PF8(12, 2);
-        else if (gpw == 10 && fp == 4) QFEC_PF8(4, 3);
+        if (gpw == 10 && fp == 4) QFEC_PF8(4, 3);
         else if (gpw == 10) QFEC_PF8(12, 3);
         else if (gpw == 1 && fp == 4) QFEC_PF(1, 4, 1);
         else if (gpw == 1) QFEC_PF(1, 12, 1);
@@ -1631,17 +1611,13 @@ hipError_t launch_len_by_status(int32_t* len, const int32_t* status, uint64_t ro
 
 hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s) {
     if (!a.rows) return hipSuccess;
-    const int fr = tuning().frame_rows;
-    if (fr > 1 && a.in_pitch <= 2048 && a.out_pitch <= 2048) {
-        // 2 (the default): two rows per wave built in LDS and stored flat; 3: the same two rows
-        // stored directly (A/B; 701 against 671 us on the bench's 1.3 M datagrams)
-        if (fr == 2 && a.out_pitch % 16 == 0)
-            hipLaunchKernelGGL((k_frame_udp_rows<2, true>), dim3(waves_grid((a.rows + 1) / 2)), dim3(256),
-                               4 * 2 * a.out_pitch, s, a);
-        else if (fr == 2 || fr == 3)
-            hipLaunchKernelGGL(k_frame_udp_rows<2>, dim3(waves_grid((a.rows + 1) / 2)), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_frame_udp_rows<4>, dim3(waves_grid((a.rows + 3) / 4)), dim3(256), 0, s, a);
+    if (a.in_pitch <= 2048 && a.out_pitch <= 2048) {
+        // two rows per wave, their loads issued first; frames built in LDS and stored flat where
+        // the output pitch allows it (701 against 671 us stored directly, on the bench's 1.3 M
+        // datagrams); one row per wave and four rows per wave measured slower
+        // (the ABI's pitches are multiples of 16)
+        hipLaunchKernelGGL((k_frame_udp_rows<2, true>), dim3(waves_grid((a.rows + 1) / 2)), dim3(256),
+                           4 * 2 * a.out_pitch, s, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_frame_udp, dim3(waves_grid(a.rows)), dim3(256), 0, s, a);
@@ -1650,12 +1626,8 @@ hipError_t launch_frame_udp(const FrameArgs& a, hipStream_t s) {
 
 hipError_t launch_unframe_udp(const FrameArgs& a, hipStream_t s) {
     if (!a.rows) return hipSuccess;
-    const int fr = tuning().frame_rows;
-    if (fr > 1 && a.in_pitch <= 2048 && a.out_pitch <= 2048) {
-        if (fr == 2 || fr == 3)
-            hipLaunchKernelGGL(k_unframe_udp_rows<2>, dim3(waves_grid((a.rows + 1) / 2)), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_unframe_udp_rows<4>, dim3(waves_grid((a.rows + 3) / 4)), dim3(256), 0, s, a);
+    if (a.in_pitch <= 2048 && a.out_pitch <= 2048) {
+        hipLaunchKernelGGL(k_unframe_udp_rows<2>, dim3(waves_grid((a.rows + 1) / 2)), dim3(256), 0, s, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_unframe_udp, dim3(waves_grid(a.rows)), dim3(256), 0, s, a);

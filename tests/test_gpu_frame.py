@@ -23,12 +23,10 @@ def dev(a):
 @pytest.mark.parametrize("session", [False, True])
 @pytest.mark.parametrize("pitch", [64, 1056, 1088, 2080])
 @pytest.mark.parametrize("op64", [False, True])
-@pytest.mark.parametrize("rows_per_wave", [1, 2, 3, 4])
-def test_frame_vs_oracle(oracle, session, pitch, op64, rows_per_wave):
-    """With the default 16-B output pitch and a 64-B multiple one; one, two (staged in LDS:
-    frame_rows 2, the default; stored directly: 3) or four rows per wave (rows longer than
-    2 KiB always take one row per wave).  301 rows: the
-    last wave is partly empty."""
+def test_frame_vs_oracle(oracle, session, pitch, op64):
+    """With the default 16-B output pitch and a 64-B multiple one; two rows per wave, built in
+    LDS and stored flat, up to 2 KiB rows, one row per wave above (2080).  301 rows: the last
+    wave is partly empty."""
     rng = np.random.default_rng(pitch + session)
     R = 301
     lens = rng.integers(0, pitch + 1, size=R).astype(np.int32)
@@ -38,14 +36,10 @@ def test_frame_vs_oracle(oracle, session, pitch, op64, rows_per_wave):
     ch = rng.integers(0, 2**32, size=(R, 2), dtype=np.uint64).astype(np.uint32) if session else None
     gmask = 0x3C
     P = 12 if session else 4
-    qa.tune("frame_rows", rows_per_wave)
-    try:
-        out, out_len = qa.frame_udp(dev(rows), dev(lens), dev(masks), gmask=gmask,
-                                    conv_hid=dev(ch.view(np.int32)) if session else None,
-                                    out_pitch=(pitch + P + 63) // 64 * 64 if op64 else None)
-        torch.cuda.synchronize()
-    finally:
-        qa.tune("frame_rows", 2)
+    out, out_len = qa.frame_udp(dev(rows), dev(lens), dev(masks), gmask=gmask,
+                                conv_hid=dev(ch.view(np.int32)) if session else None,
+                                out_pitch=(pitch + P + 63) // 64 * 64 if op64 else None)
+    torch.cuda.synchronize()
     out, out_len = out.cpu().numpy(), out_len.cpu().numpy()
     P = 12 if session else 4
     for r in range(R):
@@ -59,16 +53,8 @@ def test_frame_vs_oracle(oracle, session, pitch, op64, rows_per_wave):
         assert not out[r, len(ref):].any(), r  # zero up to the pitch
 
 
-@pytest.fixture(params=[2, 1, 4], ids=["rows2", "rows1", "rows4"])
-def frame_rows(request):
-    """Rows per wave of the framing kernels (frame_rows; 2 is the default)."""
-    qa.tune("frame_rows", request.param)
-    yield request.param
-    qa.tune("frame_rows", 2)
-
-
 @pytest.mark.parametrize("session", [False, True])
-def test_unframe_roundtrip_and_errors(oracle, session, frame_rows):
+def test_unframe_roundtrip_and_errors(oracle, session):
     rng = np.random.default_rng(7 + session)
     R, pitch = 403, 1072  # odd: the last wave of two or four rows is partly empty
     P = 12 if session else 4

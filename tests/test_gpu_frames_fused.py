@@ -53,17 +53,9 @@ CASES = [(10, 13, 500, 1040, 1), (4, 6, 501, 1040, 1), (8, 12, 13, 1040, 1), (10
          (4, 6, 77, 528, 1), (10, 13, 200, 1408, 1), (10, 13, 150, 1040, 0), (5, 8, 120, 1040, 1)]
 
 
-@pytest.fixture(params=[1, 3], ids=["lanes16", "lanes8"])
-def send_wave(request):
-    """The one-pass frame send on 16-B lanes (wire_send_wave 1, the default) and on 8-B lanes (3)."""
-    qa.tune("wire_send_wave", request.param)
-    yield request.param
-    qa.tune("wire_send_wave", 1)
-
-
 @pytest.mark.parametrize("session", [False, True], ids=["udp", "session"])
 @pytest.mark.parametrize("k,n,G,sp,checksum", CASES)
-def test_pack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session, send_wave):
+def test_pack_frames_vs_oracle(oracle, k, n, G, sp, checksum, session):
     """One pass where it applies (checksums on, 1088 / 576-B frame pitch), the two-call path
     otherwise; both against pack_group o frame_udp, padding zero, a void group -1."""
     rng = np.random.default_rng(k * 1000 + G + sp + session)

@@ -82,25 +82,13 @@ def main():
     variants = [
         ("encode auto (the library's own choice)", lambda: qa.tune("encode_impl", -1), enc, enc_bytes),
         ("encode impl0 (all rows)", lambda: qa.tune("encode_impl", 0), enc, enc_bytes),
-        ("encode impl1 (row loop)", lambda: qa.tune("encode_impl", 1), enc, enc_bytes),
         ("encode impl2 (inputs in halves)", lambda: qa.tune("encode_impl", 2), enc, enc_bytes),
         ("encode ldslog", lambda: (qa.tune("encode_impl", 0), qa.set_kernel_variant(1)), enc, enc_bytes),
         ("probe xor (traffic only)", lambda: None, probe, enc_bytes),
         ("recon auto (the library's own choice)", lambda: qa.tune("recon_impl", -1), rec, dec_bytes),
-        ("recon impl0 (row loop)", lambda: qa.tune("recon_impl", 0), rec, dec_bytes),
-        ("recon impl1 (all rows)", lambda: qa.tune("recon_impl", 1), rec, dec_bytes),
-        ("recon impl2 (exact e rows)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),
-        ("recon impl3 (exact e, 8-B lanes, full lines)", lambda: (qa.tune("recon_full_lines", 2), qa.tune("recon_impl", 3)), rec,
-         dec_bytes),
-        ("recon impl3 partial last line", lambda: (qa.tune("recon_full_lines", 0), qa.tune("recon_impl", 3)), rec,
-         dec_bytes),
-        ("recon impl3 tables in record", lambda: (qa.tune("recon_compact", 0), qa.tune("recon_impl", 3)), rec,
-         dec_bytes),
-        ("recon impl2 tables in record", lambda: (qa.tune("recon_compact", 0), qa.tune("recon_impl", 2)), rec,
-         dec_bytes),
+        ("recon impl2 (exact e rows, 16-B lanes)", lambda: qa.tune("recon_impl", 2), rec, dec_bytes),
+        ("recon impl3 (exact e, 8-B lanes)", lambda: qa.tune("recon_impl", 3), rec, dec_bytes),
         ("recon impl4 (exact e, 12-B lanes)", lambda: qa.tune("recon_impl", 4), rec, dec_bytes),
-        ("recon impl5 (one wave per group, 8-B slabs)", lambda: qa.tune("recon_impl", 5), rec, dec_bytes),
-        ("recon impl6 (impl3 at 8 waves/SIMD)", lambda: qa.tune("recon_impl", 6), rec, dec_bytes),
         ("recon impl8 (impl3, one group per block)", lambda: qa.tune("recon_impl", 8), rec, dec_bytes),
     ]
     if a.recon_only:
@@ -110,7 +98,7 @@ def main():
     if a.recon8:
         variants = [v for v in variants if v[0].startswith(("recon impl3", "recon impl2", "recon impl4", "probe"))]
     if a.encode_only:
-        variants = [v for v in variants if v[0].startswith(("encode impl0", "encode impl1", "probe"))]
+        variants = [v for v in variants if v[0].startswith(("encode impl0", "encode impl2", "probe"))]
     if a.pairs:
         variants = []
     times = {v[0]: [] for v in variants}
@@ -118,8 +106,6 @@ def main():
     for r in range(a.rounds):
         for name, setup, fn, _ in variants:
             qa.set_kernel_variant(0)
-            qa.tune("recon_full_lines", 1)
-            qa.tune("recon_compact", 1)
             setup()
             fn()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -162,7 +148,7 @@ def main():
         qa.tune("recon_impl", -1)
     qa.set_kernel_variant(0)
     qa.tune("encode_impl", -1)
-    qa.tune("recon_impl", 0)
+    qa.tune("recon_impl", -1)
     code.encode(data, par, B)
     torch.cuda.synchronize()
     assert torch.equal(par, ref_par)

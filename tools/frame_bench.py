@@ -52,7 +52,6 @@ def main():
     fns = {"frame": lambda: qa.frame_udp(rows, lens, masks, gmask=0x3C, out_pitch=op),
            "unframe": lambda: qa.unframe_udp(framed, flen, gmask=0x3C, out_pitch=1088)}
     for spec in a.variants.split(";"):
-        qa.tune("frame_rows", 2)  # the defaults, then the variant's knobs
         if spec != "base":
             for kv in spec.split(","):
                 kk, v = kv.split("=")

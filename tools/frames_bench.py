@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--session", action="store_true")
     ap.add_argument("--payload", type=int, default=1024)
-    ap.add_argument("--tune", default="", help="qfec_tune settings, e.g. wire_send_wave=3")
+    ap.add_argument("--tune", default="", help="qfec_tune settings, e.g. wire_rx=3")
     a = ap.parse_args()
     for kv in filter(None, a.tune.split(",")):
         kk, vv = kv.split("=")

@@ -17,6 +17,6 @@ echo "== rocprofv3" && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --
   -d $R/$OUT/prof -o trace -- python3 $R/tools/wire_bench.py --cpu-seconds 0 > $R/$OUT/wire_prof.json 2> $R/$OUT/wire_prof.err) || { tail -20 $OUT/wire_prof.err; exit 4; }
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/wire_kernel_stats.csv \;
 cut -d, -f1-4 $OUT/wire_kernel_stats.csv | head -8
-echo "== A/B" && timeout -k 10 300 python tools/wire_ab.py > $OUT/wire_ab.txt 2>&1 && timeout -k 10 300 python tools/wire_ab.py --unpack --variants "base;wire_rx_tail=0;wire_fused_rx=0" >> $OUT/wire_ab.txt 2>&1 || { tail -20 $OUT/wire_ab.txt; exit 5; }
+echo "== A/B" && timeout -k 10 300 python tools/wire_ab.py > $OUT/wire_ab.txt 2>&1 && timeout -k 10 300 python tools/wire_ab.py --unpack --variants "base;wire_rx=3;wire_rx=0" >> $OUT/wire_ab.txt 2>&1 || { tail -20 $OUT/wire_ab.txt; exit 5; }
 cat $OUT/wire_ab.txt
 echo done

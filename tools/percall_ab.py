@@ -19,7 +19,7 @@ import quicknet_amd as qa  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="percall_resident=1;percall_resident=0,percall_spin=1;percall_resident=0,percall_spin=0")
+    ap.add_argument("--variants", default="percall_resident=1;percall_resident=0")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=2000)
     ap.add_argument("--ref", action="store_true", help="also time the reference fec.c per-call on this CPU")

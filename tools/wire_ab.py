@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 import quicknet_amd as qa  # noqa: E402
 
-KNOBS = {"wire_fused": 1, "wire_store_nt": 3, "wire_rx": 1, "wire_chunk": 0, "wire_send_wave": 1, "wire_line": 1}
+KNOBS = {"wire_fused": 1, "wire_rx": 1}
 
 
 def main():
@@ -27,7 +27,7 @@ def main():
     p.add_argument("--groups", type=int, default=100_000)
     p.add_argument("--rounds", type=int, default=10)
     p.add_argument("--reps", type=int, default=10)
-    p.add_argument("--variants", default="base;wire_store_nt=0;wire_store_nt=1;wire_fused=0")
+    p.add_argument("--variants", default="base;wire_fused=0")
     p.add_argument("--unpack", action="store_true", help="time qfec_unpack_datagrams (n - k losses per group)")
     p.add_argument("--align", type=int, default=16, help="shard and wire row pitches rounded to this (16 or 64)")
     p.add_argument("--wire-align", type=int, default=0, help="wire row pitch rounded to this instead (e.g. 64)")
