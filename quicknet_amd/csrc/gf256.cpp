@@ -274,7 +274,9 @@ void build_record(const RecordLayout& L, int k, int e, const uint8_t* rows, cons
         for (int j = 0; j < e; ++j)
             if (rows[(size_t)j * k] == 0) {
                 out[L.hdr + ((size_t)j * k) * QFEC_TAB_STRIDE + 5] = 1;
-                out[1] |= 1u << j;
+                // word 1 covers rows 0..31: its readers (the specialised kernels, the LUT's seed
+                // bit) only see codes with n <= QFEC_LUT_MAX_N; wider rows rely on the table flag
+                if (j < 32) out[1] |= 1u << j;
             }
 }
 

@@ -462,10 +462,13 @@ int ensure_small(DevCtx& c, size_t words) {
 // true if p is device (or managed) memory visible to the current device
 // Plain (malloc'd, unregistered) host pointers this thread has probed, a small direct-mapped
 // cache: the per-packet ABIs probe every packet pointer, and a probe costs a runtime lookup
-// (tools/ptr_probe.cpp).  An address the runtime does not know is outside the HSA runtime's
-// device and managed allocations, and those are never placed at it later (they come from the
-// GPU virtual-address apertures the runtime reserves when it starts), so the answer "not device
-// memory" cannot go stale; registering or pinning the block later still leaves it host memory.
+// (tools/ptr_probe.cpp).  What the cache relies on: hipMalloc'd device memory comes from the GPU
+// virtual-address apertures the runtime reserves, so a freed malloc block's address does not
+// become device memory later.  The runtime does not promise that for every kind: an HMM-backed
+// hipMallocManaged allocation is ordinary mmap'd memory and may reuse such an address, and then
+// stays "host" here.  The bytes are still right (the CPU reaches managed memory; the copies go
+// through the CPU), only the path is the host one.  Registering or pinning a block later leaves
+// it host memory.
 bool is_device_ptr(const void* p) {
     if (!p) return false;
     thread_local const void* plain[64] = {};
@@ -2108,6 +2111,28 @@ size_t count_device_ptrs(unsigned char* const* ptrs, size_t count, HostPool& poo
     return ndev.load();
 }
 
+// QFEC_RS_TRACE=1: where a host-pointer call's time goes (host gather, event waits, host scatter),
+// printed per call to stderr
+thread_local double t_rs_classify = 0;  // seconds the entry spent classifying the pointers
+thread_local std::chrono::steady_clock::time_point t_rs_entry;  // when the ABI entry was called
+
+struct RsTrace {
+    bool on = getenv("QFEC_RS_TRACE") != nullptr;
+    double gather = 0, wait = 0, scatter = 0;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    static double since(std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+    }
+    void report(const char* what, long long chunks, int threads) const {
+        if (on)
+            fprintf(stderr,
+                    "[qfec] %s: %.2f ms in the call (classify %.2f, pipeline %.2f: gather %.2f, wait %.2f, scatter %.2f "
+                    "ms); %lld chunks, %d threads\n",
+                    what, since(t_rs_entry) * 1e3, t_rs_classify * 1e3, since(t0) * 1e3, gather * 1e3, wait * 1e3,
+                    scatter * 1e3, chunks, threads);
+    }
+};
+
 // bytes of caller shards per pipelined chunk of the host-pointer paths (tuning "host_chunk"
 // overrides with groups per chunk)
 constexpr size_t kRsPipeBytes = (size_t)16 << 20;
@@ -2137,6 +2162,7 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
     for (auto& h : ctx.host)
         if ((rc = ensure_host_slot(h, slot_bytes, 16))) return rc;
     const bool zc = tuning().host_zero_copy != 0;
+    RsTrace tr;
     long long pending[2] = {-1, -1};
     auto rows_job = [&](size_t nrows, const std::function<void(size_t)>& row) {
         pool->run(
@@ -2149,10 +2175,14 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
     auto drain = [&](int sl) -> int {
         if (pending[sl] < 0) return QFEC_OK;
         DevCtx::HostSlot& h = ctx.host[sl];
+        auto tw = std::chrono::steady_clock::now();
         HIP_TRY(hipEventSynchronize(h.done));
+        tr.wait += RsTrace::since(tw);
+        tw = std::chrono::steady_clock::now();
         const long long g0 = pending[sl], gn = std::min(per, G - g0);
         const uint8_t* hp = h.h_in + (size_t)gn * dg;
         rows_job((size_t)gn * m, [&](size_t i) { memcpy(par[(size_t)g0 * m + i], hp + i * pitch, (size_t)B); });
+        tr.scatter += RsTrace::since(tw);
         pending[sl] = -1;
         return QFEC_OK;
     };
@@ -2165,10 +2195,12 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
         uint8_t* hp = h.h_in + (size_t)gn * dg;
         // data rows (and, when a parity row keeps its old bytes -- the rs.c quirk -- the parity rows)
         const size_t nd = (size_t)gn * k, np = any_stale ? (size_t)gn * m : 0;
+        const auto tg = std::chrono::steady_clock::now();
         rows_job(nd + np, [&](size_t r) {
             if (r < nd) memcpy(hd + r * pitch, data[(size_t)g0 * k + r], (size_t)B);
             else memcpy(hp + (r - nd) * pitch, par[(size_t)g0 * m + (r - nd)], (size_t)B);
         });
+        tr.gather += RsTrace::since(tg);
         uint8_t* z = rs_slot_dev(h, zc);
         uint8_t* dd = z ? z : h.d_buf;
         if (!z) {
@@ -2187,6 +2219,7 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
     }
     if (!rc) rc = drain((int)((nchunks - 1) & 1));
     if (rc) quiesce_host_slots(ctx);  // nothing may still be writing into the slots
+    tr.report("reed_solomon_encode (host)", nchunks, pool->threads());
     return rc;
 }
 
@@ -2210,6 +2243,7 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
     for (auto& h : ctx.host)
         if ((rc = ensure_host_slot(h, slot_bytes, 16))) return rc;
     const bool zc = tuning().host_zero_copy != 0;
+    RsTrace tr;
     std::vector<uint8_t> todo[2];  // per slot, per group: 1 = decoded (scatter its erased data rows)
     long long pending[2] = {-1, -1};
     std::atomic<long long> fails{0};
@@ -2220,7 +2254,10 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
     auto drain = [&](int sl) -> int {
         if (pending[sl] < 0) return QFEC_OK;
         DevCtx::HostSlot& h = ctx.host[sl];
+        auto tw = std::chrono::steady_clock::now();
         HIP_TRY(hipEventSynchronize(h.done));
+        tr.wait += RsTrace::since(tw);
+        tw = std::chrono::steady_clock::now();
         const long long g0 = pending[sl], gn = std::min(per, G - g0);
         const uint8_t* todo_s = todo[sl].data();
         const uint8_t* hd = h.h_in;
@@ -2232,6 +2269,7 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
                     if (dm[i]) memcpy(data[(size_t)(g0 + g) * k + i], hd + ((size_t)g * k + i) * pitch, (size_t)B);
             }
         });
+        tr.scatter += RsTrace::since(tw);
         pending[sl] = -1;
         return QFEC_OK;
     };
@@ -2245,6 +2283,7 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
         uint8_t* hm = h.h_in + (size_t)gn * (dg + pg);
         todo[sl].assign((size_t)gn, 0);
         uint8_t* todo_s = todo[sl].data();
+        const auto tg = std::chrono::steady_clock::now();
         groups_job(gn, [&](long long a, long long b) {
             long long nf = 0;
             for (long long g = a; g < b; ++g) {
@@ -2277,6 +2316,7 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
             }
             fails += nf;
         });
+        tr.gather += RsTrace::since(tg);
         uint8_t* z = rs_slot_dev(h, zc);
         uint8_t* dd = z ? z : h.d_buf;
         const size_t used = (size_t)gn * (dg + pg + n);
@@ -2299,6 +2339,7 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
     if (!rc) rc = drain((int)((nchunks - 1) & 1));
     if (rc) quiesce_host_slots(ctx);
     *nfail = fails.load();
+    tr.report("reed_solomon_reconstruct (host)", nchunks, pool->threads());
     return rc;
 }
 
@@ -2398,6 +2439,7 @@ int reed_solomon_encode(reed_solomon* rs, unsigned char** shards, int nr_shards,
     const int k = rs->data_shards, m = rs->parity_shards, n = rs->shards;
     const long long G = nr_shards / n;
     if (G <= 0 || block_size <= 0) return 0;
+    t_rs_entry = std::chrono::steady_clock::now();
     sync_rows(h);
     qfec_code* c = h->code;
     DevCtx* ctx = nullptr;
@@ -2416,7 +2458,9 @@ int reed_solomon_encode(reed_solomon* rs, unsigned char** shards, int nr_shards,
     // every shard pointer is classified: all device -> in place (or device gathers), all host ->
     // the pipelined host path, a mix -> one copy per row, whatever memory each row is in
     const size_t nptr = (size_t)G * n;
+    const auto tc = std::chrono::steady_clock::now();
     const size_t ndev = count_device_ptrs(shards, nptr, *host_pool());
+    t_rs_classify = RsTrace::since(tc);
     if (ndev == 0) {
         rc = rs_encode_pipe(*ctx, c, tab, data, par, G, block_size, any_stale);
         if (rc) fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
@@ -2460,6 +2504,7 @@ int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned 
     const int k = rs->data_shards, m = rs->parity_shards, n = rs->shards;
     const long long G = nr_shards / n;
     if (G <= 0 || block_size <= 0) return 0;
+    t_rs_entry = std::chrono::steady_clock::now();
     sync_rows(h);
     qfec_code* c = h->code;
     const bool dev_marks = is_device_ptr(marks);
@@ -2487,7 +2532,10 @@ int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned 
             fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error());
             return rc;
         }
-        if (count_device_ptrs(shards, (size_t)G * n, *host_pool()) == 0) {
+        const auto tc = std::chrono::steady_clock::now();
+        const bool all_host = count_device_ptrs(shards, (size_t)G * n, *host_pool()) == 0;
+        t_rs_classify = RsTrace::since(tc);
+        if (all_host) {
             DevTables* d = nullptr;
             std::vector<uint8_t> seed;
             {

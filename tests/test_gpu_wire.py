@@ -245,28 +245,20 @@ def test_unpack_row_tails(k, n, checksum, pitch):
     assert ok_rows > G * k // 2
 
 
-@pytest.mark.parametrize("k,n,G,sp,wp,wave", [(10, 13, 500, 1040, 1088, 1), (4, 6, 500, 1040, 1088, 1),
-                                              (8, 12, 500, 1040, 1088, 1), (5, 8, 500, 1040, 1088, 1),
-                                              (10, 13, 13, 1040, 1088, 1), (10, 13, 500, 528, 576, 1),
-                                              (4, 6, 501, 528, 576, 1), (10, 13, 13, 528, 576, 1),
-                                              (10, 13, 500, 1408, 1472, 2), (4, 6, 500, 1408, 1472, 2),
-                                              (8, 12, 501, 1408, 1472, 2), (10, 13, 13, 1408, 1472, 2),
-                                              (3, 5, 300, 1104, 1152, 2), (10, 13, 200, 2096, 2112, 2),
-                                              (10, 13, 300, 784, 832, 2), (4, 6, 301, 592, 640, 2),
-                                              (10, 13, 500, 1040, 1088, 3), (4, 6, 501, 1040, 1088, 3),
-                                              (10, 13, 13, 1040, 1088, 3), (10, 13, 500, 1408, 1472, 3),
-                                              (8, 12, 501, 1408, 1472, 3), (3, 5, 300, 1536, 1600, 3),
-                                              (10, 13, 300, 784, 832, 3), (10, 13, 500, 1408, 1472, 1),
-                                              (4, 6, 77, 1408, 1472, 4)])
-def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp, wave):
-    """Payloads with a 1088-B (1 KiB class, one group per wave) or 576-B (512-B class, two
-    groups per wave) wire pitch: the send that finishes line 0 inside the wave (k_pack_wave64,
-    wire_send_wave 1) writes the same datagrams and lengths as the body + k_pack_line0 pair
-    (0), and both equal the oracle's on sampled groups.  wire_send_wave 2 also runs one wave per
-    group above 1088 B in two passes over the row (1472: 1400-B payloads, up to 2112) and below
-    1088 B with the lanes past the row idle; 3 runs it on 8-byte lanes (two passes at 1088 B,
-    three at 1472 and 1600), which 1 (the default) does above 1088 B; 4 is that body at 5 waves/SIMD.  Sizes 0 .. sp - 4 (half exactly
-    sp - 16), one oversize group, G = 13 / 501 leave the last block partly (or a wave half) dead."""
+@pytest.mark.parametrize("k,n,G,sp,wp", [(10, 13, 500, 1040, 1088), (4, 6, 500, 1040, 1088), (8, 12, 500, 1040, 1088),
+                                         (5, 8, 500, 1040, 1088), (10, 13, 13, 1040, 1088), (10, 13, 500, 528, 576),
+                                         (4, 6, 501, 528, 576), (10, 13, 13, 528, 576), (10, 13, 500, 1408, 1472),
+                                         (4, 6, 500, 1408, 1472), (8, 12, 501, 1408, 1472), (10, 13, 13, 1408, 1472),
+                                         (3, 5, 300, 1104, 1152), (10, 13, 200, 2096, 2112), (10, 13, 300, 784, 832),
+                                         (4, 6, 301, 592, 640), (3, 5, 300, 1536, 1600), (4, 6, 77, 1408, 1472)])
+def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp):
+    """The fused send at the wire pitches the library picks its forms by -- one wave per group
+    finishing line 0 itself (k_pack_wave64: 1 088 B on 16-B lanes, 576 B two groups per wave,
+    1 104..1 600 B on 8-B lanes in three passes), the body + k_pack_line0 pair at other 64-B
+    multiples (832, 640, 2 112) -- writes the same datagrams and lengths as the staged path
+    (wire_fused 0), and both equal the oracle's on sampled groups.  Sizes 0 .. sp - 4 (half
+    exactly sp - 16), one oversize group, G = 13 / 501 leave the last block partly (or a wave
+    half) dead."""
     rng = np.random.default_rng(n * 7 + k + G + sp)
     m = n - k
     sizes = rng.integers(0, sp - 3, size=G * k).astype(np.int32)
@@ -279,14 +271,15 @@ def test_pack_wave64_matches_line0(oracle, k, n, G, sp, wp, wave):
     code = qa.Code.vandermonde(k, m)
     full = np.concatenate([np.eye(k, dtype=np.uint8), code.rows])
     res = []
-    for w in (wave, 0):
-        qa.tune("wire_send_wave", w)
+    saved = qa.tune_get("wire_fused")
+    for w in (1, 0):
+        qa.tune("wire_fused", w)
         try:
             _, wire, wlen = code.pack_datagrams(padded_payload(payload), dev(offs), dev(sizes), dev(seq), True,
                                                 shard_pitch=sp, wire_pitch=wp)
             torch.cuda.synchronize()
         finally:
-            qa.tune("wire_send_wave", 1)
+            qa.tune("wire_fused", saved)
         res.append((wire.cpu().numpy(), wlen.cpu().numpy()))
     (w1, l1), (w0, l0) = res
     assert np.array_equal(l1, l0)
