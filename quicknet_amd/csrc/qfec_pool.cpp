@@ -7,8 +7,6 @@
 
 #include <algorithm>
 
-#include "qfec_internal.hpp"
-
 namespace qfec {
 
 HostPool::HostPool(int nthreads) {
@@ -91,20 +89,6 @@ int usable_cpus() {
             n = std::min<long long>(n, std::max<long long>(1, (q1 + p1 - 1) / p1));
     }
     return n;
-}
-
-std::shared_ptr<HostPool> host_pool() {
-    static std::mutex mu;
-    static std::shared_ptr<HostPool> pool;
-    static int made_with = -1;
-    std::lock_guard<std::mutex> lk(mu);
-    const int want = tuning().host_threads;
-    if (!pool || want != made_with) {
-        const int n = want > 0 ? std::min(want, 64) : std::min(usable_cpus(), 32);
-        pool = std::make_shared<HostPool>(n);
-        made_with = want;
-    }
-    return pool;
 }
 
 }  // namespace qfec

@@ -41,9 +41,9 @@ private:
 // (cgroup v2 cpu.max or v1 cpu.cfs_quota_us / cpu.cfs_period_us)
 int usable_cpus();
 
-// the process-wide pool, created on first use with tuning "host_threads" threads (0: usable_cpus(),
-// at most 32) and re-created when that knob changes; callers keep the returned reference while
-// they use it
+// the process-wide pool of libqfec's module/rs.h host paths (defined in qfec_runtime.cpp), created
+// on first use with tuning "host_threads" threads (0: usable_cpus(), at most 32) and re-created
+// when that knob changes; callers keep the returned reference while they use it
 std::shared_ptr<HostPool> host_pool();
 
 }  // namespace qfec

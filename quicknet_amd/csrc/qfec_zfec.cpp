@@ -25,6 +25,7 @@
 // send groups' payloads -- move to the other arena of the pair, and the rest is dropped.
 // Sessions' send and receive machines run on several threads; the callbacks run in session
 // order, op order, on the flushing thread.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -45,6 +46,7 @@
 
 #include "../../include/qfec.h"
 #include "../../include/qfec_zfec.h"
+#include "qfec_pool.hpp"
 
 namespace {
 
@@ -162,6 +164,33 @@ struct Op {
     float f = 0;
     uint64_t uid = 0;  // OP_UNPACK: the datagram's id (decode cache keys)
 };
+// OP_UNPACK: the header fields the flush reads, taken at the input call while the datagram is in
+// cache (the flush would otherwise miss on every arena header): a = tag (d[0], -1 if empty),
+// b = i_recv (d[1..4]), c = src (d[5..8]), f's bits = ik|k|n (d[9..10]) << 16 | the shard's size
+// field (the two bytes after the header; 0 if the datagram ends first)
+inline void parse_head(Op& o, const uint8_t* d, uint32_t size) {
+    o.a = size >= 1 ? d[0] : -1;
+    uint32_t ikn = 0, szf = 0;
+    if (size >= 11) {
+        o.b = (int)rd32(d + 1);
+        o.c = (int)rd32(d + 5);
+        ikn = (uint32_t)d[9] | (uint32_t)d[10] << 8;
+        const uint32_t hdr = d[0] == 0xED ? 13 : 11;
+        if (size >= hdr + 2) szf = (uint32_t)d[hdr] | (uint32_t)d[hdr + 1] << 8;
+    }
+    const uint32_t w = ikn << 16 | szf;
+    memcpy(&o.f, &w, 4);
+}
+inline uint32_t op_ikn(const Op& o) {
+    uint32_t w;
+    memcpy(&w, &o.f, 4);
+    return w >> 16;
+}
+inline uint32_t op_szf(const Op& o) {
+    uint32_t w;
+    memcpy(&w, &o.f, 4);
+    return w & 0xFFFF;
+}
 
 // send state (zfec_pack_input) and the open group carried across flushes
 struct TxState {
@@ -178,7 +207,7 @@ struct TxState {
     int g_emitted = 0;
 };
 
-struct Session {
+struct alignas(64) Session {  // (one cache line boundary per session: threads run adjacent ones)
     void* peer = nullptr;
     int max_pkt = 0, kmax = 0;
     TxState tx;
@@ -235,12 +264,47 @@ struct HostArena {
     // n bytes at a 16-B aligned offset, 16 readable bytes after them (the kernels' loads)
     bool append(const void* p, size_t n, uint32_t* off) {
         const size_t o = round16(used);
-        if (o + n + 16 > (size_t)UINT32_MAX || !reserve(o + n + 16)) return false;
-        if (n) memcpy(h + o, p, n);
-        memset(h + o + n, 0, 16);
+        if (o + round16(n) + 16 > (size_t)UINT32_MAX || !reserve(o + round16(n) + 16)) return false;
+        if (arena_nt()) {
+            copy_stream(h + o, static_cast<const uint8_t*>(p), n);
+        } else {
+            if (n) memcpy(h + o, p, n);
+            memset(h + o + n, 0, 16);
+        }
         used = o + n;
         *off = (uint32_t)o;
         return true;
+    }
+    // QFEC_ZFEC_NT=1 (A/B): the input calls' copies bypass the caches (streaming stores)
+    static bool arena_nt() {
+        static const bool on = getenv("QFEC_ZFEC_NT") && atoi(getenv("QFEC_ZFEC_NT")) == 1;
+        return on;
+    }
+    // dst 16-B aligned: n bytes, zeros up to round16(n) + 16, with streaming stores (no read for
+    // ownership; the arena is read next by the DMA engine and, much later, by the callbacks)
+    static void copy_stream(uint8_t* dst, const uint8_t* src, size_t n) {
+        size_t i = 0;
+        for (; i + 64 <= n; i += 64) {
+            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+            const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+            const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+            const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+        }
+        for (; i + 16 <= n; i += 16)
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i),
+                             _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i)));
+        if (i < n) {
+            alignas(16) uint8_t t[16] = {};
+            memcpy(t, src + i, n - i);
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_load_si128(reinterpret_cast<const __m128i*>(t)));
+            i += 16;
+        }
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_setzero_si128());
+        _mm_sfence();  // visible to the flush (maybe on another thread) and to the DMA engine
     }
 };
 
@@ -284,6 +348,7 @@ struct qfec_zfec {
     int rxc = 0, txc = 0;
     HostArena io;            // per-flush pinned staging: tables in, results and datagrams out
     DevBuf d_rx, d_tx, d_io, d_work;
+    std::unique_ptr<qfec::HostPool> pool;  // the flush's session threads (kept between flushes)
 };
 
 namespace {
@@ -313,20 +378,21 @@ struct Bufs {
     }
 };
 
-// run f(i) for i < count on up to `threads` threads
+// run f(i) for i < count on up to `threads` threads of the context's pool (the calling thread
+// is one of them; the pool's threads stay between flushes)
 template <class F>
-void parallel_for(size_t count, unsigned threads, F&& f) {
+void parallel_for(qfec_zfec* z, size_t count, unsigned threads, F&& f) {
     if (threads <= 1 || count <= 1) {
         for (size_t i = 0; i < count; ++i) f(i);
         return;
     }
+    if (!z->pool || z->pool->threads() < (int)threads) z->pool.reset(new qfec::HostPool((int)threads));
     std::atomic<size_t> next{0};
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < threads; ++t)
-        th.emplace_back([&]() {
+    z->pool->run(
+        [&](int, int) {
             for (size_t i; (i = next.fetch_add(1)) < count;) f(i);
-        });
-    for (auto& x : th) x.join();
+        },
+        (int)threads);
 }
 
 // staging bump allocator over the pinned io arena and its device twin (same offsets)
@@ -493,6 +559,7 @@ struct DecodeOut {
 };
 struct DecodeReq {
     DecodeKey key;
+    bool fresh = false;  // the first request of its key (the one that is launched)
     int nsh = 0;
     View shard[16];  // the k shards, ik in key.ik
     DecodeOut* out = nullptr;
@@ -507,9 +574,8 @@ struct RxPass {
 // the receive side of one session over its queued ops (NetFecCodec.cpp:189-371)
 class RxMachine {
    public:
-    RxMachine(Session& S, int sidx, const std::vector<Verdict>& verd, RxPass& pass, std::vector<Emit>& out,
-              const uint8_t* rx)
-        : S(S), R(S.rx), sidx(sidx), verd(verd), pass(pass), out(out), rx(rx) {}
+    RxMachine(Session& S, int sidx, const std::vector<Verdict>& verd, RxPass& pass, std::vector<Emit>& out)
+        : S(S), R(S.rx), sidx(sidx), verd(verd), pass(pass), out(out) {}
 
     void run() {
         size_t v = 0;
@@ -529,7 +595,6 @@ class RxMachine {
     const std::vector<Verdict>& verd;
     RxPass& pass;
     std::vector<Emit>& out;
-    const uint8_t* rx;
     uint32_t cur = 0;
 
     void deliver(const View& v, uint32_t src) {
@@ -635,17 +700,16 @@ class RxMachine {
     }
 
     void unpack(const Op& op, const Verdict& vd) {  // zfec_unpack_input :189-371
-        const uint8_t* d = rx + op.off;
         const uint32_t size = op.size;
         if (size > (uint32_t)R.dec_pkt_size) R.dec_pkt_size = (int)size;  // unpack_fec_head realloc (:345-352)
         if (!vd.fec) {  // not an FEC datagram: handed over minus its tag, source index 0 (:201-209)
             if (size >= 1) deliver(View{SRC_RX, op.off + 1, size - 1}, 0u);
             return;
         }
-        R.is_checksum = d[0] == 0xED;  // (:364)
+        R.is_checksum = op.a == 0xED;  // (:364)
         if (!vd.ok || !vd.usable) return;  // (:210-213)
-        const uint32_t i_recv = rd32(d + 1), src = rd32(d + 5);
-        const uint32_t ikn = (uint32_t)d[9] | (uint32_t)d[10] << 8;
+        const uint32_t i_recv = (uint32_t)op.b, src = (uint32_t)op.c;  // (header fields, parse_head)
+        const uint32_t ikn = op_ikn(op);
         const int cur_n = (int)(ikn & 0xF), cur_k = (int)((ikn >> 4) & 0xF), cur_ni = (int)((ikn >> 8) & 0xF);
         const uint32_t seg_beg = i_recv - (uint32_t)cur_ni;
         R.i_recv_pkt = std::max(i_recv, R.i_recv_pkt);
@@ -974,7 +1038,10 @@ static int queue_bytes(qfec_zfec* z, int s, OpType t, const void* p, unsigned in
     o.t = t;
     o.size = size;
     if (!A.append(p, size, &o.off)) return QFEC_ENOMEM;
-    if (t == OP_UNPACK) o.uid = z->next_uid++;
+    if (t == OP_UNPACK) {
+        o.uid = z->next_uid++;
+        parse_head(o, static_cast<const uint8_t*>(p), size);
+    }
     z->sessions[s].ops.push_back(o);
     return QFEC_OK;
 }
@@ -985,12 +1052,17 @@ int qfec_zfec_unpack_input(qfec_zfec* z, int s, const void* datagram, unsigned i
     return queue_bytes(z, s, OP_UNPACK, datagram, size);
 }
 
-int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn unpack_out, void* stream) {
-    if (!z) return QFEC_EINVAL;
-    std::lock_guard<std::mutex> lk(z->mu);
-    // QFEC_ZFEC_TIMING=1: phase times of each flush on stderr (profiling aid)
-    static const bool timing = getenv("QFEC_ZFEC_TIMING") != nullptr;
-    auto t_prev = std::chrono::steady_clock::now();
+}  // extern "C"
+
+namespace {
+// QFEC_ZFEC_TIMING=1: phase times of each flush on stderr (profiling aid)
+const bool g_zfec_timing = getenv("QFEC_ZFEC_TIMING") != nullptr;
+thread_local std::chrono::steady_clock::time_point t_zfec_phase;
+
+int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn unpack_out, void* stream) {
+    const bool timing = g_zfec_timing;
+    auto& t_prev = t_zfec_phase;
+    t_prev = std::chrono::steady_clock::now();
     auto phase = [&](const char* name) {
         if (!timing) return;
         const auto t = std::chrono::steady_clock::now();
@@ -1031,7 +1103,15 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     }
     // ---- send: the machines (threaded over sessions), then their groups merged per (k, n)
     std::vector<std::vector<LocalGroup>> lgroups(NS);
-    parallel_for(NS, threads, [&](size_t si) { tx_machine(z->sessions[si], tx_out[si], lgroups[si], own[si], TXA.h); });
+    parallel_for(z, NS, threads, [&](size_t si) {  // (local vectors: see the receive machines)
+        std::vector<Emit> out;
+        std::vector<LocalGroup> groups;
+        std::vector<uint8_t> own_b;
+        tx_machine(z->sessions[si], out, groups, own_b, TXA.h);
+        out.swap(tx_out[si]);
+        groups.swap(lgroups[si]);
+        own_b.swap(own[si]);
+    });
     std::vector<PackBatch> packs;
     std::map<std::pair<int, int>, int> pack_of;  // (k, n) -> index in packs
     z->io.used = 0;
@@ -1133,70 +1213,112 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     // ---- receive: verdicts of this flush's FEC datagrams (pseudo-groups by (k, n, tag, dec_pkt_size))
     std::vector<std::vector<Verdict>> verd(NS);
     std::vector<UnpackBatch> vb;
-    std::map<std::tuple<int, int, int, int>, int> vb_of;
-    // rows taken in each pseudo-group (shared by all sessions: a row's verdict is its own)
-    std::vector<std::vector<uint16_t>> taken;  // per batch, per group: bit ik
-    std::tuple<int, int, int, int> last_key{-1, -1, -1, -1};
-    int last_bi = -1;
-    for (size_t si = 0; si < NS; ++si) {
-        Session& S = z->sessions[si];
-        int dps = S.rx.dec_pkt_size;  // its growth over the queue (unpack_fec_head realloc)
-        for (auto& op : S.ops) {
-            if (op.t != OP_UNPACK) continue;
-            Verdict v;
-            const uint8_t* d = RXA.h + op.off;
-            const size_t size = op.size;
-            if ((int)size > dps) dps = (int)size;
-            v.fec = size >= 11 && (d[0] == 0xEC || d[0] == 0xED);
-            if (v.fec) {
-                const uint32_t ikn = (uint32_t)d[9] | (uint32_t)d[10] << 8;
-                const int n = (int)(ikn & 0xF), k = (int)((ikn >> 4) & 0xF), ik = (int)((ikn >> 8) & 0xF);
-                v.usable = k >= 1 && k < n && n <= 15 && ik < n;
-                if (v.usable) {
-                    const int cs = d[0] == 0xED ? 1 : 0;
-                    const auto key = std::make_tuple(k, n, cs, dps);
-                    int bi;
-                    if (key == last_key && last_bi >= 0) {
-                        bi = last_bi;
-                    } else if (vb_of.count(key)) {
-                        bi = vb_of[key];
-                    } else {
-                        UnpackBatch b;
-                        b.k = k;
-                        b.n = n;
-                        b.checksum = cs;
-                        b.dec_pkt_size = dps;
-                        vb.push_back(std::move(b));
-                        taken.emplace_back();
-                        bi = (int)vb.size() - 1;
-                        vb_of.emplace(key, bi);
-                    }
-                    last_key = key;
-                    last_bi = bi;
-                    UnpackBatch& b = vb[(size_t)bi];
-                    auto& used = taken[(size_t)bi];
-                    int g = -1;
-                    for (size_t gi = used.size() > 8 ? used.size() - 8 : 0; gi < used.size(); ++gi)
-                        if (!((used[gi] >> ik) & 1u)) {
-                            g = (int)gi;
-                            break;
+    {
+        // per session (on the session threads): its rows placed into pseudo-groups of its own
+        // batches; then the sessions' batches are concatenated per key in session order (any
+        // placement is valid: a row's verdict is its own)
+        using Key = std::tuple<int, int, int, int>;
+        struct Local {
+            Key key;
+            int groups = 0;
+            size_t need = 0;
+            std::vector<UnpackRow> rows;
+            std::vector<uint16_t> taken;  // per group: bit ik
+        };
+        std::vector<std::vector<Local>> loc(NS);
+        parallel_for(z, NS, threads, [&](size_t si) {
+            Session& S = z->sessions[si];
+            std::vector<Local> L;  // (local vectors: see the receive machines)
+            std::vector<Verdict> V;
+            V.reserve(S.ops.size());
+            int dps = S.rx.dec_pkt_size;  // its growth over the queue (unpack_fec_head realloc)
+            int last = -1;
+            for (auto& op : S.ops) {
+                if (op.t != OP_UNPACK) continue;
+                Verdict v;
+                const size_t size = op.size;
+                if ((int)size > dps) dps = (int)size;
+                v.fec = size >= 11 && (op.a == 0xEC || op.a == 0xED);
+                if (v.fec) {
+                    const uint32_t ikn = op_ikn(op);
+                    const int n = (int)(ikn & 0xF), k = (int)((ikn >> 4) & 0xF), ik = (int)((ikn >> 8) & 0xF);
+                    v.usable = k >= 1 && k < n && n <= 15 && ik < n;
+                    if (v.usable) {
+                        const int cs = op.a == 0xED ? 1 : 0;
+                        const Key key = std::make_tuple(k, n, cs, dps);
+                        if (last < 0 || L[(size_t)last].key != key) {
+                            last = -1;
+                            for (size_t x = 0; x < L.size(); ++x)
+                                if (L[x].key == key) last = (int)x;
+                            if (last < 0) {
+                                L.emplace_back();
+                                L.back().key = key;
+                                L.back().rows.reserve(S.ops.size());
+                                last = (int)L.size() - 1;
+                            }
                         }
-                    if (g < 0) {
-                        used.push_back(0);
-                        g = b.groups++;
+                        Local& b = L[(size_t)last];
+                        int g = -1;
+                        for (size_t gi = b.taken.size() > 8 ? b.taken.size() - 8 : 0; gi < b.taken.size(); ++gi)
+                            if (!((b.taken[gi] >> ik) & 1u)) {
+                                g = (int)gi;
+                                break;
+                            }
+                        if (g < 0) {
+                            b.taken.push_back(0);
+                            g = b.groups++;
+                        }
+                        b.taken[(size_t)g] |= (uint16_t)(1u << ik);
+                        b.rows.push_back(UnpackRow{g, ik, op.off, (uint32_t)size});
+                        // the row bytes dec_src_pkt_info may read: head + the shard's size field
+                        const size_t hdr = cs ? 13 : 11;
+                        if (ik < k && size >= hdr + 2) b.need = std::max(b.need, (size_t)(cs ? 4 : 2) + op_szf(op));
+                        v.batch = last;  // local until the merge
+                        v.group = g;
+                        v.ik = ik;
                     }
-                    used[(size_t)g] |= (uint16_t)(1u << ik);
-                    b.rows.push_back(UnpackRow{g, ik, op.off, (uint32_t)size});
-                    // the row bytes dec_src_pkt_info may read: head + the shard's size field
-                    const size_t hdr = cs ? 13 : 11;
-                    if (ik < k && size >= hdr + 2)
-                        b.need = std::max(b.need, (size_t)(cs ? 4 : 2) + (d[hdr] | (size_t)d[hdr + 1] << 8));
-                    v.batch = bi;
-                    v.group = g;
-                    v.ik = ik;
+                }
+                V.push_back(v);
+            }
+            V.swap(verd[si]);
+            L.swap(loc[si]);
+        });
+        std::map<Key, int> vb_of;
+        std::vector<std::pair<int, int>> where;  // local batch -> (batch, group offset)
+        for (size_t si = 0; si < NS; ++si) {
+            where.assign(loc[si].size(), std::make_pair(0, 0));
+            for (size_t x = 0; x < loc[si].size(); ++x) {
+                Local& lb = loc[si][x];
+                auto it = vb_of.find(lb.key);
+                int bi;
+                if (it == vb_of.end()) {
+                    UnpackBatch b;
+                    b.k = std::get<0>(lb.key);
+                    b.n = std::get<1>(lb.key);
+                    b.checksum = std::get<2>(lb.key);
+                    b.dec_pkt_size = std::get<3>(lb.key);
+                    vb.push_back(std::move(b));
+                    bi = (int)vb.size() - 1;
+                    vb_of.emplace(lb.key, bi);
+                } else {
+                    bi = it->second;
+                }
+                UnpackBatch& b = vb[(size_t)bi];
+                const int goff = b.groups;
+                where[x] = std::make_pair(bi, goff);
+                b.groups += lb.groups;
+                b.need = std::max(b.need, lb.need);
+                if (goff == 0 && b.rows.empty()) {
+                    b.rows.swap(lb.rows);
+                } else {
+                    for (auto& r : lb.rows) b.rows.push_back(UnpackRow{r.group + goff, r.ik, r.off, r.len});
                 }
             }
-            verd[si].push_back(v);
+            for (auto& v : verd[si])
+                if (v.batch >= 0) {
+                    v.group += where[(size_t)v.batch].second;
+                    v.batch = where[(size_t)v.batch].first;
+                }
         }
     }
     phase("rx grouping");
@@ -1215,7 +1337,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             if ((rc = run_unpack(z, b, z->d_rx.d, st))) return rc;
         if (hipStreamSynchronize(st) != hipSuccess) return QFEC_EHIP;
     }
-    parallel_for(NS, threads, [&](size_t si) {
+    parallel_for(z, NS, threads, [&](size_t si) {
         size_t v = 0;
         for (auto& op : z->sessions[si].ops) {
             if (op.t != OP_UNPACK) continue;
@@ -1223,7 +1345,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
             if (vd.group < 0) continue;
             const UnpackBatch& b = vb[(size_t)vd.batch];
             const size_t row = (size_t)vd.group * b.n + vd.ik;
-            const uint32_t hdr = RXA.h[op.off] == 0xED ? 13 : 11;
+            const uint32_t hdr = op.a == 0xED ? 13 : 11;
             vd.ok = b.rx[row] >= 0;
             if (vd.ok) vd.shard = View{SRC_RX, op.off + hdr, op.size - hdr};
             if (vd.ik < b.k && vd.ok) {
@@ -1240,7 +1362,7 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     // every row of it decoded and passed (the common case) and leaves placeholders for its
     // deliveries; after the launches the placeholders are filled when that held for every such
     // decode, and otherwise the machines are replayed from the flush's starting state.
-    DecodeCache cache;
+    std::vector<DecodeCache> caches(NS);  // per session (keys name their session)
     std::vector<RxState> start(NS);
     for (size_t si = 0; si < NS; ++si) start[si] = z->sessions[si].rx;
     std::vector<uint8_t> dec_bytes;  // decoded payloads that are not views of an input shard
@@ -1249,13 +1371,28 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     for (int pass_no = 0;; ++pass_no) {
         missing.clear();
         std::vector<std::vector<DecodeReq>> miss_s(NS);
-        parallel_for(NS, threads, [&](size_t si) {  // sessions are independent
+        parallel_for(z, NS, threads, [&](size_t si) {  // sessions are independent
             Session& S = z->sessions[si];
             if (pass_no) S.rx = start[si];
-            rx_out[si].clear();
-            RxPass pass{&cache, &miss_s[si]};
-            RxMachine m(S, (int)si, verd[si], pass, rx_out[si], RXA.h);
+            // thread-local vectors, swapped in at the end: the per-session vector headers lie
+            // side by side, and a push_back on each would bounce their cache lines between threads
+            std::vector<Emit> out;
+            out.swap(rx_out[si]);
+            out.clear();
+            std::vector<DecodeReq> miss;
+            DecodeCache& cache = caches[si];
+            RxPass pass{&cache, &miss};
+            RxMachine m(S, (int)si, verd[si], pass, out);
             m.run();
+            // this session's new keys enter its cache (node addresses survive rehashing)
+            cache.reserve(cache.size() + miss.size());
+            for (auto& q : miss) {
+                auto ins = cache.emplace(q.key, DecodeOut{});
+                q.out = &ins.first->second;
+                q.fresh = ins.second;
+            }
+            out.swap(rx_out[si]);
+            miss.swap(miss_s[si]);
         });
         // the requests numbered in session order, as one thread would have numbered them
         for (size_t si = 0; si < NS; ++si) {
@@ -1273,12 +1410,8 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
         // pitch (only a corrupt one can) is decoded again at dec_pkt_size + 4 in round 1, as the
         // reference reads it.
         std::vector<const DecodeReq*> todo;
-        cache.reserve(cache.size() + missing.size());
-        for (auto& q : missing) {
-            auto ins = cache.emplace(q.key, DecodeOut{});  // (node addresses survive rehashing)
-            q.out = &ins.first->second;
-            if (ins.second) todo.push_back(&q);
-        }
+        for (auto& q : missing)
+            if (q.fresh) todo.push_back(&q);
         phase("decode dedup");
         for (int round = 0; round < 2 && !todo.empty(); ++round) {
             std::vector<UnpackBatch> db;
@@ -1396,13 +1529,41 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     B.io = z->io.h;
     B.own = &own;
     int calls = 0;
+    // the bytes a callback is handed: an emit's datagram or payload (nullptr: nothing handed)
+    auto bytes_of = [&](const Emit& e, size_t si, unsigned* len) -> const uint8_t* {
+        if (e.kind == 0) {
+            const PackBatch& b = packs[(size_t)e.batch];
+            const size_t row = (size_t)e.group * b.n + e.row;
+            const int wl = reinterpret_cast<const int*>(z->io.h + b.o_wlen)[row];
+            *len = wl > 0 ? (unsigned)wl : 0u;
+            return wl > 0 ? z->io.h + b.o_wire + row * b.wp : nullptr;
+        }
+        *len = e.v.len;
+        return B.p(e.v, si);
+    };
+    // the arenas are far larger than the caches: the bytes a few callbacks ahead are requested
+    // now, so a consumer reading every byte (a socket send, a checksum) finds them on the way
+    static const size_t kAhead = getenv("QFEC_ZFEC_AHEAD") ? (size_t)atoi(getenv("QFEC_ZFEC_AHEAD")) : 3;  // (r05 A/B)
+    auto prefetch = [&](const std::vector<Emit>& l, size_t i, size_t si) {
+        if (i >= l.size() || l[i].kind == 3) return;
+        unsigned len = 0;
+        const uint8_t* q = bytes_of(l[i], si, &len);
+        if (!q) return;
+        for (unsigned o = 0; o < len; o += 64) __builtin_prefetch(q + o, 0, 0);
+    };
     for (size_t si = 0; si < NS; ++si) {
         Session& S = z->sessions[si];
         const auto& to = tx_out[si];
         const auto& ro = rx_out[si];
         size_t a = 0, c = 0;
+        for (size_t i = 0; i < kAhead; ++i) {
+            prefetch(to, i, si);
+            prefetch(ro, i, si);
+        }
         while (a < to.size() || c < ro.size()) {
             const bool take_tx = c >= ro.size() || (a < to.size() && to[a].op <= ro[c].op);
+            if (take_tx) prefetch(to, a + kAhead, si);
+            else prefetch(ro, c + kAhead, si);
             const Emit& e = take_tx ? to[a++] : ro[c++];
             if (e.kind == 0) {
                 const PackBatch& b = packs[(size_t)e.batch];
@@ -1450,6 +1611,19 @@ int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_outp
     }
     phase("compact");
     return calls;
+}
+}  // namespace
+
+extern "C" {
+
+int qfec_zfec_flush(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn unpack_out, void* stream) {
+    if (!z) return QFEC_EINVAL;
+    std::lock_guard<std::mutex> lk(z->mu);
+    const int rc = flush_body(z, pack_out, unpack_out, stream);
+    if (g_zfec_timing)  // what the flush's locals cost to free
+        fprintf(stderr, "[qfec] zfec flush %-12s %8.3f ms\n", "teardown",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_zfec_phase).count());
+    return rc;
 }
 
 int qfec_zfec_stats(const qfec_zfec* z, int s, long long* out8) {

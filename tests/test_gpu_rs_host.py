@@ -231,3 +231,69 @@ def test_rs_host_while_tuning(oracle):
     for k, v in before.items():
         qa.tune(k, v)
     assert not errors, errors[:5]
+
+
+@pytest.mark.parametrize("kind", ["pinned", "shm", "file", "pinned_dev_mix"])
+def test_rs_host_memory_kinds(oracle, tmp_path, kind):
+    """Shards in the other kinds of system memory the pointer classifier meets (pinned host
+    tensors, /dev/shm and regular-file mappings), alone and mixed with device rows: encode and
+    reconstruct equal the oracle's."""
+    import mmap
+    k, m, B, G = 10, 3, 1000, 9
+    n = k + m
+    nbytes = G * n * B
+    keep = []
+    if kind in ("pinned", "pinned_dev_mix"):
+        t = torch.zeros(nbytes, dtype=torch.uint8).pin_memory()
+        keep.append(t)
+        base = t.numpy()
+    else:
+        path = f"/dev/shm/qfec_test_{__import__('os').getpid()}" if kind == "shm" else str(tmp_path / "rows.bin")
+        with open(path, "wb") as f:
+            f.write(b"\0" * nbytes)
+        f = open(path, "r+b")
+        mm = mmap.mmap(f.fileno(), nbytes)
+        keep += [f, mm]
+        base = np.frombuffer(mm, dtype=np.uint8)
+        if kind == "shm":
+            __import__("os").unlink(path)
+    rows = [base[i * B:(i + 1) * B] for i in range(G * n)]
+    if kind == "pinned_dev_mix":
+        rows = [torch.zeros(B, dtype=torch.uint8, device=DEV) if i % 5 == 1 else r for i, r in enumerate(rows)]
+
+    def put(i, a):
+        if isinstance(rows[i], np.ndarray):
+            rows[i][:] = a
+        else:
+            rows[i].copy_(torch.from_numpy(np.ascontiguousarray(a)).to(DEV))
+
+    def get(i):
+        return rows[i].copy() if isinstance(rows[i], np.ndarray) else rows[i].cpu().numpy()
+
+    data0 = synth_bytes(0xC0DE, G * k * B).reshape(G, k, B)
+    for i in range(G * k):
+        put(i, data0.reshape(G * k, B)[i])
+    torch.cuda.synchronize()
+    rs = qa.ReedSolomon(k, m)
+    L = qa.lib()
+    ptrs = ptr_array(rows)
+    assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == 0
+    torch.cuda.synchronize()
+    want = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(oracle.cauchy(k, m), data0, want, B)
+    assert np.array_equal(np.stack([get(G * k + i) for i in range(G * m)]).reshape(G, m, B), want)
+    gm = mixed_marks(G, k, m, 21)
+    marks = marks_to_rs_layout(gm, k)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+    for i in range(G * k):
+        put(i, d.reshape(G * k, B)[i])
+    torch.cuda.synchronize()
+    rc = L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(marks.ctypes.data), G * n, B)
+    torch.cuda.synchronize()
+    exp = d.copy()
+    rc_o = oracle.rs_reconstruct(oracle.cauchy(k, m), exp, want.copy(), marks, B)
+    assert rc == rc_o == -1
+    assert np.array_equal(np.stack([get(i) for i in range(G * k)]).reshape(G, k, B), exp)
+    rs.close()
+    del rows, base

@@ -10,3 +10,7 @@ step rs_t8_c3000 200 python tools/rs_abi_rate.py --reps 2 --threads 8 --chunk 30
 step rs_default 200 python tools/rs_abi_rate.py --reps 2
 cat $OUT/maps.log
 grep -h "value\|\[qfec\]" $OUT/rs_*.log | cut -c1-260
+QFEC_ZFEC_TIMING=1 step zfec_timing 200 python tools/zfec_rate.py --reps 3
+grep -h "rep \|zfec flush" $OUT/zfec_timing.log | tail -40
+QFEC_ZFEC_NT=1 QFEC_ZFEC_TIMING=1 step zfec_timing_nt 200 python tools/zfec_rate.py --reps 3
+grep -h "rep " $OUT/zfec_timing_nt.log | tail -6
