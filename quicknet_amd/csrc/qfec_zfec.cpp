@@ -25,7 +25,6 @@
 // send groups' payloads -- move to the other arena of the pair, and the rest is dropped.
 // Sessions' send and receive machines run on several threads; the callbacks run in session
 // order, op order, on the flushing thread.
-#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -265,46 +264,11 @@ struct HostArena {
     bool append(const void* p, size_t n, uint32_t* off) {
         const size_t o = round16(used);
         if (o + round16(n) + 16 > (size_t)UINT32_MAX || !reserve(o + round16(n) + 16)) return false;
-        if (arena_nt()) {
-            copy_stream(h + o, static_cast<const uint8_t*>(p), n);
-        } else {
-            if (n) memcpy(h + o, p, n);
-            memset(h + o + n, 0, 16);
-        }
+        if (n) memcpy(h + o, p, n);
+        memset(h + o + n, 0, 16);
         used = o + n;
         *off = (uint32_t)o;
         return true;
-    }
-    // QFEC_ZFEC_NT=1 (A/B): the input calls' copies bypass the caches (streaming stores)
-    static bool arena_nt() {
-        static const bool on = getenv("QFEC_ZFEC_NT") && atoi(getenv("QFEC_ZFEC_NT")) == 1;
-        return on;
-    }
-    // dst 16-B aligned: n bytes, zeros up to round16(n) + 16, with streaming stores (no read for
-    // ownership; the arena is read next by the DMA engine and, much later, by the callbacks)
-    static void copy_stream(uint8_t* dst, const uint8_t* src, size_t n) {
-        size_t i = 0;
-        for (; i + 64 <= n; i += 64) {
-            const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
-            const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
-            const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
-            const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
-        }
-        for (; i + 16 <= n; i += 16)
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i),
-                             _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i)));
-        if (i < n) {
-            alignas(16) uint8_t t[16] = {};
-            memcpy(t, src + i, n - i);
-            _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_load_si128(reinterpret_cast<const __m128i*>(t)));
-            i += 16;
-        }
-        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_setzero_si128());
-        _mm_sfence();  // visible to the flush (maybe on another thread) and to the DMA engine
     }
 };
 
@@ -766,7 +730,9 @@ class RxMachine {
         auto it = pass.cache->find(key);
         const DecodeOut* res = it == pass.cache->end() ? nullptr : &it->second;
         int req = -1;  // index of this decode's request (placeholders refer to it)
-        if (!res) {
+        if (!res && !pass.missing->empty() && pass.missing->back().key == key) {
+            req = (int)pass.missing->size() - 1;  // the same decode as this session's last request
+        } else if (!res) {
             pass.missing->emplace_back();
             DecodeReq& q = pass.missing->back();
             q.key = key;
@@ -1367,10 +1333,10 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
     for (size_t si = 0; si < NS; ++si) start[si] = z->sessions[si].rx;
     std::vector<uint8_t> dec_bytes;  // decoded payloads that are not views of an input shard
     dec_bytes.reserve((size_t)4 << 20);
-    std::vector<DecodeReq> missing;
+    std::vector<const DecodeReq*> missing;  // this pass's requests (in the sessions' miss_s)
+    std::vector<std::vector<DecodeReq>> miss_s(NS);
     for (int pass_no = 0;; ++pass_no) {
         missing.clear();
-        std::vector<std::vector<DecodeReq>> miss_s(NS);
         parallel_for(z, NS, threads, [&](size_t si) {  // sessions are independent
             Session& S = z->sessions[si];
             if (pass_no) S.rx = start[si];
@@ -1400,7 +1366,7 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
             if (base)
                 for (auto& e : rx_out[si])
                     if (e.kind == 3) e.batch += base;
-            for (auto& q : miss_s[si]) missing.push_back(std::move(q));
+            for (auto& q : miss_s[si]) missing.push_back(&q);
         }
         phase("rx machine");
         if (missing.empty()) break;
@@ -1410,8 +1376,8 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
         // pitch (only a corrupt one can) is decoded again at dec_pkt_size + 4 in round 1, as the
         // reference reads it.
         std::vector<const DecodeReq*> todo;
-        for (auto& q : missing)
-            if (q.fresh) todo.push_back(&q);
+        for (const DecodeReq* q : missing)
+            if (q->fresh) todo.push_back(q);
         phase("decode dedup");
         for (int round = 0; round < 2 && !todo.empty(); ++round) {
             std::vector<UnpackBatch> db;
@@ -1507,16 +1473,16 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
         }
         phase("decode results");
         bool all_ok = true;
-        for (auto& q : missing) {
-            const DecodeOut& o = *q.out;
-            for (int i = 0; i < q.key.k; ++i) all_ok &= o.ok[i];
+        for (const DecodeReq* q : missing) {
+            const DecodeOut& o = *q->out;
+            for (int i = 0; i < q->key.k; ++i) all_ok &= o.ok[i];
         }
         if (!all_ok) continue;  // replay with the results
         for (size_t si = 0; si < NS; ++si)  // the assumption held: fill the placeholders
             for (auto& e : rx_out[si])
                 if (e.kind == 3) {
                     e.kind = 2;
-                    e.v = missing[(size_t)e.batch].out->payload[e.row];
+                    e.v = missing[(size_t)e.batch]->out->payload[e.row];
                 }
         break;
     }  // (terminates: a pass that asks for decodes adds their keys to the cache)
@@ -1543,7 +1509,9 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
     };
     // the arenas are far larger than the caches: the bytes a few callbacks ahead are requested
     // now, so a consumer reading every byte (a socket send, a checksum) finds them on the way
-    static const size_t kAhead = getenv("QFEC_ZFEC_AHEAD") ? (size_t)atoi(getenv("QFEC_ZFEC_AHEAD")) : 3;  // (r05 A/B)
+    // (3, 6 and 10 ahead measured alike, profiles/r05j; streaming stores for the input copies
+    // instead made them slower, 20 -> 36 ms, profiles/r05g)
+    constexpr size_t kAhead = 4;
     auto prefetch = [&](const std::vector<Emit>& l, size_t i, size_t si) {
         if (i >= l.size() || l[i].kind == 3) return;
         unsigned len = 0;
@@ -1581,6 +1549,15 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
         S.ops.clear();
     }
     phase("callbacks");
+    // the per-session scratch is freed on the session threads (its blocks came from their
+    // allocator arenas; one thread freeing ~10^5 decode-cache nodes took ~3 ms, r05i)
+    parallel_for(z, NS, threads, [&](size_t si) {
+        DecodeCache().swap(caches[si]);
+        std::vector<DecodeReq>().swap(miss_s[si]);
+        std::vector<Emit>().swap(rx_out[si]);
+        std::vector<Emit>().swap(tx_out[si]);
+        std::vector<Verdict>().swap(verd[si]);
+    });
     // ---- what the state still refers to moves to the spare arenas: the window slots'
     // datagrams and the open send groups' payloads; everything else is dropped
     {
