@@ -395,6 +395,15 @@ struct UnpackBatch {
     std::vector<uint32_t> fetch;  // decodes: the rows (g * n + i) to bring back, in this order
     size_t need = 0;           // row bytes dec_src_pkt_info may read (head + size field), if known
     std::vector<UnpackRow> rows;
+    // verdicts: the sessions' own row lists, each with its first group's index in this batch
+    // (placed on the session threads; visited in place, not merged)
+    std::vector<std::pair<const std::vector<UnpackRow>*, int>> segs;
+    template <class F>
+    void for_rows(F&& f) const {
+        for (auto& r : rows) f(r.group, r);
+        for (auto& sg : segs)
+            for (auto& r : *sg.first) f(r.group + sg.second, r);
+    }
     size_t sp = 0, wp = 0;
     // staging (io arena, host and device alike): offsets and lengths in, results out
     size_t o_off = 0, o_len = 0, o_rx = 0, o_st = 0, o_ps = 0, o_hsh = 0;
@@ -412,7 +421,7 @@ struct UnpackBatch {
 void unpack_layout(UnpackBatch& b, Stage& io, Stage& work) {
     const size_t G = (size_t)b.groups, R = G * b.n;
     size_t maxd = 16;
-    for (auto& r : b.rows) maxd = std::max(maxd, (size_t)r.len + (b.wrap ? 11u : 0u));
+    b.for_rows([&](int, const UnpackRow& r) { maxd = std::max(maxd, (size_t)r.len + (b.wrap ? 11u : 0u)); });
     b.sp = round16(std::max(maxd, std::min(b.need, (size_t)b.dec_pkt_size + 4)));
     b.wp = round16(b.sp + 13);
     b.o_off = io.take(R * 8);
@@ -441,11 +450,11 @@ int run_unpack(qfec_zfec* z, UnpackBatch& b, const uint8_t* d_rx, hipStream_t s)
     int* len = reinterpret_cast<int*>(h + b.o_len);
     memset(off, 0, R * 8);
     memset(len, 0, R * 4);
-    for (auto& r : b.rows) {
-        const size_t i = (size_t)r.group * b.n + r.ik;
+    b.for_rows([&](int g, const UnpackRow& r) {
+        const size_t i = (size_t)g * b.n + r.ik;
         off[i] = r.off;
         len[i] = (int)r.len;
-    }
+    });
     if (hipMemcpyAsync(d + b.o_off, h + b.o_off, b.o_rx - b.o_off, hipMemcpyHostToDevice, s) != hipSuccess)
         return QFEC_EHIP;
     int rc = qfec_gather_rows(d_rx, reinterpret_cast<const unsigned long long*>(d + b.o_off),
@@ -1063,6 +1072,8 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
             }
         if (any_pack && TXA.used && z->d_tx.ensure(TXA.used + 16) == QFEC_OK)
             tx_staged = hipMemcpyAsync(z->d_tx.d, TXA.h, TXA.used + 16, hipMemcpyHostToDevice, st) == hipSuccess;
+        // (copying the arena to the device while the input calls still fill it, 16 MiB at a time,
+        // moved the time into the input calls instead: slower overall, profiles/r05l)
         if (any_unpack && RXA.used && z->d_rx.ensure(RXA.used + 16) == QFEC_OK)
             rx_staged = hipMemcpyAsync(z->d_rx.d, RXA.h, RXA.used + 16, hipMemcpyHostToDevice, st) == hipSuccess;
         (void)hipGetLastError();
@@ -1179,19 +1190,20 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
     // ---- receive: verdicts of this flush's FEC datagrams (pseudo-groups by (k, n, tag, dec_pkt_size))
     std::vector<std::vector<Verdict>> verd(NS);
     std::vector<UnpackBatch> vb;
+    using Key = std::tuple<int, int, int, int>;
+    struct Local {
+        Key key;
+        int groups = 0;
+        size_t need = 0;
+        std::vector<UnpackRow> rows;
+        std::vector<uint16_t> taken;  // per group: bit ik
+    };
+    std::vector<std::vector<Local>> loc;  // (the batches visit their rows in place: kept to the verdicts)
     {
         // per session (on the session threads): its rows placed into pseudo-groups of its own
         // batches; then the sessions' batches are concatenated per key in session order (any
         // placement is valid: a row's verdict is its own)
-        using Key = std::tuple<int, int, int, int>;
-        struct Local {
-            Key key;
-            int groups = 0;
-            size_t need = 0;
-            std::vector<UnpackRow> rows;
-            std::vector<uint16_t> taken;  // per group: bit ik
-        };
-        std::vector<std::vector<Local>> loc(NS);
+        loc.assign(NS, {});
         parallel_for(z, NS, threads, [&](size_t si) {
             Session& S = z->sessions[si];
             std::vector<Local> L;  // (local vectors: see the receive machines)
@@ -1250,8 +1262,9 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
             L.swap(loc[si]);
         });
         std::map<Key, int> vb_of;
-        std::vector<std::pair<int, int>> where;  // local batch -> (batch, group offset)
+        std::vector<std::vector<std::pair<int, int>>> where_s(NS);  // local batch -> (batch, group offset)
         for (size_t si = 0; si < NS; ++si) {
+            auto& where = where_s[si];
             where.assign(loc[si].size(), std::make_pair(0, 0));
             for (size_t x = 0; x < loc[si].size(); ++x) {
                 Local& lb = loc[si][x];
@@ -1274,18 +1287,17 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
                 where[x] = std::make_pair(bi, goff);
                 b.groups += lb.groups;
                 b.need = std::max(b.need, lb.need);
-                if (goff == 0 && b.rows.empty()) {
-                    b.rows.swap(lb.rows);
-                } else {
-                    for (auto& r : lb.rows) b.rows.push_back(UnpackRow{r.group + goff, r.ik, r.off, r.len});
-                }
+                b.segs.emplace_back(&lb.rows, goff);
             }
+        }
+        parallel_for(z, NS, threads, [&](size_t si) {
+            const auto& where = where_s[si];
             for (auto& v : verd[si])
                 if (v.batch >= 0) {
                     v.group += where[(size_t)v.batch].second;
                     v.batch = where[(size_t)v.batch].first;
                 }
-        }
+        });
     }
     phase("rx grouping");
     // the receive arena's bytes on the device once: verdict and decode launches gather from it
@@ -1557,6 +1569,7 @@ int flush_body(qfec_zfec* z, qfec_pack_output_fn pack_out, qfec_unpack_output_fn
         std::vector<Emit>().swap(rx_out[si]);
         std::vector<Emit>().swap(tx_out[si]);
         std::vector<Verdict>().swap(verd[si]);
+        if (si < loc.size()) std::vector<Local>().swap(loc[si]);
     });
     // ---- what the state still refers to moves to the spare arenas: the window slots'
     // datagrams and the open send groups' payloads; everything else is dropped

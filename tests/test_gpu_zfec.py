@@ -61,3 +61,21 @@ def test_zfec_forged_check_packets():
     z = qa.Zfec()
     replay(z, scripts, [run_oracle(s) for s in scripts], "one_flush")
     z.close()
+
+
+def test_zfec_rate_tool_large_flush_verified():
+    """A large flush (16 sessions x 3000 datagrams of ~1 KiB, ~50 MB of arena, the threaded
+    session machines): the send flush, the per-datagram input calls and the receive flush; every
+    payload arrives (count, bytes, word sum) and the sampled ones match byte for byte
+    (tools/zfec_rate.py)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "zfec_rate.py"), "--sessions", "16",
+                          "--packets", "3000", "--reps", "2", "--json"], capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["verified"] and res["e2e"]["verified"], res
+    assert res["e2e"]["byte_check"]["mismatched"] == 0 and res["e2e"]["byte_check"]["sampled"] > 0
