@@ -41,6 +41,13 @@
 #include "qfec_device.hpp"
 #include "qfec_internal.hpp"
 
+// QFEC_RX_ABLATE (measurement builds only, tools/rx_stage_ablate.sh; results are wrong in such
+// a build): bit 0 drops the decode MAC, bit 1 the row checksums (byte sums and their totals),
+// bit 2 the row stores, bit 3 the unaligned row loads (rows read at a 16-B-aligned offset).
+// The SQ counters of each build against the full one give the per-stage instruction counts.
+#ifndef QFEC_RX_ABLATE
+#define QFEC_RX_ABLATE 0
+#endif
 namespace qfec {
 
 namespace {
@@ -247,7 +254,8 @@ __device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __r
     for (int c = 0; c < K; ++c) {
 #pragma unroll
         for (int d = 0; d < NV; ++d) x[c].d[d] = 0;
-        if (c < pl.ns && act) load_chunk<NV>(x[c], wire_g + rlane(pl.v_soff, c) + pos);
+        if (c < pl.ns && act)
+            load_chunk<NV>(x[c], wire_g + ((QFEC_RX_ABLATE & 8) ? rlane(pl.v_soff, c) & ~15u : rlane(pl.v_soff, c)) + pos);
     }
     if constexpr (FR) {
 #pragma unroll
@@ -269,19 +277,21 @@ __device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __r
                 }
             }
     }
+    if constexpr (!(QFEC_RX_ABLATE & 2)) {
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-        uint32_t s = dsum[c];
+        for (int c = 0; c < K; ++c) {
+            uint32_t s = dsum[c];
 #pragma unroll
-        for (int d = 0; d < NV; ++d) s = sad(x[c].d[d], s);
-        dsum[c] = s;
+            for (int d = 0; d < NV; ++d) s = sad(x[c].d[d], s);
+            dsum[c] = s;
+        }
     }
     Chunk<NV> acc[E > 0 ? E : 1];
-    if constexpr (E > 0) {
 #pragma unroll
-        for (int j = 0; j < E; ++j)
+    for (int j = 0; j < (E > 0 ? E : 1); ++j)
 #pragma unroll
-            for (int d = 0; d < NV; ++d) acc[j].d[d] = 0;
+        for (int d = 0; d < NV; ++d) acc[j].d[d] = 0;
+    if constexpr (E > 0 && !(QFEC_RX_ABLATE & 1)) {
 #pragma unroll
         for (int c = 0; c < K; ++c) {
             Sel sc[NV];
@@ -311,7 +321,7 @@ __device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __r
 #pragma unroll
         for (int j = 0; j < E; ++j) dw0[j] = rlane(acc[j].d[0], 0);
     }
-    if (act) {
+    if (act && !(QFEC_RX_ABLATE & 4)) {
 #pragma unroll
         for (int c = 0; c < K; ++c) {
             const uint32_t r = rlane(pl.v_srow, c) & 0xFFFFu;
@@ -327,7 +337,7 @@ __device__ __forceinline__ void rx_pass(const Plan<K, M>& pl, const uint8_t* __r
         }
     }
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
+    for (int j = 0; j < ((QFEC_RX_ABLATE & 2) ? 0 : E); ++j) {
         const int hi = head + (int)(dw0[j] & 0xFFFFu);  // payload end of decoded row j
         uint32_t s = psl[j];
         if (pend > hi) {
@@ -558,7 +568,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NV == 4
             for (int c = 0; c < K; ++c) v[c] = dsum[c];
 #pragma unroll
             for (int j = 0; j < M; ++j) v[K + j] = psl[j];
-            totals<K + M>(v, o);
+            if constexpr (QFEC_RX_ABLATE & 2) {
+#pragma unroll
+                for (int i = 0; i < K + M; ++i) o[i] = v[i];
+            } else {
+                totals<K + M>(v, o);
+            }
             uint32_t t = 0;
 #pragma unroll
             for (int i = 0; i < K + M; ++i) t = wlanei(t, i, o[i]);
@@ -583,7 +598,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NV == 4
             if (ln < pl.ns) {
                 bool rb = false, rv = false;
                 if ((summed >> r) & 1u) {
-                    if ((v_dt & 0xFFFFu) != (sr >> 16)) rb = true;
+                    // (ablation builds whose sums are wrong by construction take every row as good)
+                    if (!(QFEC_RX_ABLATE & 10) && (v_dt & 0xFFFFu) != (sr >> 16)) rb = true;
                     else rv = true;
                 }
                 if constexpr (FR) {  // ProtocolUdp::CheckSum over frame bytes 2.. (ProtocolBasic.cpp:80-87)

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build libqfec variants whose receive kernel (k_rx) drops one stage each (QFEC_RX_ABLATE bits,
+# qfec_rx.hip): tools/_abl/libqfec_rx<bits>.so.  Measurement builds only: their outputs are wrong.
+# The SQ counters of each against the full build give the per-stage instruction counts
+# (tools/gpu_r05n.sh).
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p tools/_abl/rxbuild
+C=quicknet_amd/csrc
+for bits in 1 2 4 8; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -DQFEC_RX_ABLATE=$bits \
+    -c $C/qfec_rx.hip -o tools/_abl/rxbuild/qfec_rx_$bits.o &
+done
+wait
+for bits in 1 2 4 8; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-Bsymbolic -o tools/_abl/libqfec_rx$bits.so \
+    $C/build/qfec_kernels.hip.o $C/build/qfec_wire.hip.o $C/build/qfec_percall.hip.o tools/_abl/rxbuild/qfec_rx_$bits.o \
+    $C/build/qfec_runtime.cpp.o $C/build/gf256.cpp.o $C/build/qfec_net.cpp.o $C/build/qfec_zfec.cpp.o $C/build/qfec_pool.cpp.o
+done
+ls -la tools/_abl/libqfec_rx*.so

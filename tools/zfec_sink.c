@@ -72,8 +72,10 @@ static unsigned samp_src[SAMP_MAX], samp_size[SAMP_MAX];
 static unsigned char samp_buf[SAMP_MAX][SAMP_BYTES];
 
 /* receive side without a copy: fold the payload where the layer hands it over */
+static unsigned samp_left;  /* deliveries until the next sample (a countdown: no division per call) */
 int sink_unpack_fold(void *peer, const char *p, unsigned int size, unsigned int src) {
-    if (samp_every && ndeliv % samp_every == 0 && nsamp < SAMP_MAX) {
+    if (samp_every && samp_left-- == 0 && nsamp < SAMP_MAX) {
+        samp_left = samp_every - 1;
         samp_peer[nsamp] = (int)(intptr_t)peer;
         samp_src[nsamp] = src;
         samp_size[nsamp] = size;
@@ -119,24 +121,31 @@ int sink_pack_inputs(void *z, void *fn, const int *sess, int nsess, int packets,
  * negative code */
 long long sink_unpack_inputs(void *z, void *fn, const int *rx_of, int nsess, int nn, int ndrop) {
     unpack_input_fn f = (unpack_input_fn)fn;
-    unsigned long long *cnt = calloc((size_t)nsess, sizeof(unsigned long long));
+    /* per session: position j in its current group of nn and that group's index g mod nn, kept
+     * incrementally (the same drops as sink_pack_forward, without a division per datagram) */
+    int *pos = calloc((size_t)nsess * 2, sizeof(int));
     long long kept = 0;
     for (size_t i = 0; i < n; ++i) {
         const int s = (int)peers[i] - 1;
-        const unsigned long long c = cnt[s]++;
-        const int j = (int)(c % (unsigned long long)nn), g = (int)(c / (unsigned long long)nn);
+        const int j = pos[2 * s], gm = pos[2 * s + 1];
+        if (++pos[2 * s] == nn) {
+            pos[2 * s] = 0;
+            pos[2 * s + 1] = gm + 1 == nn ? 0 : gm + 1;
+        }
         int drop = 0;
-        for (int t = 0; t < ndrop; ++t)
-            if ((g + t) % nn == j) drop = 1;
+        for (int t = 0; t < ndrop; ++t) {
+            const int x = gm + t;
+            if ((x >= nn ? x - nn : x) == j) drop = 1;
+        }
         if (drop) continue;
         const int rc = f(z, rx_of[s], buf + offs[i], lens[i]);
         if (rc < 0) {
-            free(cnt);
+            free(pos);
             return rc;
         }
         ++kept;
     }
-    free(cnt);
+    free(pos);
     return kept;
 }
 
@@ -188,7 +197,7 @@ int sink_unpack(void *peer, const char *p, unsigned int size, unsigned int src) 
 
 unsigned long long sink_fold(const unsigned char *q, unsigned int size) { return fold(q, size); }
 
-void sink_reset(void) { used = n = 0; ndeliv = dbytes = dsum = 0; nsamp = 0; }
+void sink_reset(void) { used = n = 0; ndeliv = dbytes = dsum = 0; nsamp = 0; samp_left = 0; }
 size_t sink_count(void) { return n; }
 const unsigned char *sink_buf(void) { return buf; }
 const uint32_t *sink_offs(void) { return offs; }
