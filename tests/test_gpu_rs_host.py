@@ -297,3 +297,38 @@ def test_rs_host_memory_kinds(oracle, tmp_path, kind):
     assert np.array_equal(np.stack([get(i) for i in range(G * k)]).reshape(G, k, B), exp)
     rs.close()
     del rows, base
+
+
+@pytest.mark.parametrize("zero_copy", [1, 0])
+def test_rs_host_pipeline_quirk_edits(oracle, knobs, zero_copy):
+    """Edited public matrices through the pipelined host path over many chunks: a zero
+    coefficient in column 0 of `rs->parity` leaves that parity row's old bytes in place
+    (rs.c:116-117: the pipeline then stages the parity rows too), and `rs->m` edited so the
+    reconstruct decodes with the edited rows (rs.c:505, 536-556) -- both against the oracle."""
+    knobs("host_zero_copy", zero_copy)
+    knobs("host_chunk", 4)
+    k, m, B, G = 10, 3, 600, 23
+    rs = qa.ReedSolomon(k, m)
+    rows = rs.parity.copy()
+    rows[1, 0] = 0  # parity row 1 keeps its old bytes where column 0 contributes
+    rs.parity[:] = rows
+    data0 = synth_bytes(0xED17, G * k * B).reshape(G, k, B)
+    par0 = synth_bytes(0x0DD, G * m * B).reshape(G, m, B)  # stale parity the quirk keeps
+    par = par0.copy()
+    assert rs.encode(data0, par, B) == 0
+    want = par0.copy()
+    oracle.rs_encode(rows, data0, want, B)
+    assert np.array_equal(par, want)
+    full = rs.m_matrix.copy()
+    full[k + 2, 3] ^= 0x21  # a parity row of the decode matrix edited (the reconstruct reads rs->m)
+    rs.m_matrix[:] = full
+    gm = mixed_marks(G, k, m, 77)
+    marks = marks_to_rs_layout(gm, k)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+    exp = d.copy()
+    rc_o = oracle.rs_reconstruct_full(full, exp, want.copy(), marks, B)
+    rc = rs.reconstruct(d, want.copy(), marks, B)
+    assert rc == rc_o
+    assert np.array_equal(d, exp)
+    rs.close()
