@@ -2170,10 +2170,14 @@ struct MapSnap {
     }
 };
 
+constexpr size_t kMapsMinPointers = 4096;
+
 // number of device pointers among ptrs[0 .. count), classified on the host pool's threads
 size_t count_device_ptrs(unsigned char* const* ptrs, size_t count, HostPool& pool) {
+    // reading the maps costs ~0.1-0.3 ms: worth it for large arrays only; a call with a few
+    // groups probes its pointers directly (a probe per 64 KiB window, ~0.1 us each)
     MapSnap maps;
-    const bool have_maps = maps.load();
+    const bool have_maps = count >= kMapsMinPointers && maps.load();
     std::atomic<size_t> ndev{0};
     pool.run(
         [&](int t, int nt) {
