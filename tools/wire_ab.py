@@ -18,6 +18,16 @@ import quicknet_amd as qa  # noqa: E402
 
 KNOBS = {"wire_fused": 1, "wire_rx": 1}
 
+if os.environ.get("QFEC_LIB"):  # an older build (tools/ab_lib.sh): knobs it predates are skipped
+    _tune = qa.tune
+
+    def _tune_compat(key, value):
+        try:
+            _tune(key, value)
+        except qa.QfecError:
+            pass
+    qa.tune = _tune_compat
+
 
 def main():
     p = argparse.ArgumentParser()
