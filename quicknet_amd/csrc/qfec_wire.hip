@@ -106,7 +106,7 @@ __device__ __forceinline__ uint4 xor16n(uint4 v, uint32_t mm, int n) {
                       v.w ^ (mm & byte_mask(0, n, 3)));
 }
 
-// datagram store: non-temporal or write-back (tuning "wire_store_nt"), wave-uniform flag
+// datagram store: non-temporal or write-back (WireArgs::store_nt), wave-uniform flag
 __device__ __forceinline__ void stw(uint8_t* p, const uint4& v, int nt) {
     if (nt) st16(p, v);
     else st16a(p, v);
@@ -771,7 +771,7 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
 // ------------------------------------------------------------------ send: one wave per group
 // HDR 13 with a 1088-B wire pitch (1 KiB payloads): the body's chunks 4..67 are exactly 64
 // lanes, so with groups wave-aligned each wave holds one whole group and can finish its first
-// 64-B line itself (tuning "wire_send_wave"): wave sums of the body's chunks, then lanes 0..15
+// 64-B line itself: wave sums of the body's chunks, then lanes 0..15
 // take dword i of line 0 of every row -- header, shard bytes 0-3, payload bytes 0..46 and
 // their check bytes (a dword-wide encode) -- and store each row's line 0 as one instruction.
 // This replaces k_pack_line0's scattered second pass (13 lines 1088 B apart per group).
@@ -803,7 +803,7 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
 // first wire_pitch / 16 - 68 lanes.  Row sums accumulate over the passes, so line 0 is
 // unchanged.
 //
-// LW 8 (tuning "wire_send_wave" 3): 8-byte lanes, NP passes over the 8-B chunks 8 .. wire_pitch
+// LW 8 (wire pitches 1104 .. 1600): 8-byte lanes, NP passes over the 8-B chunks 8 .. wire_pitch
 // / 8 - 1 (1088: two full passes; 1472: 64 + 64 + 48 lanes), fewer registers per pass.
 template <int K, int M, int GPW, int FP = 0, int NP = 1, int LW = 16, int WV = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WV ? WV : LW == 8 ? (NP >= 3 ? 4 : 6) : FP ? FRAME_WAVES : 4))) k_pack_wave64(WireArgs a, const uint8_t* __restrict__ payload,
@@ -1128,11 +1128,11 @@ __global__ void __launch_bounds__(256) k_frame_udp(FrameArgs a) {
     }
 }
 
-// k_frame_udp over ROWS rows per wave with every load issued before any use (tuning
-// "frame_rows"): one row per wave keeps ~1 KB in flight per wave, too little to cover the
+// k_frame_udp over ROWS rows per wave with every load issued before any use: one row per wave
+// keeps ~1 KB in flight per wave, too little to cover the
 // memory latency at this kernel's occupancy; ROWS rows put ROWS times as many bytes in flight.
 // Rows of at most 2 048 B (one pass of two 16-B chunks per lane); the host checks.
-// STAGE (frame_rows 2, the default): the ROWS output rows are built in LDS (zeroed first) and stored as one
+// STAGE (the launch uses ROWS 2 with STAGE): the ROWS output rows are built in LDS (zeroed first) and stored as one
 // flat range, so no 64-B line of the output is written in two parts by one wave; rows with
 // out_len -1 then read back zeros instead of being left untouched
 template <int ROWS, bool STAGE = false>
@@ -1298,8 +1298,8 @@ __global__ void __launch_bounds__(256) k_unframe_udp(FrameArgs a) {
     }
 }
 
-// k_unframe_udp over ROWS rows per wave, every load issued before any use (tuning "frame_rows",
-// as k_frame_udp_rows); rows of at most 2 048 B
+// k_unframe_udp over ROWS rows per wave, every load issued before any use (as
+// k_frame_udp_rows); rows of at most 2 048 B
 template <int ROWS>
 __global__ void __launch_bounds__(256) k_unframe_udp_rows(FrameArgs a) {
     const uint64_t row0 = ((uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6)) * ROWS;
@@ -1392,10 +1392,9 @@ hipError_t launch_build_shards(const WireArgs& a, hipStream_t s) {
 }
 
 // the one-wave send's mapping for a wire (or frame) pitch that is the 64-B multiple above the row:
-// 1 one group per wave, one pass (1088 B; tuning "wire_send_wave" 2: any pitch 592..1088);
-// 2 two groups per wave (576 B); 5 one group per wave, two passes (1104..2112 B, "wire_send_wave"
-// 2 only: at 1472 B, RS(10,13) x 100k 1400-B payloads, it ran 841 us against 782 for the body +
-// line-0 pair -- the second pass keeps 24 of 64 lanes busy; profiles/r03_wire/r03n_mtu_ab.txt); 0 none
+// 1 one group per wave, one pass (1088 B); 2 two groups per wave (576 B); 10 one group per wave on
+// 8-B lanes (1104..1600 B); 0 none.  (16-B lanes in two passes above 1088 B, a retired A/B, ran
+// 841 us against 782 for the body + line-0 pair at 1472 B: profiles/r03_wire/r03n_mtu_ab.txt)
 static int send_wave_gpw(uint64_t wire_pitch) {
     // above 1088 B: 8-B lanes in three passes (1472 B, RS(10,13) x 100k: 737 against 781 us for
     // the body + line-0 pair); at 1088 B 16-B lanes, one pass (497 against 545 us on 8-B lanes)
@@ -1409,8 +1408,8 @@ template <int K, int M, int HDR>
 hipError_t pack_fused_shape(const WireArgs& a, const uint32_t* tab, uint32_t* part, hipStream_t s) {
     // body lanes per group cover chunks [TS, tn): the longest datagram the shard pitch allows;
     // groups are packed back to back (no rounding), partial sums go per 16-lane row.
-    // LINE (tuning "wire_line", when the wire pitch is the 64-B multiple just above HDR + shard
-    // pitch): chunks [TS, wire_pitch / 16), so lanes per group is a multiple of 4 and every
+    // LINE (when the wire pitch is the 64-B multiple just above HDR + shard pitch): chunks
+    // [TS, wire_pitch / 16), so lanes per group is a multiple of 4 and every
     // 64-B line of a row is one store instruction (a line written in two parts costs the
     // memory a read-modify-write: tools/wrskel.hip, profiles/r02zn_wrskel.txt)
     const bool line = a.wire_pitch % 64 == 0 &&
