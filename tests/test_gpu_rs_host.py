@@ -334,3 +334,67 @@ def test_rs_host_pipeline_quirk_edits(oracle, knobs, zero_copy):
     assert rc == rc_o
     assert np.array_equal(d, exp)
     rs.close()
+
+
+def _ref_codec():
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    from oracle.oracle import RefCodec
+    if not RefCodec.available():
+        pytest.skip("reference libraries not built (make -C oracle ref)")
+    return RefCodec()
+
+
+@pytest.mark.parametrize("k,m,B,G,edit", [(10, 3, 1000, 61, False), (10, 3, 1024, 40, True), (16, 4, 1400, 37, True),
+                                          (4, 2, 37, 200, True), (20, 5, 256, 50, False), (3, 2, 33, 90, True)])
+def test_rs_host_pipeline_vs_reference_rs(knobs, k, m, B, G, edit):
+    """The pipelined host path against the reference's own module/rs.c (oracle/_ref, compiled from
+    /root/reference) on identical scattered rows: the same public-matrix edits on both handles
+    (a zero column-0 coefficient, an edited row of rs->m), encode, then reconstruct with 0..m+1
+    erasures per group (unrecoverable groups included) -- bytes and return codes equal."""
+    ref = _ref_codec()
+    knobs("host_chunk", 9)
+    n = k + m
+    rng = np.random.default_rng(k * 1000 + B)
+    rows, _keep = scattered_rows(G, n, B, k + B)
+    rrows, _rkeep = scattered_rows(G, n, B, k + B + 1)
+    data0 = synth_bytes(0xC0FFEE + k + B, G * k * B).reshape(G * k, B)
+    par0 = synth_bytes(0xFACADE + m + B, G * m * B).reshape(G * m, B)
+    for i in range(G * k):
+        rows[i][:] = data0[i]
+        rrows[i][:] = data0[i]
+    for i in range(G * m):
+        rows[G * k + i][:] = par0[i]
+        rrows[G * k + i][:] = par0[i]
+    rs = qa.ReedSolomon(k, m)
+    h = ref.rs.reed_solomon_new(k, m)
+    try:
+        if edit:
+            par_ref = np.ctypeslib.as_array(h.contents.parity, shape=(m, k))
+            m_ref = np.ctypeslib.as_array(h.contents.m, shape=(n, k))
+            r = int(rng.integers(0, m))
+            rs.parity[r, 0] = 0
+            par_ref[r, 0] = 0
+            j, c, v = int(rng.integers(0, n)), int(rng.integers(0, k)), int(rng.integers(1, 256))
+            rs.m_matrix[j, c] ^= v
+            m_ref[j, c] ^= v
+        L = qa.lib()
+        ptrs, rptrs = ptr_array(rows), ptr_array(rrows)
+        assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == ref.rs_encode(h, rptrs, G * n, B) == 0
+        assert all(np.array_equal(rows[i], rrows[i]) for i in range(G * n))
+        gm = mixed_marks(G, k, m, k + m + B)
+        marks = marks_to_rs_layout(gm, k)
+        for i in range(G * k):
+            if marks[i]:
+                rows[i][:] = 0x5A
+                rrows[i][:] = 0x5A
+        rc = L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(marks.ctypes.data), G * n, B)
+        rc_ref = ref.rs_reconstruct(h, rptrs, marks, G * n, B)
+        assert rc == rc_ref == -1
+        bad = [i for i in range(G * n) if not np.array_equal(rows[i], rrows[i])]
+        assert not bad, bad[:10]
+    finally:
+        ref.rs.reed_solomon_release(h)
+        rs.close()
