@@ -599,3 +599,50 @@ def _gf_row(oracle, c, row):
     """c * row over GF(2^8) via the oracle's multiplication table (256 products, then a gather)."""
     t = np.array([oracle.mul(c, b) for b in range(256)], np.uint8)
     return t[row]
+
+
+@pytest.mark.parametrize("k,n,sz", [(10, 13, 1028), (4, 6, 100), (16, 20, 4096), (7, 12, 333), (1, 2, 64),
+                                    (128, 256, 96), (200, 255, 40)])
+def test_fec_packets_vs_reference_fec(k, n, sz):
+    """fec_encode / fec_decode of libqfec against the reference's own system/fec.c
+    (oracle/_ref/libref_fec.so) on the same packets: every parity index encoded by both, then
+    decodes from random k-subsets handed over in random order (fec_decode's shuffle moves them
+    into place) -- output packets, index arrays and return codes equal."""
+    import ctypes as C
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.oracle import RefCodec
+    if not RefCodec.available():
+        pytest.skip("reference libraries not built (make -C oracle ref)")
+    ref = RefCodec()
+    L = qa.lib()
+    rng = np.random.default_rng(k * 7 + n + sz)
+    data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    h, hr = L.fec_new(k, n), ref.fec.fec_new(k, n)
+    try:
+        src = (C.c_void_p * k)(*[data[i].ctypes.data for i in range(k)])
+        coded = np.zeros((n, sz), np.uint8)
+        coded[:k] = data
+        for idx in range(k, n):
+            out, outr = np.zeros(sz, np.uint8), np.zeros(sz, np.uint8)
+            L.fec_encode(h, src, out.ctypes.data, idx, sz)
+            ref.fec.fec_encode(hr, src, outr.ctypes.data, idx, sz)
+            assert np.array_equal(out, outr), idx
+            coded[idx] = out
+        for trial in range(6):
+            keep = rng.choice(n, size=k, replace=False)
+            if trial % 2:
+                keep = np.sort(keep)
+            bufs = [coded[keep].copy(), coded[keep].copy()]
+            idxs = [np.ascontiguousarray(keep, dtype=np.int32), np.ascontiguousarray(keep, dtype=np.int32)]
+            rcs = []
+            for (b, ix, fn, hh) in ((bufs[0], idxs[0], L.fec_decode, h), (bufs[1], idxs[1], ref.fec.fec_decode, hr)):
+                pk = (C.c_void_p * k)(*[b[i].ctypes.data for i in range(k)])
+                rcs.append(fn(hh, pk, ix.ctypes.data_as(C.POINTER(C.c_int)), sz))
+            assert rcs[0] == rcs[1] == 0
+            assert np.array_equal(idxs[0], idxs[1])
+            assert np.array_equal(bufs[0], bufs[1])
+    finally:
+        L.fec_free(h)
+        ref.fec.fec_free(hr)
