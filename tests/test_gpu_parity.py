@@ -499,3 +499,51 @@ def test_rs_edits_vs_golden(golden, name, path):
     assert rc == z[f"rc_{name}"][0]
     assert rs_edit_match(z, f"out_{name}", out)
     rs.close()
+
+
+@pytest.mark.parametrize("k,m,B,G", [(10, 3, 1024, 5000), (16, 4, 1400, 2000), (4, 2, 1024, 5000), (12, 4, 333, 3000)])
+def test_batched_vs_reference_rs_live(k, m, B, G):
+    """The batched device path (qfec_encode / qfec_reconstruct on HBM-resident batches, the
+    kernels the bench times) against the reference's own module/rs.c (oracle/_ref/libref_rs.so)
+    on the same bytes: encode, then reconstruct with 0..m+1 erasures per group (unrecoverable
+    groups included) over inconsistent parity -- every byte and the failed-group count equal."""
+    import ctypes as C
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle.oracle import RefCodec
+    if not RefCodec.available():
+        pytest.skip("reference libraries not built (make -C oracle ref)")
+    ref = RefCodec()
+    n = k + m
+    rng = np.random.default_rng(k * 31 + B)
+    data = synth_bytes(0xA5A5 + k + B, G * k * B).reshape(G, k, B)
+    code = qa.Code.cauchy(k, m)
+    dd, pd = to_dev(data), torch.zeros((G, m, B), dtype=torch.uint8, device=DEV)
+    code.encode(dd, pd, B)
+    torch.cuda.synchronize()
+    par_ref = np.zeros((G, m, B), np.uint8)
+    h = ref.rs.reed_solomon_new(k, m)
+    try:
+        rdata = data.copy()
+        assert ref.rs_encode(h, ref.shard_ptrs(rdata, par_ref), G * n, B) == 0
+        assert np.array_equal(pd.cpu().numpy(), par_ref)
+        gm = np.zeros((G, n), np.uint8)
+        for g in range(G):
+            gm[g, rng.choice(n, size=int(rng.integers(0, m + 2)), replace=False)] = 1
+        marks = marks_to_rs_layout(gm, k)
+        damaged = data.copy()
+        damaged.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+        par_in = synth_bytes(0x77 + B, G * m * B).reshape(G, m, B)  # inconsistent parity: pins the survivor rule
+        ddev = to_dev(damaged)
+        failed = torch.zeros(1, dtype=torch.int32, device=DEV)
+        code.reconstruct(ddev, to_dev(par_in), to_dev(marks), B, failed)
+        torch.cuda.synchronize()
+        rd, rp = damaged.copy(), par_in.copy()
+        rc = ref.rs_reconstruct(h, ref.shard_ptrs(rd, rp), marks, G * n, B)
+        assert np.array_equal(ddev.cpu().numpy(), rd)
+        unrecoverable = int(((gm[:, :k].sum(1) > 0) & (gm.sum(1) > m)).sum())
+        assert int(failed.item()) == unrecoverable
+        assert rc == (-1 if unrecoverable else 0)
+    finally:
+        ref.rs.reed_solomon_release(h)
