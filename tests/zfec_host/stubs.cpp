@@ -179,6 +179,8 @@ hipError_t hipHostFree(void* p) {
     free(p);
     return hipSuccess;
 }
+hipError_t hipHostRegister(void*, size_t, unsigned int) { return hipSuccess; }
+hipError_t hipHostUnregister(void*) { return hipSuccess; }
 hipError_t hipGetLastError(void) { return hipSuccess; }
 hipError_t hipGetDevice(int* d) {
     *d = 0;
