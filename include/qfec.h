@@ -233,7 +233,9 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
 /* Knobs.  Integration settings: host chunking, host copy threads, zero copy, the per-call
  * server's footprint.  Plus one A/B switch per kernel family (tools/ab.py, tools/wire_ab.py)
  * and one test hook.  Defaults are the measured best; outputs are identical either way.
- *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies
+ *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies (module/rs.h on host
+ *                      pointers: the reconstruct only; its encode always stages through the device,
+ *                      measured faster for a freshly gathered slot)
  *   "host_chunk"       groups per staged host chunk (0: by bytes: ~32 MiB for qfec_*_host, ~16 MiB of
  *                      caller shards for module/rs.h on host pointers)
  *   "host_threads"     host threads that gather / scatter module/rs.h host shard pointers (0: the

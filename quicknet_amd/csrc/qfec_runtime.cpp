@@ -2190,7 +2190,11 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
     int rc = QFEC_OK;
     for (auto& h : ctx.host)
         if ((rc = ensure_host_slot(h, slot_bytes, 16))) return rc;
-    const bool zc = tuning().host_zero_copy != 0;
+    // staged: the DMA engines move the slot to the device and the parity back.  Reading the
+    // freshly gathered slot in place over PCIe ran slower for the encode (26.4-26.9 against
+    // 28.3-38.8 GiB/s in alternating processes, profiles/r05af); the reconstruct, which reads only
+    // the survivors it needs and writes only the erased rows, stays in place (host_zero_copy)
+    const bool zc = false;
     RsTrace tr;
     long long pending[2] = {-1, -1};
     auto rows_job = [&](size_t nrows, const std::function<void(size_t)>& row) {
