@@ -560,9 +560,15 @@ __global__ void __launch_bounds__(256) k_probe_xor(EncodeArgs a) {
     const uint8_t* src = a.data + g * a.dgs + (uint64_t)col * 16u;
     uint8_t* dst = a.parity + g * a.pgs + (uint64_t)col * 16u;
     uint4 acc = make_uint4(0, 0, 0, 0);
-    for (int c = 0; c < a.k; ++c) {
-        const uint4 v = ld16(src + (uint64_t)c * a.pitch);
-        acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+    // up to 16 rows in flight per lane, as the encode has them (a load-then-XOR loop would keep one)
+    for (int c0 = 0; c0 < a.k; c0 += 16) {
+        uint4 v[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+            if (c0 + c < a.k) v[c] = ld16(src + (uint64_t)(c0 + c) * a.pitch);
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+            if (c0 + c < a.k) { acc.x ^= v[c].x; acc.y ^= v[c].y; acc.z ^= v[c].z; acc.w ^= v[c].w; }
     }
     for (int r = 0; r < a.m; ++r) {
         st16(dst + (uint64_t)r * a.pitch, acc);
@@ -579,13 +585,36 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
 // auto (encode_impl -1): inputs in halves for k >= 16, where all k inputs in registers cap the
 // kernel at 4 waves per SIMD (RS(16,4) B=1400: 1 202 against 1 244 us, 0.98 of the XOR probe;
 // RS(10,3) equal within 1 %, profiles/r04c/)
+//
+// Resident waves (tuning "encode_lds" -1, auto): a dynamic LDS allocation per 256-thread block,
+// out of the CU's 160 KiB, holds the blocks per CU below what the registers allow.  Fewer
+// concurrent row streams per CU move more bytes per second through HBM (tools/occ_probe.hip: an
+// XOR stream of the 10:3 shape at 16 -> 5 waves per CU, 6.03 -> 6.36 TB/s); interleaved A/B of
+// the encode on four boxes (profiles/r05ak, r05al, r05am, r05an2):
+//   all k inputs in registers (impl 0), k = 10, rows >= 512 B: 2 blocks = 8 waves per CU
+//                                                 RS(10,3) B=512/1024/1400 +2-5 %
+//   inputs in halves (impl 2), rows <= 1 KiB:   6 blocks = 24 waves per CU  RS(16,4), RS(20,4) B=1024 +1-4 %
+//   otherwise, k >= 3:                          4 blocks = 16 waves per CU  RS(3,2), (4,2), (5,3), (6,2),
+//                                                 (8,4), (12,4), RS(16,4) B=1400 +1-5 %, RS(10,3) B=64 equal
+//   k <= 2: none (RS(2,1) 2 % slower capped)
+// Launches under 4 096 blocks (four rounds of the chip) keep every slot.  The reconstruct and the
+// datagram kernels lose with any cap (profiles/r05ak, r05al) and have none.
+static inline size_t enc_lds(const EncodeArgs& a, int K, int im, unsigned grid) {
+    if (a.lds >= 0) return (size_t)a.lds;
+    if (grid < 4096 || K <= 2) return 0;
+    if (im == 0 && K == 10) return a.cols >= 32 ? 65536 : 40960;
+    if (im == 2 && a.cols <= 64) return 27000;
+    return 40960;
+}
+
 #define QFEC_ENC_CASE(KK, MM)                                                                 \
     if (a.k == KK && a.m == MM) {                                                             \
         const int im = a.impl < 0 ? (KK >= 16 ? 2 : 0) : a.impl;                              \
+        const size_t lds = enc_lds(a, KK, im, grid);                                          \
         if (im == 2)                                                                          \
-            hipLaunchKernelGGL((k_encode_perm_halves<KK, MM>), dim3(grid), dim3(256), 0, stream, a); \
+            hipLaunchKernelGGL((k_encode_perm_halves<KK, MM>), dim3(grid), dim3(256), lds, stream, a); \
         else                                                                                  \
-            hipLaunchKernelGGL((k_encode_perm<KK, MM>), dim3(grid), dim3(256), 0, stream, a);  \
+            hipLaunchKernelGGL((k_encode_perm<KK, MM>), dim3(grid), dim3(256), lds, stream, a);  \
         return hipGetLastError();                                                             \
     }
 
@@ -684,6 +713,11 @@ hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream) {
     QFEC_REC_CASE(3, 2)
     QFEC_REC_CASE(8, 4)
     QFEC_REC_CASE(12, 4)
+    QFEC_REC_CASE(5, 3)
+    QFEC_REC_CASE(6, 2)
+    QFEC_REC_CASE(7, 1)
+    QFEC_REC_CASE(8, 2)
+    QFEC_REC_CASE(20, 4)
     hipLaunchKernelGGL((k_reconstruct_any<true>), dim3(grid), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
@@ -697,7 +731,10 @@ hipError_t launch_synth_fill(uint8_t* p, uint64_t nbytes, uint64_t seed, hipStre
 
 hipError_t launch_probe_xor(const EncodeArgs& a, hipStream_t stream) {
     if (a.work == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_probe_xor, dim3(grid_for(a.work, 256)), dim3(256), 0, stream, a);
+    // the ceiling of the shape, so at the residency the encode of that k runs with
+    const unsigned grid = grid_for(a.work, 256);
+    const size_t lds = enc_lds(a, a.k, 0, grid);
+    hipLaunchKernelGGL(k_probe_xor, dim3(grid), dim3(256), lds, stream, a);
     return hipGetLastError();
 }
 

@@ -731,7 +731,7 @@ bool vec16_ok(const void* a, const void* b, int block, long long pitch) {
 // launch encode over `groups` groups with tables `tab` covering `m` rows
 int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, const uint8_t* d_data,
                uint8_t* d_par, long long groups, int block, long long pitch, hipStream_t s,
-               long long dgs = -1, long long pgs = -1) {
+               long long dgs = -1, long long pgs = -1, bool host_mem = false) {
     EncodeArgs a{};
     a.tab = tab;
     a.gf_exp = ctx.d_gf;
@@ -741,6 +741,9 @@ int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, cons
     a.pitch = (uint64_t)pitch;
     a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
     a.impl = tuning().encode_impl;
+    // a cap on resident waves pays in HBM (qfec_kernels.hip launch_encode), not over PCIe, where
+    // latency wants every wave the registers allow
+    a.lds = host_mem ? 0 : tuning().encode_lds.load();
     a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
     a.cols_div = make_div_magic(a.cols);
     a.dgs = dgs >= 0 ? (uint64_t)dgs : (uint64_t)c->k * pitch;
@@ -959,6 +962,7 @@ const std::vector<Knob>& knob_table() {
         {"percall_timeout_us", &g_percall_timeout_us, 0, 0x7FFFFFFF},
         {"percall_idle_us", &g_percall_idle_us, 0, 1000000},
         {"percall_resident", &g_percall_resident, 0, 1},
+        {"encode_lds", &tuning().encode_lds, -1, 163840},
     };
     return t;
 }
@@ -1130,7 +1134,7 @@ int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char
         // zero copy: one launch reads the data and writes the parity in host memory
         if ((rc = ensure_host_slot(ctx->host[0], 0, 0))) return rc;
         hipStream_t st = ctx->host[0].stream;
-        rc = run_encode(*ctx, code, tab, m, z_in, z_out, groups, block_size, pitch, st);
+        rc = run_encode(*ctx, code, tab, m, z_in, z_out, groups, block_size, pitch, st, -1, -1, true);
         const hipError_t e = hipStreamSynchronize(st);
         if (!rc && e != hipSuccess) rc = hip_fail(e, "qfec_encode_host: zero-copy encode");
         return rc;
@@ -1367,6 +1371,7 @@ int qfec_probe_stream(const unsigned char* d_data, unsigned char* d_parity, long
     a.work = (uint64_t)groups * a.cols;
     a.dgs = (uint64_t)k * pitch;
     a.pgs = (uint64_t)m * pitch;
+    a.lds = tuning().encode_lds.load();
     if (a.work >= 0x80000000ull) return QFEC_EINVAL;
     hipError_t e = launch_probe_xor(a, (hipStream_t)stream);
     return e == hipSuccess ? QFEC_OK : hip_fail(e, "probe launch");
@@ -1550,7 +1555,7 @@ int qfec_pipe_encode(qfec_pipe* p, qfec_code* code, const unsigned char* h_data,
             // zero copy: the piece's kernel reads and writes the pinned host buffers directly
             s->busy = true;
             if ((rc = run_encode(*s->ctx, code, tab, m, z_in + (size_t)g0 * in_g, z_out + (size_t)g0 * out_g, gn,
-                                 block_size, pitch, s->stream)))
+                                 block_size, pitch, s->stream, -1, -1, true)))
                 break;
             if (hipEventRecord(s->done, s->stream) != hipSuccess) { rc = hip_fail(hipGetLastError(), "event"); break; }
             continue;

@@ -217,7 +217,8 @@ def test_fec_decode_vs_golden(golden, k, n):
 @pytest.mark.parametrize("flavour", ["cauchy", "vandermonde"])
 @pytest.mark.parametrize("k,m,B", [(5, 2, 1024), (32, 8, 256), (20, 4, 1400), (9, 5, 100), (12, 4, 1024)])
 def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
-    """Shapes without a templated kernel (runtime k, m loops) and LUT-sized reconstruct."""
+    """Shapes without a templated kernel ((5,2), (9,5): runtime k, m loops), n > 24 ((32,8): host
+    decode records) and templated shapes through the same calls."""
     G = 33
     code = getattr(qa.Code, flavour)(k, m)
     rows = code.rows
@@ -253,7 +254,8 @@ def test_generic_shapes_vs_oracle(oracle, flavour, k, m, B):
 
 @pytest.mark.parametrize("impl", [-1, 2, 3, 4, 8])
 @pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (4, 2, 100), (12, 4, 40), (3, 2, 1400),
-                                   (10, 3, 1400), (4, 2, 1012), (16, 4, 1024), (12, 4, 1400), (8, 4, 1024)])
+                                   (10, 3, 1400), (4, 2, 1012), (16, 4, 1024), (12, 4, 1400), (8, 4, 1024),
+                                   (5, 3, 1024), (6, 2, 1400), (7, 1, 1024), (8, 2, 200), (20, 4, 1400), (20, 4, 100)])
 def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
     """Every LUT reconstruct body (-1 = the auto choice; exact-e rows on 16-B, 8-B and 12-B
     lanes, the 8-B body one group per block), the coefficient tables read from the 256-entry
@@ -310,6 +312,36 @@ def test_encode_impls_vs_oracle(oracle, impl, flavour, k, m, B):
         torch.cuda.synchronize()
     finally:
         qa.tune("encode_impl", -1)
+    assert np.array_equal(p.cpu().numpy()[..., :B], expect)
+
+
+_RESID_EXPECT = {}
+
+
+@pytest.mark.parametrize("lds", [-1, 0, 40960, 65536, 163840])
+@pytest.mark.parametrize("k,m,B,G", [(10, 3, 1024, 20000), (16, 4, 1400, 12000), (16, 4, 1024, 17000),
+                                     (4, 2, 1024, 20000), (3, 2, 512, 40000)])
+def test_encode_residency_caps_vs_oracle(oracle, lds, k, m, B, G):
+    """The encode's residency cap (tuning "encode_lds": -1 auto, 0 none, else LDS bytes per block)
+    changes only how many waves share a CU: outputs equal the oracle's at every setting, on
+    launches large enough (>= 4 096 blocks) for the auto rule to apply."""
+    assert G * round16(B) // 16 >= 4096 * 256
+    code = qa.Code.cauchy(k, m)
+    key = (k, m, B, G)
+    if key not in _RESID_EXPECT:
+        data = synth_bytes(k * 41 + B, G * k * B).reshape(G, k, B)
+        expect = np.zeros((G, m, B), np.uint8)
+        oracle.rs_encode(code.rows, data, expect, B)
+        _RESID_EXPECT.clear()
+        _RESID_EXPECT[key] = (to_dev(padded(data, round16(B), 0xC3)), expect)
+    d, expect = _RESID_EXPECT[key]
+    p = torch.full((G, m, round16(B)), 0x5A, dtype=torch.uint8, device=DEV)
+    qa.tune("encode_lds", lds)
+    try:
+        code.encode(d, p, B)
+        torch.cuda.synchronize()
+    finally:
+        qa.tune("encode_lds", -1)
     assert np.array_equal(p.cpu().numpy()[..., :B], expect)
 
 
