@@ -258,10 +258,11 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *                      pinned staging | 0 the staged DMA path (the one device-pointer packets take)
  *   "encode_lds"       -1 auto | 0 none | N: bytes of LDS each 256-thread encode block allocates (and
  *                      does not use), of the CU's 160 KiB: a cap on the encode's resident waves per CU.
- *                      Auto caps device-resident launches of >= 4 096 blocks at 8 waves per CU for
- *                      k = 10, 24 for the two-half inputs on rows <= 1 KiB, else 16 (fewer concurrent
- *                      row streams move more bytes per second through HBM); encodes of host memory
- *                      are never capped.  The XOR probe follows the same rule for its k
+ *                      Auto caps device-resident launches of >= 8 192 blocks at 16 waves per CU, 24
+ *                      for the two-half inputs on rows <= 1 KiB, 8 for k = 10 from 16 384 blocks
+ *                      (fewer concurrent row streams move more bytes per second through HBM); k <= 2
+ *                      and encodes of host memory are never capped.  The XOR probe follows the same
+ *                      rule for its k
  * A/B, one per kernel family:
  *   "encode_impl"      -1 auto (2 for k >= 16, else 0) | 0 all rows | 2 all rows, the inputs loaded in
  *                      two halves (fewer registers, more waves per SIMD)

@@ -591,18 +591,21 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
 // concurrent row streams per CU move more bytes per second through HBM (tools/occ_probe.hip: an
 // XOR stream of the 10:3 shape at 16 -> 5 waves per CU, 6.03 -> 6.36 TB/s); interleaved A/B of
 // the encode on four boxes (profiles/r05ak, r05al, r05am, r05an2):
-//   all k inputs in registers (impl 0), k = 10, rows >= 512 B: 2 blocks = 8 waves per CU
-//                                                 RS(10,3) B=512/1024/1400 +2-5 %
+//   all k inputs in registers (impl 0), k = 10, rows >= 512 B, >= 16 384 blocks: 2 blocks = 8 waves
+//                                                 per CU  RS(10,3) B=512/1024/1400 +2-5 % at 100 000
+//                                                 groups, +0.7 % at 50 000, -4 % / -7 % at 25 000 /
+//                                                 17 000 (the last round of blocks runs half empty)
 //   inputs in halves (impl 2), rows <= 1 KiB:   6 blocks = 24 waves per CU  RS(16,4), RS(20,4) B=1024 +1-4 %
 //   otherwise, k >= 3:                          4 blocks = 16 waves per CU  RS(3,2), (4,2), (5,3), (6,2),
 //                                                 (8,4), (12,4), RS(16,4) B=1400 +1-5 %, RS(10,3) B=64 equal
 //   k <= 2: none (RS(2,1) 2 % slower capped)
-// Launches under 4 096 blocks (four rounds of the chip) keep every slot.  The reconstruct and the
+// Launches under 8 192 blocks keep every slot (RS(16,4) B=1400 at 31 250 groups, config 4's share
+// of 8 ranks, 10 742 blocks: +4 %, profiles/r05ap).  The reconstruct and the
 // datagram kernels lose with any cap (profiles/r05ak, r05al) and have none.
 static inline size_t enc_lds(const EncodeArgs& a, int K, int im, unsigned grid) {
     if (a.lds >= 0) return (size_t)a.lds;
-    if (grid < 4096 || K <= 2) return 0;
-    if (im == 0 && K == 10) return a.cols >= 32 ? 65536 : 40960;
+    if (grid < 8192 || K <= 2) return 0;
+    if (im == 0 && K == 10) return a.cols >= 32 && grid >= 16384 ? 65536 : 40960;
     if (im == 2 && a.cols <= 64) return 27000;
     return 40960;
 }

@@ -49,16 +49,16 @@ def main():
     p.add_argument("--rounds", type=int, default=8)
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--lds", default=",".join(map(str, LDS)))
-    p.add_argument("--shapes", default="10,3,1024;16,4,1400", help="k,m,B;... (groups sized to ~1.3 GB)")
+    p.add_argument("--shapes", default="10,3,1024;16,4,1400", help="k,m,B[,groups];... (groups default: the bench's, else ~1.3 GB)")
     p.add_argument("--encode-only", action="store_true")
     p.add_argument("--probe", action="store_true", help="time the XOR probe of each shape too")
     a = p.parse_args()
     ldss = [int(x) for x in a.lds.split(",")]
     shapes = {}
     for i, sh in enumerate(a.shapes.split(";")):
-        k, m, B = (int(x) for x in sh.split(","))
-        G = 250_000 if (k, m, B) == (16, 4, 1400) else 100_000 if (k, m, B) == (10, 3, 1024) else int(1.3e9 // ((k + m) * B))
-        shapes[f"RS({k},{m}) B={B}"] = shape(k, m, B, G, m, 0x5EED0002 + 16 * i)
+        k, m, B, *g = (int(x) for x in sh.split(","))
+        G = g[0] if g else 250_000 if (k, m, B) == (16, 4, 1400) else 100_000 if (k, m, B) == (10, 3, 1024) else int(1.3e9 // ((k + m) * B))
+        shapes[f"RS({k},{m}) B={B} G={G}"] = shape(k, m, B, G, m, 0x5EED0002 + 16 * i)
     s = torch.cuda.current_stream()
     times = {}
     for r in range(a.rounds):
