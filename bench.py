@@ -608,6 +608,29 @@ def side_config(flavour, k, m, B, G, E, rank, steps=20, warmup=5, spinup_ms=25.0
 CONFIG4 = dict(k=16, m=4, B=1400, E=4)
 
 
+def skeleton_ratio(data, parity, marks, B, dec_ms, reps=10):
+    """The reconstruct against its own memory skeleton (qfec_probe_reconstruct: the auto body's
+    mapping, marks reads, survivor rows and erased-row writes, XOR in place of the decode; RS(10,3)
+    and RS(16,4) only), timed on a copy of the batch right here: frac_of_skeleton = skeleton time /
+    reconstruct time, i.e. how close the reconstruct runs to the ceiling of its access pattern."""
+    try:
+        skel = data.clone()
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(3):
+            qa.probe_reconstruct(skel, parity, marks, B)
+        e0.record(s)
+        for _ in range(reps):
+            qa.probe_reconstruct(skel, parity, marks, B)
+        e1.record(s)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        del skel
+        return {"skeleton_avg_ms": round(ms, 4), "frac_of_skeleton": round(ms / dec_ms, 4)}
+    except qa.QfecError as exc:  # a shape without a skeleton instance
+        return {"skeleton_avg_ms": None, "skeleton_error": str(exc)}
+
+
 def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=25.0):
     """BASELINE configs[3]: RS(16,4) encode + decode of 4 000 000 x 1400 B packets = 250 000
     groups, split contiguously over the ranks (quicknet_amd.sharding.shard_range; groups are
@@ -655,6 +678,7 @@ def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=2
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     ok = bool(torch.equal(work[..., :B], data[..., :B]))
     ok = all_sum(0.0 if ok else 1.0, world) == 0.0
+    skel = skeleton_ratio(data, parity, marks, B, dec_ms) if rank == 0 else {}
     bytes_rank = (G + dec_groups) * k * B * steps
     total = all_sum(float(bytes_rank), world)
     per_rank_ms = all_gather_float(el_rank / steps * 1e3, world, rank)
@@ -668,6 +692,17 @@ def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=2
            "rank0_reconstruct_frac": round(dec_alg / (dec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "rank0_encode_avg_ms": round(enc_ms, 4), "rank0_reconstruct_avg_ms": round(dec_ms, 4),
            "verified": ok}
+    if rank == 0:
+        out["rank0_reconstruct_skeleton"] = skel
+        # PMC traffic of this rank's launches (tools/pmc_traffic.py --erasures 4, the same shape and
+        # group count through bench.py's headline leg; keyed by the rank's group count)
+        tr, src = load_traffic(TRAFFIC_PATH, f"rs{k}_{m}_b{B}_g{G}_e{E}")
+        if isinstance(tr, dict):
+            et, dt = tr.get("encode_bytes_per_launch"), tr.get("reconstruct_bytes_per_launch")
+            out["rank0_traffic"] = {"encode_bytes_per_launch": et, "reconstruct_bytes_per_launch": dt,
+                                    "encode_traffic_over_alg": round(et / enc_alg, 4) if et else None,
+                                    "reconstruct_traffic_over_alg": round(dt / dec_alg, 4) if dt else None}
+        out["rank0_traffic_source"] = src
     del data, parity, work, marks
     torch.cuda.empty_cache()
     return out
@@ -1052,6 +1087,7 @@ def main(argv=None):
         probe_gbs = enc_alg / (probe_ms * 1e-3) / 1e9
         for r in (r_enc, r_dec):
             r["frac_of_probe"] = round(r["achieved"] / probe_gbs, 4)
+        r_dec.update(skeleton_ratio(data, parity, marks, B, dec_ms))
         cdst = torch.empty_like(data)
         for _ in range(3):
             cdst.copy_(data)

@@ -230,6 +230,14 @@ int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long s
 int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long long groups, int k, int m,
                       int block_size, long long pitch, void *stream);
 
+/* Calibration probe, NOT a codec: the reconstruct's memory skeleton for RS(10,3) and RS(16,4) --
+ * the same mapping, marks reads, survivor rows and erased-row writes as the auto reconstruct body,
+ * XOR in place of the decode (the erased rows receive garbage; no other byte is written).
+ * lds_cap: LDS bytes per block (0 none), a residency cap.  QFEC_EUNSUP for other shapes. */
+int qfec_probe_reconstruct(unsigned char *d_data, const unsigned char *d_parity, const unsigned char *d_marks,
+                           long long groups, int k, int m, int block_size, long long pitch, int lds_cap,
+                           void *stream);
+
 /* Knobs.  Integration settings: host chunking, host copy threads, zero copy, the per-call
  * server's footprint.  Plus one A/B switch per kernel family (tools/ab.py, tools/wire_ab.py)
  * and one test hook.  Defaults are the measured best; outputs are identical either way.
@@ -250,10 +258,13 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *                      is resident waits for it: at most this long after the last call.
  *   "percall_timeout_us" how long a call spins for the server before it stops the block and waits
  *                      for it (the block serves the pending request first), or, if the request was
- *                      never taken, runs it through one launch (default 2 000 000).  The wait after
- *                      the timeout is NOT bounded: it lasts until the block gets a CU and exits (a
- *                      device whose every CU is held by other persistent kernels keeps the call
- *                      waiting)
+ *                      never taken, runs it through one launch (default 2 000 000)
+ *   "percall_stop_us"  how long that wait for the stopped block may last (default 2 000 000).  A
+ *                      block still not done then (every CU held by other persistent kernels) is
+ *                      abandoned: the call fails -- fec_encode prints to stderr and leaves dst as it
+ *                      was, fec_decode returns 1 (module/fec.c's own failure shapes, fec.c:730-732,
+ *                      833-836) -- and the device takes the one-launch path until percall_resident
+ *                      is set to 1 again (the abandoned block's buffers stay allocated)
  *   "percall_fast"     1 per-packet calls on host packets through the server / one launch on mapped
  *                      pinned staging | 0 the staged DMA path (the one device-pointer packets take)
  *   "encode_lds"       -1 auto | 0 none | N: bytes of LDS each 256-thread encode block allocates (and
@@ -277,7 +288,8 @@ int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long
  *                      every input byte are unchanged | 0 one request per index
  * Test hook:
  *   "percall_fault"    1 requests are never handed to a server, so every call takes the timeout
- *                      branch */
+ *                      branch | 2 the same, and the stopped server counts as not done within
+ *                      percall_stop_us (the abandon branch) */
 int qfec_tune(const char *key, int value);
 /* The current value of a knob of qfec_tune (*value); QFEC_EINVAL for an unknown key. */
 int qfec_tune_get(const char *key, int *value);
@@ -291,7 +303,8 @@ int qfec_percall_stats(unsigned long long out[5]);
 /* The same counters and more, as many as `n` asks for (returns how many were written, or an error):
  * [0..4] as qfec_percall_stats, [5] requests the server did not serve within percall_timeout_us
  * (each then waited for the stopped server, or ran through one launch), [6] / [7] fec_encode calls
- * served from / computing the group cache (all handles), [8] the current percall_idle_us. */
+ * served from / computing the group cache (all handles), [8] the current percall_idle_us, [9] servers
+ * abandoned after percall_stop_us (qfec_percall_stats out[4] is then -2). */
 int qfec_percall_counters(unsigned long long *out, int n);
 
 int qfec_set_kernel_variant(int variant);

@@ -25,6 +25,15 @@
  * qfec_tune("percall_idle_us", 0) makes it exit after every call.
  * fec_encode of a parity index computes the group's n - k rows at once and serves the group's
  * other indices from a per-handle copy while src[], sz and every input byte are unchanged.
+ *
+ * Device failure: a call whose request the resident block has not served within
+ * percall_timeout_us (default 2 s; e.g. other kernels hold every CU) stops the block and waits
+ * for it at most percall_stop_us more (default 2 s).  If the block still has not run then, the
+ * call gives up: fec_encode prints "[qfec] fec_encode: ..." to stderr and leaves dst as it was (as
+ * the reference does for an invalid index), fec_decode returns 1 (as for a singular matrix).  The
+ * same two outcomes report any other device error.  Neither call blocks longer than about
+ * percall_timeout_us + percall_stop_us in the server path (tests/test_gpu_host.py::
+ * test_percall_abandon_branch).
  */
 #ifndef QFEC_FEC_H
 #define QFEC_FEC_H

@@ -17,7 +17,7 @@ import numpy as np
 from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
 
 __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
-           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "device_count", "frame_udp", "unframe_udp",
+           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "probe_reconstruct", "device_count", "frame_udp", "unframe_udp",
            "NetFec", "Pipe", "Zfec"]
 
 
@@ -86,20 +86,31 @@ def percall_stats():
 
 
 def percall_counters():
-    """qfec_percall_counters: percall_stats plus timeouts, fec_encode group-cache hits / misses and
-    the current percall_idle_us."""
-    out = (C.c_ulonglong * 9)()
-    n = lib().qfec_percall_counters(out, 9)
+    """qfec_percall_counters: percall_stats plus timeouts, fec_encode group-cache hits / misses, the
+    current percall_idle_us and the servers abandoned after percall_stop_us."""
+    out = (C.c_ulonglong * 10)()
+    n = lib().qfec_percall_counters(out, 10)
     check(n if n < 0 else 0, "qfec_percall_counters")
     usable = out[4] if out[4] < 2**63 else out[4] - 2**64
     return {"calls": out[0], "launches": out[1], "relaunches": out[2], "running": bool(out[3]), "usable": usable,
-            "timeouts": out[5], "group_hits": out[6], "group_misses": out[7], "idle_us": out[8]}
+            "timeouts": out[5], "group_hits": out[6], "group_misses": out[7], "idle_us": out[8],
+            "abandoned": out[9]}
 
 
 def synth_fill(t, seed, stream=None):
     """Fill a device uint8 tensor with quicknet_amd.synth.synth_bytes(seed, t.numel())."""
     check(lib().qfec_synth_fill(_dev_ptr(t, what="synth_fill"), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(stream)),
           "qfec_synth_fill")
+
+
+def probe_reconstruct(data, parity, marks, block_size, lds_cap=0, stream=None):
+    """Calibration only: the reconstruct's memory skeleton (RS(10,3), RS(16,4)); the erased rows
+    of `data` receive garbage.  lds_cap: LDS bytes per block (0 none), a residency cap."""
+    G, k, pitch = data.shape
+    m = parity.shape[1]
+    check(lib().qfec_probe_reconstruct(_dev_ptr(data, what="data"), _dev_ptr(parity, what="parity"),
+                                       _dev_ptr(marks, what="marks"), G, k, m, block_size, pitch, lds_cap,
+                                       _stream_handle(stream)), "qfec_probe_reconstruct")
 
 
 def probe_stream(data, parity, block_size, stream=None):

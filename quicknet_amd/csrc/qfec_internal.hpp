@@ -71,6 +71,7 @@ struct ReconArgs {
     uint32_t wpg;             // waves per group = ceil(cols / 64) (vec16 LUT kernels)
     uint32_t cols8, wpg8;     // the same at 8-B columns: ceil(B / 8), ceil(cols8 / 64)
     uint32_t cols12, wpg12;   // the same at 12-B columns (recon_impl 4)
+    int rlds;                 // reconstruct skeleton probe: LDS bytes per block, a residency cap (0 none)
 };
 
 // FEC datagram batches (qfec_wire.hip): shards[G][n][pitch], wire[G][n][wire_pitch]
@@ -94,7 +95,6 @@ struct WireArgs {
     int checksum;
     int dec_pkt_size;
     int store_nt;             // fused send: bit 0 body, bit 1 head use non-temporal stores
-    int rx_skip_lost;         // receive (k_unpack_v2): rows with wire_len <= 0 are not read at all
 };
 
 hipError_t launch_build_shards(const WireArgs& a, hipStream_t s);
@@ -133,9 +133,9 @@ hipError_t launch_unpack_frames(const WireArgs& a, const FrameRecv& fr, int fp, 
 hipError_t launch_len_by_status(int32_t* len, const int32_t* status, uint64_t rows, hipStream_t s);
 hipError_t launch_gather_rows(const uint8_t* base, const uint64_t* off, const int32_t* len, uint64_t rows, int wrap_n,
                               int wrap_k, uint8_t* out, uint64_t out_pitch, int32_t* out_len, hipStream_t s);
-// fused receive for templated (k, m); *launched = false when the shape has no instance
-hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
-                               hipStream_t s, bool* launched);
+// the datagram receive k_rx (qfec_rx.hip) for templated (k, m); *launched = false when the shape has no instance
+hipError_t launch_rx(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr, hipStream_t s,
+                     bool* launched);
 hipError_t launch_unframe_udp(const FrameArgs& a, hipStream_t s);
 hipError_t launch_emit_wire(const WireArgs& a, hipStream_t s);
 hipError_t launch_parse_wire(const WireArgs& a, hipStream_t s);
@@ -160,6 +160,7 @@ hipError_t launch_encode(const EncodeArgs& a, int variant, hipStream_t stream);
 hipError_t launch_reconstruct(const ReconArgs& a, hipStream_t stream);
 hipError_t launch_synth_fill(uint8_t* p, uint64_t nbytes, uint64_t seed, hipStream_t stream);
 hipError_t launch_probe_xor(const EncodeArgs& a, hipStream_t stream);
+hipError_t launch_probe_recon(const ReconArgs& a, hipStream_t stream);
 
 // ---------------------------------------------------------------- host GF(2^8) (gf256.cpp)
 struct Field {

@@ -338,23 +338,9 @@ struct RTab {
         for (int i = 0; i < 5; ++i) t5[i] = at(j, c, K)[i];
     }
 };
+// acc[j] ^= sum_c coef(j, c) * x[c] over one column, exact E rows, survivors already in registers
 template <int K, int E, int D>
-__device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
-                                               uint64_t lost_bits, const RTab& T, uint64_t pitch, uint64_t off) {
-    uint32_t x[K][D];
-#pragma unroll
-    for (int c = 0; c < K; ++c) ldv<D>(x[c], src[c] + off);
-    uint8_t* dst[E];
-    uint32_t acc[E][D];
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-        const uint32_t l = (uint32_t)__builtin_ctzll(lost_bits);
-        lost_bits &= lost_bits - 1;
-        dst[j] = data_g + (uint64_t)l * pitch + off;
-#pragma unroll
-        for (int d = 0; d < D; ++d) acc[j][d] = 0;
-        if (T.quirk(j, K)) ldv_plain<D>(acc[j], dst[j]);  // rs.c column-0 quirk
-    }
+__device__ __forceinline__ void recon_mac_core(const uint32_t (&x)[K][D], uint32_t (&acc)[E][D], const RTab& T) {
 #pragma unroll
     for (int c = 0; c + 1 < K; c += 2) {
         Sel sa[D], sb[D];
@@ -382,6 +368,26 @@ __device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], u
                 acc[j][d] = xor3(acc[j][d], pp0(sl[d], t[0], t[1]), pp1(sl[d], t[2], t[3])) ^ pp2(sl[d], t[4]);
         }
     }
+}
+
+template <int K, int E, int D>
+__device__ __forceinline__ void recon_column_e(const uint8_t* const (&src)[K], uint8_t* __restrict__ data_g,
+                                               uint64_t lost_bits, const RTab& T, uint64_t pitch, uint64_t off) {
+    uint32_t x[K][D];
+#pragma unroll
+    for (int c = 0; c < K; ++c) ldv<D>(x[c], src[c] + off);
+    uint8_t* dst[E];
+    uint32_t acc[E][D];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(lost_bits);
+        lost_bits &= lost_bits - 1;
+        dst[j] = data_g + (uint64_t)l * pitch + off;
+#pragma unroll
+        for (int d = 0; d < D; ++d) acc[j][d] = 0;
+        if (T.quirk(j, K)) ldv_plain<D>(acc[j], dst[j]);  // rs.c column-0 quirk
+    }
+    recon_mac_core<K, E, D>(x, acc, T);
 #pragma unroll
     for (int j = 0; j < E; ++j) stv<D>(dst[j], acc[j]);
 }
@@ -574,6 +580,61 @@ __global__ void __launch_bounds__(256) k_probe_xor(EncodeArgs a) {
         st16(dst + (uint64_t)r * a.pitch, acc);
         acc.x += 1u;
     }
+}
+
+// the reconstruct's memory skeleton (calibration, not a codec): the auto body's mapping (8-B lanes,
+// one group per block of wpg8 waves) and accesses -- the marks, the K lowest surviving rows
+// (data and parity regions), the e erased data rows written -- with XOR in place of the decode
+template <int K, int M>
+__global__ void __launch_bounds__(256) k_probe_recon(ReconArgs a) {
+    constexpr int N = K + M;
+    const int lane = threadIdx.x & 63;
+    const uint64_t g = blockIdx.x;
+    const uint32_t part = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t mk = 0;
+    if (lane < K) mk = a.marks[g * K + lane];
+    else if (lane < N) mk = a.marks[a.groups * K + g * M + (lane - K)];
+    const uint64_t mask = __ballot(mk != 0) & ((1ull << N) - 1ull);
+    uint64_t lost = mask & ((1ull << K) - 1ull);
+    if (!lost) return;
+    uint64_t avail = ~mask & ((1ull << N) - 1ull);
+    if (__builtin_popcountll(avail) < K) return;
+    const uint32_t col = part * 64u + lane;
+    if (col >= a.cols8) return;
+    const uint64_t off = (uint64_t)col * 8u;
+    uint8_t* data_g = a.data + g * a.dgs;
+    const uint8_t* par_g = a.parity + g * a.pgs;
+    uint32_t x[K][2];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+        const uint32_t s = (uint32_t)__builtin_ctzll(avail);
+        avail &= avail - 1;
+        ldv<2>(x[c], (s < (uint32_t)K ? data_g + (uint64_t)s * a.pitch : par_g + (uint64_t)(s - K) * a.pitch) + off);
+    }
+    uint32_t acc[2] = {0, 0};
+#pragma unroll
+    for (int c = 0; c < K; ++c) { acc[0] ^= x[c][0]; acc[1] ^= x[c][1]; }
+    while (lost) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(lost);
+        lost &= lost - 1;
+        stv<2>(data_g + (uint64_t)l * a.pitch + off, acc);
+        acc[0] += 1u;
+    }
+}
+
+hipError_t launch_probe_recon(const ReconArgs& a, hipStream_t stream) {
+    if (a.groups == 0) return hipSuccess;
+    if (a.wpg8 < 1 || a.wpg8 > 4 || a.groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+#define QFEC_PROBE_REC(KK, MM)                                                                                    \
+    if (a.k == KK && a.m == MM) {                                                                                 \
+        hipLaunchKernelGGL((k_probe_recon<KK, MM>), dim3((unsigned)a.groups), dim3(64 * a.wpg8),               \
+                           (size_t)std::max(a.rlds, 0), stream, a);                                               \
+        return hipGetLastError();                                                                                 \
+    }
+    QFEC_PROBE_REC(10, 3)
+    QFEC_PROBE_REC(16, 4)
+#undef QFEC_PROBE_REC
+    return hipErrorInvalidValue;
 }
 
 // ------------------------------------------------------------------ launchers

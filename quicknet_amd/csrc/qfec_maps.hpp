@@ -1,5 +1,5 @@
 // qfec_maps.hpp -- which caller pointers are system memory, from the process's mappings
-// (module/rs.h host-pointer paths, qfec_runtime.cpp count_device_ptrs).  Header-only so the CPU
+// (module/rs.h host-pointer paths, qfec_rs_abi.cpp classify_ptrs).  Header-only so the CPU
 // suite can hold the rules to synthetic /proc/self/maps text (tests/test_maps_classify.py).
 #pragma once
 

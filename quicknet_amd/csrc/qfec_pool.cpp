@@ -35,9 +35,17 @@ void HostPool::loop(int id) {
             job = job_;
             nt = nt_;
         }
-        if (id < nt) (*job)(id, nt);
+        std::exception_ptr e;
+        if (id < nt) {
+            try {
+                (*job)(id, nt);
+            } catch (...) {
+                e = std::current_exception();
+            }
+        }
         {
             std::lock_guard<std::mutex> lk(mu_);
+            if (e && !err_) err_ = e;
             if (--pending_ == 0) cv_done_.notify_one();
         }
     }
@@ -55,13 +63,23 @@ void HostPool::run(const std::function<void(int, int)>& fn, int parts) {
         job_ = &fn;
         nt_ = nt;
         pending_ = (int)workers_.size();
+        err_ = nullptr;
         ++gen_;
     }
     cv_job_.notify_all();
-    fn(0, nt);
+    std::exception_ptr mine;
+    try {
+        fn(0, nt);
+    } catch (...) {
+        mine = std::current_exception();
+    }
     std::unique_lock<std::mutex> lk(mu_);
-    cv_done_.wait(lk, [&] { return pending_ == 0; });
+    cv_done_.wait(lk, [&] { return pending_ == 0; });  // every worker is done with fn
     job_ = nullptr;
+    std::exception_ptr e = mine ? mine : err_;
+    err_ = nullptr;
+    lk.unlock();
+    if (e) std::rethrow_exception(e);
 }
 
 static int read_int_file(const char* path, long long* a, long long* b) {

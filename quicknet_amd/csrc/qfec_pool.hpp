@@ -5,6 +5,7 @@
 #pragma once
 
 #include <condition_variable>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -21,7 +22,11 @@ public:
     HostPool& operator=(const HostPool&) = delete;
 
     int threads() const { return (int)workers_.size() + 1; }
-    // fn(t, nt) for t in [0, nt); nt = min(threads(), max(1, parts)).  Serialised between callers.
+    // fn(t, nt) for t in [0, nt); nt = min(threads(), max(1, parts)).  Serialised between callers:
+    // concurrent module/rs.h calls, on one device or several, run their copy phases one after
+    // another (each phase already uses every thread of the process's CPU share).  An exception
+    // thrown by any part is rethrown here once every part has finished, so no worker is left
+    // holding `fn`.
     void run(const std::function<void(int, int)>& fn, int parts = 1 << 30);
 
 private:
@@ -35,6 +40,7 @@ private:
     unsigned long long gen_ = 0;
     int pending_ = 0;
     bool stop_ = false;
+    std::exception_ptr err_;  // the first exception a part of the current job threw
 };
 
 // CPUs this process may actually use: the affinity mask, capped by a cgroup CPU quota

@@ -14,7 +14,7 @@
 //   * dec_src_pkt_info (FecCodecBuf.cpp:109-133) on every data row: payload size, payload
 //     checksum, status.
 // Outputs are those of the staged path (k_parse_wire -> reconstruct -> k_check_payloads) and of
-// the round-2..4 kernel k_unpack_v2, byte for byte.
+// the receive kernel of rounds 2-4 (retired in round 5), byte for byte.
 //
 // The design is set by what bounds the receive: issue, not bytes (profiles/r05a: the
 // round-4 kernel issued 1 775 VALU + 1 137 SALU per group and its waves waited on memory half of
@@ -588,7 +588,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NV == 4
             }
             v_dt = t;
         }
-        // ---- verdicts on the survivors (k_unpack_fused's rules), ln c for survivor c
+        // ---- verdicts on the survivors (a survivor whose header or shard checksum fails is dropped and
+        // the group decoded from the next valid row, NetFecCodec.cpp:504-528), ln c for survivor c
         uint32_t nb = 0, vr = 0, fb = 0;  // ln c: row bit if bad / verified / frame-checksum bad
         {
             const uint32_t r = pl.v_srow & 0xFu, rb_bit = 1u << r;
@@ -826,8 +827,8 @@ hipError_t rx_dispatch(const WireArgs& a, const int32_t* lut, const uint32_t* re
 
 }  // namespace
 
-hipError_t launch_unpack_fused(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr,
-                               hipStream_t s, bool* launched) {
+hipError_t launch_rx(const WireArgs& a, const int32_t* lut, const uint32_t* records, uint32_t rec_hdr, hipStream_t s,
+                     bool* launched) {
     return rx_dispatch<false>(a, lut, records, rec_hdr, s, launched, FrameRecv{}, 0);
 }
 

@@ -253,7 +253,15 @@ struct HostArena {
     // where that fails: alternating processes on one box, the receive flush 14.4-14.9 -> 11.7-12.5 ms
     // and the send flush 16.6-16.8 -> 14.9-15.1 ms (fewer page translations for the arena's H2D and
     // D2H and for the callbacks' reads; profiles/r05w)
+    // A registration that fails once (no device: FEC-off contexts need none) is not tried again:
+    // later growths go straight to hipHostMalloc / malloc instead of mapping, zeroing and unmapping
+    // a block each time.
+    static std::atomic<bool>& register_failed() {
+        static std::atomic<bool> f{false};
+        return f;
+    }
     static uint8_t* map_huge(size_t bytes) {
+        if (register_failed().load(std::memory_order_relaxed)) return nullptr;
         void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (p == MAP_FAILED) return nullptr;
         (void)madvise(p, bytes, MADV_HUGEPAGE);
@@ -261,6 +269,7 @@ struct HostArena {
         if (hipHostRegister(p, bytes, hipHostRegisterMapped) != hipSuccess) {
             (void)hipGetLastError();
             munmap(p, bytes);
+            register_failed().store(true, std::memory_order_relaxed);
             return nullptr;
         }
         return static_cast<uint8_t*>(p);

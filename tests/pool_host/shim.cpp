@@ -2,6 +2,8 @@
 // thread pool of the module/rs.h host paths and of qfec_zfec's session machines) driven from
 // tests/test_host_pool.py on CPU.  Never shipped.
 #include <atomic>
+#include <chrono>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -43,5 +45,33 @@ int pool_check(int threads, int parts, int jobs, int callers, long long* calls_o
     for (auto& t : th) t.join();
     *calls_out = calls.load();
     return bad.load();
+}
+
+// part `thrower` of each job throws; run() must rethrow it only after every other part has returned
+// (a part sleeps first, so a run() that returned early would be seen).  Returns the number of jobs
+// that did not rethrow, or rethrew before all parts were done; then checks the pool still works.
+int pool_throw_check(int threads, int thrower, int jobs) {
+    qfec::HostPool pool(threads);
+    int bad = 0;
+    for (int j = 0; j < jobs; ++j) {
+        std::atomic<int> done{0};
+        int nt_seen = 0;
+        bool threw = false;
+        try {
+            pool.run([&](int t, int nt) {
+                if (t == 0) nt_seen = nt;
+                if (t == thrower % nt) throw std::runtime_error("part failed");
+                std::this_thread::sleep_for(std::chrono::milliseconds(2));
+                done++;
+            });
+        } catch (const std::runtime_error&) {
+            threw = true;
+        }
+        if (!threw || done.load() != nt_seen - 1) bad++;
+    }
+    std::atomic<int> after{0};
+    pool.run([&](int, int) { after++; });
+    if (after.load() != pool.threads()) bad++;
+    return bad;
 }
 }

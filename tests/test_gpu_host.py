@@ -547,6 +547,60 @@ def test_percall_timeout_branch(oracle):
     assert np.array_equal(dst, expect(data, k))
 
 
+def test_percall_abandon_branch(oracle, capfd):
+    """the wait for a stopped server is bounded by percall_stop_us.  With percall_fault
+    2 (no server takes the request, and the stopped block counts as not done within percall_stop_us)
+    fec_encode prints to stderr and leaves dst as it was, fec_decode returns 1, and the device's
+    server is abandoned (usable -2): later calls run through one launch, oracle-exact, and
+    percall_resident 1 sets up a fresh server.  No real CU starvation is needed."""
+    import time
+    k, n, sz = 10, 13, 1028
+    fp = qa.FecParms(k, n)
+    full = fp.matrix
+    expect = _encode_checker(oracle, fp, k, n)
+    rng = np.random.default_rng(57)
+    qa.tune("percall_resident", 1)
+    qa.tune("percall_group", 0)
+    c0 = qa.percall_counters()
+    if c0["usable"] == -1:
+        pytest.skip("device memory not CPU-mapped on this box: the launch-per-call path serves")
+    data = rng.integers(0, 256, (k, sz), dtype=np.uint8)
+    coded = np.concatenate([data, np.stack([expect(data, j) for j in range(k, n)])])
+    keep = list(range(3, n))
+    try:
+        qa.tune("percall_timeout_us", 0)
+        qa.tune("percall_fault", 2)
+        dst = np.full(sz, 0xA5, np.uint8)
+        t0 = time.perf_counter()
+        fp.encode(data, dst, k, sz)
+        assert time.perf_counter() - t0 < 1.0
+        assert (dst == 0xA5).all()  # left as it was
+        assert "[qfec] fec_encode:" in capfd.readouterr().err
+        c1 = qa.percall_counters()
+        assert c1["usable"] == -2 and c1["abandoned"] == c0["abandoned"] + 1, c1
+        qa.tune("percall_fault", 0)
+        fp.encode(data, dst, k, sz)  # the one-launch path while the server is abandoned
+        assert np.array_equal(dst, expect(data, k))
+        assert qa.percall_counters()["usable"] == -2
+        qa.tune("percall_resident", 1)  # retry: a fresh server at the next call
+        qa.tune("percall_fault", 2)
+        rc, _, _ = fp.decode(coded[keep], keep, sz)
+        assert rc == 1
+        assert qa.percall_counters()["abandoned"] == c0["abandoned"] + 2
+    finally:
+        qa.tune("percall_fault", 0)
+        qa.tune("percall_timeout_us", 2000000)
+        qa.tune("percall_group", 1)
+        qa.tune("percall_resident", 1)
+    rc, pk, _ = fp.decode(coded[keep], keep, sz)
+    rc2, pk2, _ = oracle.fec_decode(k, n, full, coded[keep], keep)
+    assert rc == rc2 == 0 and np.array_equal(pk, pk2)
+    dst = np.zeros(sz, np.uint8)
+    fp.encode(data, dst, k + 1, sz)
+    assert np.array_equal(dst, expect(data, k + 1))
+    assert qa.percall_counters()["usable"] == 1  # served by a fresh server again
+
+
 def test_percall_idle_knob_bounds_device_sync(oracle):
     """The resident block's footprint (qfec.h): a hipDeviceSynchronize issued
     right after a call waits for the block's idle exit, at most percall_idle_us (1 ms by default) --

@@ -292,6 +292,32 @@ def test_reconstruct_impls_vs_oracle(oracle, impl, k, m, B):
     assert int(failed.item()) == unrecoverable
 
 
+@pytest.mark.parametrize("lds", [0, 20480])
+@pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (10, 3, 1400)])
+def test_probe_reconstruct_writes_only_erased_rows(k, m, B, lds):
+    """qfec_probe_reconstruct (the reconstruct's memory skeleton, calibration only) writes the
+    erased data rows of recoverable groups and nothing else; other shapes are refused."""
+    G = 1000
+    pitch = round16(B)
+    rng = np.random.default_rng(B + k)
+    gm = np.zeros((G, k + m), np.uint8)
+    for g in range(G):
+        gm[g, rng.choice(k + m, size=int(rng.integers(0, m + 2)), replace=False)] = 1
+    marks = marks_to_rs_layout(gm, k)
+    data = synth_bytes(B * 3 + k, G * k * pitch).reshape(G, k, pitch)
+    dd = to_dev(data)
+    qa.probe_reconstruct(dd, to_dev(np.zeros((G, m, pitch), np.uint8)), to_dev(marks), B, lds)
+    torch.cuda.synchronize()
+    out = dd.cpu().numpy()
+    written = np.zeros((G, k), bool)
+    ok = (gm[:, :k].sum(1) > 0) & (gm.sum(1) <= m)
+    written[ok] = gm[ok, :k] == 1
+    assert np.array_equal(out[~written], data[~written])
+    with pytest.raises(qa.QfecError):
+        qa.probe_reconstruct(to_dev(np.zeros((4, 4, 64), np.uint8)), to_dev(np.zeros((4, 2, 64), np.uint8)),
+                             to_dev(np.zeros(24, np.uint8)), 64)
+
+
 @pytest.mark.parametrize("impl", [-1, 0, 2])
 @pytest.mark.parametrize("flavour", ["cauchy", "vandermonde"])
 @pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (10, 3, 100), (16, 4, 8)])

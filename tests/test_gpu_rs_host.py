@@ -62,12 +62,12 @@ def mixed_marks(G, k, m, seed):
 
 
 @pytest.mark.parametrize("k,m,B", [(10, 3, 1000), (4, 2, 1024), (16, 4, 1400)])
-@pytest.mark.parametrize("zero_copy", [1, 0])
 @pytest.mark.parametrize("chunk,threads", [(7, 4), (0, 0), (1, 1)])
-def test_rs_host_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_copy, chunk, threads):
-    """Many pipelined chunks (host_chunk groups each, two slots alternating), 1 to 4 copy threads,
-    zero copy or staged through the slot's device buffer; shard rows scattered in memory."""
-    knobs("host_zero_copy", zero_copy)
+def test_rs_host_encode_pipeline_vs_oracle(oracle, knobs, k, m, B, chunk, threads):
+    """reed_solomon_encode on host pointers: many pipelined chunks (host_chunk groups each, two slots
+    alternating), 1 to 4 copy threads; shard rows scattered in memory.  The encode leg always stages
+    each chunk through the slot's device buffer (reading the pinned slot in place over PCIe measured
+    slower, profiles/r05af), so host_zero_copy does not apply to it and is not varied here."""
     knobs("host_chunk", chunk)
     knobs("host_threads", threads)
     G, n = 61, k + m
@@ -78,15 +78,30 @@ def test_rs_host_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_copy, chunk, th
     for i in range(G * k, G * n):
         rows[i][:] = 0x33
     rs = qa.ReedSolomon(k, m)
-    L = qa.lib()
-    ptrs = ptr_array(rows)
-    assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == 0
+    assert qa.lib().reed_solomon_encode(rs._h, ptr_array(rows), G * n, B) == 0
     want = np.zeros((G, m, B), np.uint8)
     oracle.rs_encode(oracle.cauchy(k, m), data0, want, B)
-    got = np.stack(rows[G * k:]).reshape(G, m, B)
-    assert np.array_equal(got, want)
-    # reconstruct with inconsistent parity (pins the survivor rule byte for byte) and erased rows
-    # pre-filled with 0x5A
+    assert np.array_equal(np.stack(rows[G * k:]).reshape(G, m, B), want)
+    rs.close()
+
+
+@pytest.mark.parametrize("k,m,B", [(10, 3, 1000), (4, 2, 1024), (16, 4, 1400)])
+@pytest.mark.parametrize("zero_copy", [1, 0])
+@pytest.mark.parametrize("chunk,threads", [(7, 4), (0, 0), (1, 1)])
+def test_rs_host_reconstruct_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_copy, chunk, threads):
+    """reed_solomon_reconstruct on host pointers: many pipelined chunks, 1 to 4 copy threads, the
+    kernel reading the survivors and writing the erased rows in the pinned slot in place (zero copy)
+    or through the slot's device buffer; inconsistent parity (pins the survivor rule byte for byte),
+    erased rows pre-filled with 0x5A, unrecoverable groups."""
+    knobs("host_zero_copy", zero_copy)
+    knobs("host_chunk", chunk)
+    knobs("host_threads", threads)
+    G, n = 61, k + m
+    rows, _keep = scattered_rows(G, n, B, 5)
+    data0 = synth_bytes(0xA11CE + k, G * k * B).reshape(G, k, B)
+    rs = qa.ReedSolomon(k, m)
+    L = qa.lib()
+    ptrs = ptr_array(rows)
     par = synth_bytes(0xBEEF + k, G * m * B).reshape(G, m, B)
     gm = mixed_marks(G, k, m, 11 + k)
     marks = marks_to_rs_layout(gm, k)
@@ -103,6 +118,109 @@ def test_rs_host_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_copy, chunk, th
     assert np.array_equal(np.stack(rows[:G * k]).reshape(G, k, B), exp)
     assert np.array_equal(np.stack(rows[G * k:]).reshape(G, m, B), par)  # parity never written
     rs.close()
+
+
+@pytest.mark.parametrize("layout", ["host", "mixed"])
+def test_rs_wide_code_host_pointers(oracle, capfd, monkeypatch, layout):
+    """n = k + m > 24 (no pattern LUT: per-chunk decode records) on host shard pointers.
+    Host rows go through the pinned stage with one DMA per chunk, device rows one copy each; both
+    calls equal the oracle, return code included, and the reconstruct of 3 000 RS(20,10) groups
+    (90 000 pointers) finishes in well under a second (it had taken one pageable copy per row)."""
+    import time
+    k, m, B, G = 20, 10, 1024, 3000
+    n = k + m
+    rows, _keep = scattered_rows(G, n, B, 21)
+    dev = []
+    if layout == "mixed":  # every 7th row in device memory
+        for i in range(0, G * n, 7):
+            t = torch.zeros(B, dtype=torch.uint8, device=DEV)
+            dev.append(t)
+            rows[i] = t
+    data0 = synth_bytes(0x20 + len(dev), G * k * B).reshape(G, k, B)
+
+    def put(i, a):
+        if isinstance(rows[i], np.ndarray):
+            rows[i][:] = a
+        else:
+            rows[i].copy_(torch.from_numpy(np.ascontiguousarray(a)).to(DEV))
+
+    def get_all(lo, hi):
+        return np.stack([rows[i].copy() if isinstance(rows[i], np.ndarray) else rows[i].cpu().numpy()
+                         for i in range(lo, hi)])
+    for i in range(G * k):
+        put(i, data0.reshape(G * k, B)[i])
+    torch.cuda.synchronize()
+    rs = qa.ReedSolomon(k, m)
+    L = qa.lib()
+    ptrs = ptr_array(rows)
+    assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == 0
+    want = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(oracle.cauchy(k, m), data0, want, B)
+    assert np.array_equal(get_all(G * k, G * n).reshape(G, m, B), want)
+    gm = mixed_marks(G, k, m, 31)
+    marks = marks_to_rs_layout(gm, k)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+    for i in range(G * k):
+        put(i, d.reshape(G * k, B)[i])
+    torch.cuda.synchronize()
+    monkeypatch.setenv("QFEC_RS_TRACE", "1")
+    t0 = time.perf_counter()
+    rc = L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(marks.ctypes.data), G * n, B)
+    el = time.perf_counter() - t0
+    monkeypatch.delenv("QFEC_RS_TRACE")
+    exp = d.copy()
+    rc_o = oracle.rs_reconstruct(oracle.cauchy(k, m), exp, want.copy(), marks, B)
+    assert rc == rc_o == -1
+    assert np.array_equal(get_all(0, G * k).reshape(G, k, B), exp)
+    print(capfd.readouterr().err)
+    if layout == "host":
+        assert el < 1.0, el
+    rs.close()
+
+
+def test_rs_many_device_allocations_classify_fast(oracle, capfd, monkeypatch):
+    """every device row in its own hipMalloc (40 000 allocations): the classifier keeps
+    the allocation ranges ordered (binary search), so classifying the array costs milliseconds, not
+    a scan of every range per pointer (QFEC_RS_TRACE reports the classify time); the encode equals
+    the oracle's."""
+    import re
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t]
+    hip.hipFree.argtypes = [C.c_void_p]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    k, m, B = 10, 3, 512
+    G = 40000 // (k + m)
+    n = k + m
+    ptrs = []
+    try:
+        for _ in range(G * n):
+            p = C.c_void_p()
+            assert hip.hipMalloc(C.byref(p), 65536) == 0
+            ptrs.append(p.value)
+        data0 = synth_bytes(0x77, G * k * B).reshape(G, k, B)
+        flat = np.ascontiguousarray(data0.reshape(G * k, B))
+        for i in range(G * k):
+            assert hip.hipMemcpy(ptrs[i], flat[i].ctypes.data, B, 1) == 0  # hipMemcpyHostToDevice
+        rs = qa.ReedSolomon(k, m)
+        arr = (C.c_void_p * len(ptrs))(*ptrs)
+        monkeypatch.setenv("QFEC_RS_TRACE", "1")
+        assert qa.lib().reed_solomon_encode(rs._h, arr, G * n, B) == 0
+        monkeypatch.delenv("QFEC_RS_TRACE")
+        err = capfd.readouterr().err
+        cls = re.search(r"reed_solomon_encode \(staged\).*classify ([0-9.]+) ms", err)
+        assert cls, err[-2000:]
+        assert float(cls.group(1)) < 500.0, err[-500:]
+        got = np.zeros((G * m, B), np.uint8)
+        for i in range(G * m):
+            assert hip.hipMemcpy(got[i].ctypes.data, ptrs[G * k + i], B, 2) == 0  # hipMemcpyDeviceToHost
+        want = np.zeros((G, m, B), np.uint8)
+        oracle.rs_encode(oracle.cauchy(k, m), data0, want, B)
+        assert np.array_equal(got.reshape(G, m, B), want)
+        rs.close()
+    finally:
+        for p in ptrs:
+            hip.hipFree(p)
 
 
 def test_rs_host_pipeline_recoverable_rc0(oracle, knobs):

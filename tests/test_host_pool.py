@@ -1,6 +1,7 @@
 """The host thread pool (quicknet_amd/csrc/qfec_pool.cpp) on CPU: every part of a job runs
 exactly once with the part count the caller asked for (capped by the pool's threads), jobs from
-several caller threads are serialised, and usable_cpus() honours the affinity mask (and a cgroup
+several caller threads are serialised, an exception in any part is rethrown after all parts are
+done, and usable_cpus() honours the affinity mask (and a cgroup
 CPU quota where one is set).  tests/pool_host/shim.cpp is compiled here with g++."""
 import ctypes as C
 import os
@@ -31,6 +32,13 @@ def test_pool_parts_run_once(shim, threads, parts, jobs, callers):
     assert shim.pool_check(threads, parts, jobs, callers, C.byref(calls)) == 0
     per = min(threads, max(1, parts))
     assert calls.value == per * jobs * callers
+
+
+@pytest.mark.parametrize("threads,thrower", [(4, 0), (4, 2), (8, 7), (1, 0)])
+def test_pool_exception_waits_for_all_parts(shim, threads, thrower):
+    """A part that throws (the caller's part or a worker's): run() rethrows once every other part
+    has returned, and the pool runs the next job normally."""
+    assert shim.pool_throw_check(threads, thrower, 20) == 0
 
 
 def test_usable_cpus(shim):

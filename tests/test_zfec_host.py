@@ -107,3 +107,32 @@ def test_host_forged_check_packets(host_layer, seed):
     z = qa.Zfec(_lib=host_layer)
     replay(z, scripts, [run_oracle(s) for s in scripts], "one_flush")
     z.close()
+
+
+def test_host_arena_register_failure(host_layer):
+    """The arenas' 2 MiB-page blocks are registered with the runtime; when registration fails (no
+    device), later growths skip the mapping: one registration attempt over many arena growths, and
+    the layer's datagrams and deliveries unchanged (hipHostMalloc / malloc arenas)."""
+    import quicknet_amd as qa
+    raw = C.CDLL(OUT)
+    fail = C.c_int.in_dll(raw, "stub_register_fail")
+    calls = C.c_int.in_dll(raw, "stub_register_calls")
+    fail.value = 1
+    before = calls.value
+    try:
+        z = qa.Zfec(_lib=host_layer)
+        A, B = z.session(k=10, n=13), z.session(k=10, n=13)
+        payloads = [bytes([(i * 7 + j) & 0xFF for j in range(64)]) * 16 for i in range(256)]
+        for rep in range(24):  # ~6 MiB queued per direction: the arenas grow several times
+            for p in payloads:
+                z.pack_input(A, p)
+        sent, _ = z.flush()
+        for s, d in sent:
+            assert s == A
+            z.unpack_input(B, d)
+        _, got = z.flush()
+        assert [g[1] for g in got if g[0] == B] == payloads * 24
+        z.close()
+    finally:
+        fail.value = 0
+    assert calls.value - before == 1

@@ -179,7 +179,13 @@ hipError_t hipHostFree(void* p) {
     free(p);
     return hipSuccess;
 }
-hipError_t hipHostRegister(void*, size_t, unsigned int) { return hipSuccess; }
+// test hooks: make registration fail, and count the attempts (test_host_arena_register_failure)
+int stub_register_fail = 0;
+int stub_register_calls = 0;
+hipError_t hipHostRegister(void*, size_t, unsigned int) {
+    ++stub_register_calls;
+    return stub_register_fail ? hipErrorInvalidValue : hipSuccess;
+}
 hipError_t hipHostUnregister(void*) { return hipSuccess; }
 hipError_t hipGetLastError(void) { return hipSuccess; }
 hipError_t hipGetDevice(int* d) {

@@ -45,6 +45,7 @@ def main():
     p.add_argument("--only", default="", help="comma-separated variant-name prefixes ('_' for ' ')")
     p.add_argument("--patterns", type=int, default=0, help="draw each group's erasures from this many masks")
     p.add_argument("--pairs", action="store_true", help="time reconstruct right after encode, as bench.py does")
+    p.add_argument("--probe-lds", default="0", help="reconstruct skeleton probe: LDS bytes per block to try")
     a = p.parse_args()
     k, m, B, G = a.k, a.m, a.block, a.groups
     dev = torch.device("cuda:0")
@@ -60,6 +61,10 @@ def main():
         gm = gm[:a.patterns][pick]
     marks = torch.from_numpy(marks_to_rs_layout(gm, k)).to(dev)
     work = data.clone()
+    # the erased data rows poisoned: every reconstruct variant must rebuild them (checked in round 0)
+    lost = torch.from_numpy(gm[:, :k].astype(bool)).to(dev)
+    damaged = data.clone()
+    damaged[lost] = 0x5A
     code.encode(data, par, B)
     code.prepare_reconstruct()
     dec_groups = int((gm[:, :k].sum(1) > 0).sum())
@@ -73,8 +78,10 @@ def main():
     def rec():
         code.reconstruct(work, par, marks, B)
 
-    def probe():
-        qa.probe_stream(data, par, B)
+    probe_out = torch.empty_like(par)
+
+    def probe():  # into its own buffer: the reconstruct variants read par
+        qa.probe_stream(data, probe_out, B)
 
     def pair_enc():  # bench.py's order: reconstruct right after an encode
         code.encode(data, par, B)
@@ -91,6 +98,15 @@ def main():
         ("recon impl4 (exact e, 12-B lanes)", lambda: qa.tune("recon_impl", 4), rec, dec_bytes),
         ("recon impl8 (impl3, one group per block)", lambda: qa.tune("recon_impl", 8), rec, dec_bytes),
     ]
+
+    skel = data.clone()
+
+    # the reconstruct's memory skeleton (XOR, garbage into skel's erased rows) at LDS residency caps
+    for lds in [int(x) for x in a.probe_lds.split(",")]:
+        variants.append((f"probe recon lds{lds} (reconstruct skeleton)", lambda: None,
+                         lambda lds=lds: qa.probe_reconstruct(skel, par, marks, B, lds), dec_bytes))
+    variants.append(("recon impl8 again (drift check)", lambda: qa.tune("recon_impl", 8), rec, dec_bytes))
+
     if a.recon_only:
         variants = [v for v in variants if v[0].startswith(("recon impl2", "recon impl3", "recon impl4", "probe"))]
     if a.only:
@@ -107,7 +123,13 @@ def main():
         for name, setup, fn, _ in variants:
             qa.set_kernel_variant(0)
             setup()
+            if r == 0 and fn is rec:
+                work.copy_(damaged)
             fn()
+            if r == 0 and fn is rec:
+                torch.cuda.synchronize()
+                assert torch.equal(work[..., :B], data[..., :B]), f"{name}: wrong output"
+                print(f"  {name}: output checked", flush=True)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(a.reps):

@@ -60,6 +60,8 @@ def main():
     p.add_argument("--m", type=int, default=3)
     p.add_argument("--block", type=int, default=1024)
     p.add_argument("--groups", type=int, default=100_000)
+    p.add_argument("--erasures", type=int, default=3, help="erasures per group (bench.py --erasures); key suffix _eN "
+                                                           "when not 3 (config 4: 4, read by bench.py's config4 field)")
     p.add_argument("--tag", default="PMC run", help="which run produced the numbers (recorded in the JSON)")
     p.add_argument("--workload", choices=["headline", "wire"], default="headline")
     p.add_argument("--csv-home", default=None,
@@ -69,7 +71,7 @@ def main():
     if a.workload == "wire":
         return wire_main(a)
     bench_args = ["--steps", "5", "--warmup", "1", "--k", str(a.k), "--m", str(a.m), "--block", str(a.block),
-                  "--groups", str(a.groups), "--no-side", "--no-config4", "--no-host"]
+                  "--groups", str(a.groups), "--erasures", str(a.erasures), "--no-side", "--no-config4", "--no-host"]
     fetch = run_pass("FETCH_SIZE", a.out, bench_args, a.k, a.m)
     write = run_pass("WRITE_SIZE", a.out, bench_args, a.k, a.m)
     k, m, B, G = a.k, a.m, a.block, a.groups
@@ -85,7 +87,7 @@ def main():
     if "probe" in res:
         res["probe"]["algorithmic_read"] = probe_alg_read
         res["probe"]["algorithmic_write"] = probe_alg_write
-    key = f"rs{k}_{m}_b{B}_g{G}"
+    key = f"rs{k}_{m}_b{B}_g{G}" + (f"_e{a.erasures}" if a.erasures != 3 else "")
     doc = {}
     if os.path.exists(a.json):
         with open(a.json) as fh:
