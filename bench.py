@@ -88,6 +88,8 @@ def parse(argv=None):
                         "affinity mask and cgroup quota, quicknet_amd.topology.cpu_share; 0 skips it)")
     p.add_argument("--no-side", action="store_true", help="skip the rank-0 side configurations")
     p.add_argument("--no-config4", action="store_true", help="skip the sharded RS(16,4) config 4 leg")
+    p.add_argument("--config4-only", action="store_true",
+                   help="run only the config 4 leg and print its record (tools/pmc_traffic.py --workload config4)")
     p.add_argument("--config4-groups", type=int, default=250_000, help="config 4 job size (tests shrink it)")
     p.add_argument("--no-host", action="store_true", help="skip the host-to-host legs (config 5)")
     p.add_argument("--protocol-check", action="store_true",
@@ -987,6 +989,11 @@ def main(argv=None):
             dist.destroy_process_group()
         return rc
     qa.set_kernel_variant(args.variant)
+    if args.config4_only:  # measurement helper: the config 4 leg's launches alone, under a profiler
+        c4 = config4_sharded(rank, world, args.config4_groups, steps=args.steps, warmup=args.warmup)
+        if rank == 0:
+            print(json.dumps({"config4": c4}), flush=True)
+        return 0 if c4["verified"] else 1
     dev = torch.device("cuda", local)
     k, m, B, G, E = args.k, args.m, args.block, args.groups, args.erasures
     n = k + m

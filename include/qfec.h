@@ -225,6 +225,16 @@ int qfec_gather_rows(const unsigned char *d_base, const unsigned long long *d_of
 /* Fill nbytes of device memory with the synthetic stream of quicknet_amd/synth.py. */
 int qfec_synth_fill(unsigned char *d_ptr, long long nbytes, unsigned long long seed, void *stream);
 
+/* module/rs.h on host shard pointers (reed_solomon_encode / reed_solomon_reconstruct with every shard
+ * in host memory) pipelines its chunks over two slots on the calling thread's current device.
+ * qfec_rs_host_devices spreads them over two slots per entry of `devices` instead -- each GPU has
+ * its own PCIe link, and a device may be listed more than once (more chunks in flight on it); n = 0
+ * goes back to the current device.  Outputs are identical either way.  Not to be called while a
+ * module/rs.h call is running on another thread (it waits for it).  qfec_rs_host_devices_get
+ * copies up to `cap` entries of the list and returns its length (0: the current device). */
+int qfec_rs_host_devices(const int *devices, int n);
+int qfec_rs_host_devices_get(int *devices, int cap);
+
 /* Calibration probe, NOT a codec: streams the encode's traffic (k rows in, m rows out,
  * XOR only).  Its time is the memory-side ceiling the GF kernels are compared with. */
 int qfec_probe_stream(const unsigned char *d_data, unsigned char *d_parity, long long groups, int k, int m,
@@ -244,6 +254,8 @@ int qfec_probe_reconstruct(unsigned char *d_data, const unsigned char *d_parity,
  *   "host_zero_copy"   1 pinned host batches worked on in place | 0 staged copies (module/rs.h on host
  *                      pointers: the reconstruct only; its encode always stages through the device,
  *                      measured faster for a freshly gathered slot)
+ *   "host_lanes"       4 (default) | 2 .. 8: module/rs.h on host pointers, chunk slots in flight on the
+ *                      current device; qfec_rs_host_devices spreads them over listed devices instead
  *   "host_chunk"       groups per staged host chunk (0: by bytes: ~32 MiB for qfec_*_host, ~16 MiB of
  *                      caller shards for module/rs.h on host pointers)
  *   "host_threads"     host threads that gather / scatter module/rs.h host shard pointers (0: the

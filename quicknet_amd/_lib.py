@@ -19,7 +19,7 @@ EXPORTS = {
                "qfec_encode", "qfec_encode_host", "qfec_reconstruct", "qfec_reconstruct_host", "qfec_prepare_reconstruct", "qfec_decode_rows",
                "qfec_pipe_new", "qfec_pipe_free", "qfec_pipe_encode", "qfec_pipe_reconstruct", "qfec_pipe_wait", "qfec_pipe_slots",
                "qfec_fec_code", "qfec_rs_code", "qfec_fec_matrix", "qfec_pack_datagrams", "qfec_unpack_datagrams",
-               "qfec_frame_udp", "qfec_unframe_udp", "qfec_pack_frames", "qfec_unpack_frames", "qfec_gather_rows", "qfec_synth_fill", "qfec_probe_stream", "qfec_probe_reconstruct",
+               "qfec_frame_udp", "qfec_unframe_udp", "qfec_pack_frames", "qfec_unpack_frames", "qfec_gather_rows", "qfec_synth_fill", "qfec_probe_stream", "qfec_probe_reconstruct", "qfec_rs_host_devices", "qfec_rs_host_devices_get",
                "qfec_tune", "qfec_tune_get", "qfec_percall_stats", "qfec_percall_counters", "qfec_set_kernel_variant", "qfec_get_kernel_variant", "qfec_device_count", "qfec_strerror",
                "qfec_last_error", "qfec_version"],
     "qfec_net.h": ["qfec_net_new", "qfec_net_free", "qfec_net_session", "qfec_net_enable", "qfec_net_pack_input", "qfec_net_flush_pack",
@@ -100,6 +100,8 @@ def lib():
         "qfec_synth_fill": (i, [vp, ll, u64, vp]),
         "qfec_probe_stream": (i, [vp, vp, ll, i, i, i, ll, vp]),
         "qfec_probe_reconstruct": (i, [vp, vp, vp, ll, i, i, i, ll, i, vp]),
+        "qfec_rs_host_devices": (i, [vp, i]),
+        "qfec_rs_host_devices_get": (i, [vp, i]),
         "qfec_tune": (i, [C.c_char_p, i]),
         "qfec_tune_get": (i, [C.c_char_p, C.POINTER(i)]),
         "qfec_percall_stats": (i, [vp]),

@@ -17,7 +17,7 @@ import numpy as np
 from ._lib import QFEC_CAUCHY, QFEC_VANDERMONDE, RSStruct, QfecError, check, lib
 
 __all__ = ["Code", "FecParms", "ReedSolomon", "QfecError", "QFEC_CAUCHY", "QFEC_VANDERMONDE",
-           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "probe_reconstruct", "device_count", "frame_udp", "unframe_udp",
+           "set_kernel_variant", "tune", "synth_fill", "probe_stream", "probe_reconstruct", "rs_host_devices", "device_count", "frame_udp", "unframe_udp",
            "NetFec", "Pipe", "Zfec"]
 
 
@@ -101,6 +101,19 @@ def synth_fill(t, seed, stream=None):
     """Fill a device uint8 tensor with quicknet_amd.synth.synth_bytes(seed, t.numel())."""
     check(lib().qfec_synth_fill(_dev_ptr(t, what="synth_fill"), t.numel(), seed & 0xFFFFFFFFFFFFFFFF, _stream_handle(stream)),
           "qfec_synth_fill")
+
+
+def rs_host_devices(devices=None):
+    """qfec_rs_host_devices: spread module/rs.h's host-pointer pipelines over two slots per listed
+    device (repeats allowed); None or [] -> the calling thread's current device.  Returns the list
+    now in force."""
+    devs = list(devices or [])
+    arr = (C.c_int * max(1, len(devs)))(*devs)
+    check(lib().qfec_rs_host_devices(arr if devs else None, len(devs)), "qfec_rs_host_devices")
+    out = (C.c_int * 64)()
+    n = lib().qfec_rs_host_devices_get(out, 64)
+    check(min(n, 0), "qfec_rs_host_devices_get")
+    return list(out[:n])
 
 
 def probe_reconstruct(data, parity, marks, block_size, lds_cap=0, stream=None):

@@ -152,6 +152,7 @@ struct Tuning {
     std::atomic<int> host_chunk{0};     // host-buffer paths: groups per pipelined chunk (0: by bytes)
     std::atomic<int> host_threads{0};   // host copy threads for module/rs.h on host pointers (0: usable CPUs, <= 32)
     std::atomic<int> host_zero_copy{1}; // pinned host batches: kernels read/write them directly (0: staged copies)
+    std::atomic<int> host_lanes{4};     // module/rs.h on host pointers: chunk slots in flight on the device (2..8)
     std::atomic<int> encode_lds{-1};    // LDS bytes per encode block, capping waves per CU (-1 auto, 0 none)
 };
 Tuning& tuning();

@@ -177,12 +177,123 @@ uint8_t* rs_slot_dev(DevCtx::HostSlot& h, bool zc) {
     return nullptr;
 }
 
-// reed_solomon_encode over host shard pointers: chunks of groups alternate between two pinned
-// slots; the host threads gather a chunk's data rows into one slot while the device encodes the
-// previous chunk out of the other (reading and writing the pinned slot in place, or through the
-// slot's device buffer), and scatter each chunk's parity rows once its event has fired.
-int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigned char** data, unsigned char** par,
-                   long long G, int B, bool any_stale) {
+// ---- where the host-pointer pipelines run their chunks: host_lanes slots on the calling thread's
+// device (its context's own host slots; 4 by default: at config 2's shape 2 -> 4 slots measured
+// 28.8 -> 33.6 GiB/s, 6 34.4, profiles/r06l), or two slots per entry of the list
+// qfec_rs_host_devices set (own slots per entry, so a device may be listed more than once).  Chunk i takes lane i % lanes; a lane
+// is one slot of one entry, with the entry's device, context and code tables.
+struct RsLane {
+    int device = 0;
+    DevCtx* ctx = nullptr;
+    DevCtx::HostSlot* h = nullptr;
+    const uint32_t* tab = nullptr;  // encode tables on the lane's device
+    const DevTables* d = nullptr;   // LUT and records on the lane's device
+};
+
+struct RsDevList {
+    std::mutex mu;                                      // held by a call for its whole pipeline
+    std::vector<int> devs;                              // empty: the current device
+    std::vector<std::unique_ptr<DevCtx::HostSlot>> slots;  // 2 per entry
+};
+RsDevList& rs_devlist() {
+    static RsDevList* l = new RsDevList();  // never destroyed: no slot freed after the runtime's exit
+    return *l;
+}
+
+void free_slot(DevCtx::HostSlot& h) {
+    if (h.stream) (void)hipStreamSynchronize(h.stream);
+    if (h.d_buf) (void)hipFree(h.d_buf);
+    if (h.h_in) (void)hipHostFree(h.h_in);
+    if (h.h_out) (void)hipHostFree(h.h_out);
+    if (h.done) (void)hipEventDestroy(h.done);
+    if (h.stream) (void)hipStreamDestroy(h.stream);
+    h = DevCtx::HostSlot();
+    (void)hipGetLastError();
+}
+
+struct DeviceBack {  // the caller's current device, put back on every way out
+    int prev = -1;
+    DeviceBack() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~DeviceBack() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+// the lanes of one call, each slot sized for `in_bytes` / `out_bytes` and the code's tables made
+// current on its device (`enc`: encode tables, else LUT + records).  `lk` receives the lock that
+// keeps the slots the call's until it returns.
+int rs_lanes(DevCtx& cur, qfec_code* c, bool enc, size_t in_bytes, size_t out_bytes, std::vector<RsLane>& lanes,
+             std::unique_lock<std::mutex>& lk) {
+    RsDevList& L = rs_devlist();
+    std::unique_lock<std::mutex> ll(L.mu);
+    int rc = QFEC_OK;
+    auto tables = [&](RsLane& ln) -> int {
+        std::lock_guard<std::mutex> cl(c->mu);
+        if (enc) {
+            uint32_t* t = nullptr;
+            const int r = ensure_enc(c, ln.device, &t);
+            ln.tab = t;
+            return r;
+        }
+        DevTables* d = nullptr;
+        const int r = ensure_lut(c, ln.device, &d);
+        ln.d = d;
+        return r;
+    };
+    lanes.clear();
+    if (L.devs.empty()) {
+        ll.unlock();
+        lk = std::unique_lock<std::mutex>(cur.host_mu);
+        const int nl = std::max(2, std::min((int)tuning().host_lanes.load(), kMaxHostLanes));
+        for (int sl = 0; sl < nl; ++sl) {
+            DevCtx::HostSlot& h = cur.host[sl];
+            if ((rc = ensure_host_slot(h, in_bytes, out_bytes))) return rc;
+            RsLane ln;
+            ln.device = cur.device;
+            ln.ctx = &cur;
+            ln.h = &h;
+            if ((rc = tables(ln))) return rc;
+            lanes.push_back(ln);
+        }
+        return QFEC_OK;
+    }
+    for (size_t e = 0; e < L.devs.size(); ++e) {
+        HIP_TRY(hipSetDevice(L.devs[e]));
+        DevCtx* ctx = nullptr;
+        if ((rc = current_ctx(&ctx))) return rc;
+        for (int sl = 0; sl < 2; ++sl) {
+            DevCtx::HostSlot& h = *L.slots[e * 2 + sl];
+            if ((rc = ensure_host_slot(h, in_bytes, out_bytes))) return rc;
+            RsLane ln;
+            ln.device = L.devs[e];
+            ln.ctx = ctx;
+            ln.h = &h;
+            if ((rc = tables(ln))) return rc;
+            lanes.push_back(ln);
+        }
+    }
+    // slot sl of every entry first, so consecutive chunks land on different entries
+    std::vector<RsLane> order;
+    for (int sl = 0; sl < 2; ++sl)
+        for (size_t e = 0; e < L.devs.size(); ++e) order.push_back(lanes[e * 2 + sl]);
+    lanes.swap(order);
+    lk = std::move(ll);
+    return QFEC_OK;
+}
+
+// after an error: wait for whatever the lanes still have in flight
+void quiesce_lanes(std::vector<RsLane>& lanes) {
+    for (auto& ln : lanes) {
+        (void)hipSetDevice(ln.device);
+        if (ln.h->stream) (void)hipStreamSynchronize(ln.h->stream);
+    }
+    (void)hipGetLastError();
+}
+
+// reed_solomon_encode over host shard pointers: chunks of groups go round the lanes; the host
+// threads gather a chunk's data rows into its lane's pinned slot while the devices encode the chunks
+// before it (through the slot's device buffer), and scatter each chunk's parity rows once its event
+// has fired -- the oldest chunk first, once every lane is busy.
+int rs_encode_pipe(DevCtx& ctx, qfec_code* c, unsigned char** data, unsigned char** par, long long G, int B,
+                   bool any_stale) {
     const int k = c->k, m = c->m;
     const size_t pitch = round_up((size_t)B, 16), dg = (size_t)k * pitch, pg = (size_t)m * pitch;
     long long per = tuning().host_chunk > 0 ? (long long)tuning().host_chunk
@@ -190,17 +301,19 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
     per = std::min(per, G);
     const size_t slot_bytes = (size_t)per * (dg + pg);
     std::shared_ptr<HostPool> pool = host_pool();
-    std::lock_guard<std::mutex> lk(ctx.host_mu);
-    int rc = QFEC_OK;
-    for (auto& h : ctx.host)
-        if ((rc = ensure_host_slot(h, slot_bytes, 16))) return rc;
+    DeviceBack back;
+    std::vector<RsLane> lanes;
+    std::unique_lock<std::mutex> lk;
+    int rc = rs_lanes(ctx, c, true, slot_bytes, 16, lanes, lk);
+    if (rc) return rc;
+    const size_t W = lanes.size();
     // staged: the DMA engines move the slot to the device and the parity back.  Reading the
     // freshly gathered slot in place over PCIe ran slower for the encode (26.4-26.9 against
     // 28.3-38.8 GiB/s in alternating processes, profiles/r05af); the reconstruct, which reads only
     // the survivors it needs and writes only the erased rows, stays in place (host_zero_copy)
     const bool zc = false;
     RsTrace tr;
-    long long pending[2] = {-1, -1};
+    std::vector<long long> pending(W, -1);
     auto rows_job = [&](size_t nrows, const std::function<void(size_t)>& row) {
         pool->run(
             [&](int t, int nt) {
@@ -209,24 +322,26 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
             },
             (int)std::max<size_t>(1, nrows / 64));
     };
-    auto drain = [&](int sl) -> int {
-        if (pending[sl] < 0) return QFEC_OK;
-        DevCtx::HostSlot& h = ctx.host[sl];
+    auto drain = [&](size_t ln) -> int {
+        if (pending[ln] < 0) return QFEC_OK;
+        DevCtx::HostSlot& h = *lanes[ln].h;
         auto tw = std::chrono::steady_clock::now();
         HIP_TRY(hipEventSynchronize(h.done));
         tr.wait += RsTrace::since(tw);
         tw = std::chrono::steady_clock::now();
-        const long long g0 = pending[sl], gn = std::min(per, G - g0);
+        const long long g0 = pending[ln], gn = std::min(per, G - g0);
         const uint8_t* hp = h.h_in + (size_t)gn * dg;
         rows_job((size_t)gn * m, [&](size_t i) { memcpy(par[(size_t)g0 * m + i], hp + i * pitch, (size_t)B); });
         tr.scatter += RsTrace::since(tw);
-        pending[sl] = -1;
+        pending[ln] = -1;
         return QFEC_OK;
     };
     const long long nchunks = (G + per - 1) / per;
     for (long long i = 0; i < nchunks && !rc; ++i) {
-        const int sl = (int)(i & 1);
-        DevCtx::HostSlot& h = ctx.host[sl];
+        const size_t ln = (size_t)(i % (long long)W);
+        if ((rc = drain(ln))) break;  // the lane's previous chunk (only when every lane is busy)
+        RsLane& L = lanes[ln];
+        DevCtx::HostSlot& h = *L.h;
         const long long g0 = i * per, gn = std::min(per, G - g0);
         uint8_t* hd = h.h_in;
         uint8_t* hp = h.h_in + (size_t)gn * dg;
@@ -238,36 +353,38 @@ int rs_encode_pipe(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, unsigne
             else memcpy(hp + (r - nd) * pitch, par[(size_t)g0 * m + (r - nd)], (size_t)B);
         });
         tr.gather += RsTrace::since(tg);
+        if (hipSetDevice(L.device) != hipSuccess) { rc = hip_fail(hipGetLastError(), "reed_solomon_encode: device"); break; }
         uint8_t* z = rs_slot_dev(h, zc);
         uint8_t* dd = z ? z : h.d_buf;
         if (!z) {
             const hipError_t e = hipMemcpyAsync(dd, hd, (size_t)gn * dg + np * pitch, hipMemcpyHostToDevice, h.stream);
             if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_encode: H2D"); break; }
         }
-        if ((rc = run_encode(ctx, c, tab, m, dd, dd + (size_t)gn * dg, gn, B, (long long)pitch, h.stream))) break;
+        if ((rc = run_encode(*L.ctx, c, L.tab, m, dd, dd + (size_t)gn * dg, gn, B, (long long)pitch, h.stream))) break;
         if (!z) {
             const hipError_t e = hipMemcpyAsync(hp, dd + (size_t)gn * dg, (size_t)gn * pg, hipMemcpyDeviceToHost, h.stream);
             if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_encode: D2H"); break; }
         }
         const hipError_t e = hipEventRecord(h.done, h.stream);
         if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_encode: event"); break; }
-        pending[sl] = g0;
-        if (i > 0 && (rc = drain(sl ^ 1))) break;  // the previous chunk, while this one runs
+        pending[ln] = g0;
+        // the oldest chunk in flight, while this one runs (two lanes: the previous chunk)
+        if (i + 1 >= (long long)W && (rc = drain((size_t)((i + 1) % (long long)W)))) break;
     }
-    if (!rc) rc = drain((int)((nchunks - 1) & 1));
-    if (rc) quiesce_host_slots(ctx);  // nothing may still be writing into the slots
+    for (size_t j = 0; j < W && !rc; ++j) rc = drain((size_t)((nchunks + (long long)j) % (long long)W));  // oldest first
+    if (rc) quiesce_lanes(lanes);  // nothing may still be writing into the slots
     tr.report("reed_solomon_encode (host)", nchunks, pool->threads());
     return rc;
 }
 
-// reed_solomon_reconstruct over host shard pointers (k + m <= QFEC_LUT_MAX_N): the same two-slot
-// pipeline.  Per group only what the decode reads is staged -- the surviving data rows and the
-// first e surviving parity rows (rs.c:611-629), plus the erased rows where the pattern's record
-// seeds a row from its old bytes (the rs.c quirk) -- with the chunk's marks in rs.c layout; the
-// LUT kernel decodes and only the erased data rows of recoverable groups are scattered back.
-// Groups with more erased data than surviving parity are left untouched and counted (*nfail).
-int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uint8_t* seed, unsigned char** data,
-                        unsigned char** par, const uint8_t* mk, long long G, int B, long long* nfail) {
+// reed_solomon_reconstruct over host shard pointers (k + m <= QFEC_LUT_MAX_N): the same lanes.  Per
+// group only what the decode reads is staged -- the surviving data rows and the first e surviving
+// parity rows (rs.c:611-629), plus the erased rows where the pattern's record seeds a row from its
+// old bytes (the rs.c quirk) -- with the chunk's marks in rs.c layout; the LUT kernel decodes and
+// only the erased data rows of recoverable groups are scattered back.  Groups with more erased data
+// than surviving parity are left untouched and counted (*nfail).
+int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const uint8_t* seed, unsigned char** data, unsigned char** par,
+                        const uint8_t* mk, long long G, int B, long long* nfail) {
     const int k = c->k, m = c->m, n = k + m;
     const size_t pitch = round_up((size_t)B, 16), dg = (size_t)k * pitch, pg = (size_t)m * pitch;
     long long per = tuning().host_chunk > 0 ? (long long)tuning().host_chunk
@@ -275,28 +392,30 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
     per = std::min(per, G);
     const size_t mk_off = (size_t)per * (dg + pg), slot_bytes = round_up(mk_off + (size_t)per * n, 16);
     std::shared_ptr<HostPool> pool = host_pool();
-    std::lock_guard<std::mutex> lk(ctx.host_mu);
-    int rc = QFEC_OK;
-    for (auto& h : ctx.host)
-        if ((rc = ensure_host_slot(h, slot_bytes, 16))) return rc;
+    DeviceBack back;
+    std::vector<RsLane> lanes;
+    std::unique_lock<std::mutex> lk;
+    int rc = rs_lanes(ctx, c, false, slot_bytes, 16, lanes, lk);
+    if (rc) return rc;
+    const size_t W = lanes.size();
     const bool zc = tuning().host_zero_copy != 0;
     RsTrace tr;
-    std::vector<uint8_t> todo[2];  // per slot, per group: 1 = decoded (scatter its erased data rows)
-    long long pending[2] = {-1, -1};
+    std::vector<std::vector<uint8_t>> todo(W);  // per lane, per group: 1 = decoded (scatter its erased data rows)
+    std::vector<long long> pending(W, -1);
     std::atomic<long long> fails{0};
     auto groups_job = [&](long long gn, const std::function<void(long long, long long)>& span) {
         pool->run(
             [&](int t, int nt) { span(gn * t / nt, gn * (t + 1) / nt); }, (int)std::max<long long>(1, gn / 16));
     };
-    auto drain = [&](int sl) -> int {
-        if (pending[sl] < 0) return QFEC_OK;
-        DevCtx::HostSlot& h = ctx.host[sl];
+    auto drain = [&](size_t ln) -> int {
+        if (pending[ln] < 0) return QFEC_OK;
+        DevCtx::HostSlot& h = *lanes[ln].h;
         auto tw = std::chrono::steady_clock::now();
         HIP_TRY(hipEventSynchronize(h.done));
         tr.wait += RsTrace::since(tw);
         tw = std::chrono::steady_clock::now();
-        const long long g0 = pending[sl], gn = std::min(per, G - g0);
-        const uint8_t* todo_s = todo[sl].data();
+        const long long g0 = pending[ln], gn = std::min(per, G - g0);
+        const uint8_t* todo_s = todo[ln].data();
         const uint8_t* hd = h.h_in;
         groups_job(gn, [&](long long a, long long b) {
             for (long long g = a; g < b; ++g) {
@@ -307,19 +426,21 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
             }
         });
         tr.scatter += RsTrace::since(tw);
-        pending[sl] = -1;
+        pending[ln] = -1;
         return QFEC_OK;
     };
     const long long nchunks = (G + per - 1) / per;
     for (long long i = 0; i < nchunks && !rc; ++i) {
-        const int sl = (int)(i & 1);
-        DevCtx::HostSlot& h = ctx.host[sl];
+        const size_t ln = (size_t)(i % (long long)W);
+        if ((rc = drain(ln))) break;
+        RsLane& L = lanes[ln];
+        DevCtx::HostSlot& h = *L.h;
         const long long g0 = i * per, gn = std::min(per, G - g0);
         uint8_t* hd = h.h_in;
         uint8_t* hp = h.h_in + (size_t)gn * dg;
         uint8_t* hm = h.h_in + (size_t)gn * (dg + pg);
-        todo[sl].assign((size_t)gn, 0);
-        uint8_t* todo_s = todo[sl].data();
+        todo[ln].assign((size_t)gn, 0);
+        uint8_t* todo_s = todo[ln].data();
         const auto tg = std::chrono::steady_clock::now();
         groups_job(gn, [&](long long a, long long b) {
             long long nf = 0;
@@ -354,6 +475,10 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
             fails += nf;
         });
         tr.gather += RsTrace::since(tg);
+        if (hipSetDevice(L.device) != hipSuccess) {
+            rc = hip_fail(hipGetLastError(), "reed_solomon_reconstruct: device");
+            break;
+        }
         uint8_t* z = rs_slot_dev(h, zc);
         uint8_t* dd = z ? z : h.d_buf;
         const size_t used = (size_t)gn * (dg + pg + n);
@@ -361,7 +486,7 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
             const hipError_t e = hipMemcpyAsync(dd, h.h_in, used, hipMemcpyHostToDevice, h.stream);
             if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_reconstruct: H2D"); break; }
         }
-        if ((rc = run_reconstruct(ctx, c, d->d_lut, nullptr, d->d_rec, dd, dd + (size_t)gn * dg,
+        if ((rc = run_reconstruct(*L.ctx, c, L.d->d_lut, nullptr, L.d->d_rec, dd, dd + (size_t)gn * dg,
                                   dd + (size_t)gn * (dg + pg), gn, B, (long long)pitch, nullptr, h.stream)))
             break;
         if (!z) {
@@ -370,11 +495,11 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const DevTables* d, const uin
         }
         const hipError_t e = hipEventRecord(h.done, h.stream);
         if (e != hipSuccess) { rc = hip_fail(e, "reed_solomon_reconstruct: event"); break; }
-        pending[sl] = g0;
-        if (i > 0 && (rc = drain(sl ^ 1))) break;
+        pending[ln] = g0;
+        if (i + 1 >= (long long)W && (rc = drain((size_t)((i + 1) % (long long)W)))) break;
     }
-    if (!rc) rc = drain((int)((nchunks - 1) & 1));
-    if (rc) quiesce_host_slots(ctx);
+    for (size_t j = 0; j < W && !rc; ++j) rc = drain((size_t)((nchunks + (long long)j) % (long long)W));
+    if (rc) quiesce_lanes(lanes);
     *nfail = fails.load();
     tr.report("reed_solomon_reconstruct (host)", nchunks, pool->threads());
     return rc;
@@ -411,6 +536,43 @@ void sync_rows(rs_handle* h) {
 }  // namespace
 
 extern "C" {
+
+int qfec_rs_host_devices(const int* devices, int n) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        (void)hipGetLastError();
+        set_error("qfec_rs_host_devices: no HIP device available");
+        return QFEC_ENODEV;
+    }
+    if (n < 0 || n > 64 || (n > 0 && !devices)) {
+        set_error("qfec_rs_host_devices: invalid argument");
+        return QFEC_EINVAL;
+    }
+    for (int i = 0; i < n; ++i)
+        if (devices[i] < 0 || devices[i] >= count || devices[i] >= kMaxDevices) {
+            set_error("qfec_rs_host_devices: device %d out of range (%d visible)", devices[i], count);
+            return QFEC_EINVAL;
+        }
+    RsDevList& L = rs_devlist();
+    std::lock_guard<std::mutex> lk(L.mu);  // no pipeline is using the slots
+    DeviceBack back;
+    for (size_t i = 0; i < L.slots.size(); ++i) {
+        (void)hipSetDevice(L.devs[i / 2]);
+        free_slot(*L.slots[i]);
+    }
+    L.devs.assign(devices, devices + n);
+    L.slots.clear();
+    for (int i = 0; i < 2 * n; ++i) L.slots.emplace_back(new DevCtx::HostSlot());
+    return QFEC_OK;
+}
+
+int qfec_rs_host_devices_get(int* devices, int cap) {
+    if (cap < 0 || (cap > 0 && !devices)) return QFEC_EINVAL;
+    RsDevList& L = rs_devlist();
+    std::lock_guard<std::mutex> lk(L.mu);
+    for (int i = 0; i < cap && i < (int)L.devs.size(); ++i) devices[i] = L.devs[i];
+    return (int)L.devs.size();
+}
 
 void reed_solomon_init(void) {
     std::call_once(g_rs_init_once, [] { (void)field(); });
@@ -502,7 +664,7 @@ int reed_solomon_encode(reed_solomon* rs, unsigned char** shards, int nr_shards,
     const size_t ndev = classify_ptrs(shards, nptr, *pool, kind.data());
     t_rs_classify = RsTrace::since(tc);
     if (ndev == 0) {
-        rc = rs_encode_pipe(*ctx, c, tab, data, par, G, block_size, any_stale);
+        rc = rs_encode_pipe(*ctx, c, data, par, G, block_size, any_stale);
         if (rc) fprintf(stderr, "[qfec] reed_solomon_encode: %s\n", qfec_last_error());
         return rc;
     }
@@ -589,7 +751,7 @@ int reed_solomon_reconstruct(reed_solomon* rs, unsigned char** shards, unsigned 
             rc = ensure_lut(c, ctx->device, &d);
             if (!rc) seed = c->lut_seed;
         }
-        if (!rc) rc = rs_reconstruct_pipe(*ctx, c, d, seed->data(), data, par, mk, G, block_size, &nfail_all);
+        if (!rc) rc = rs_reconstruct_pipe(*ctx, c, seed->data(), data, par, mk, G, block_size, &nfail_all);
         if (rc) {
             fprintf(stderr, "[qfec] reed_solomon_reconstruct: %s\n", qfec_last_error());
             return rc;

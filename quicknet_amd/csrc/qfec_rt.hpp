@@ -58,6 +58,7 @@ extern std::atomic<unsigned long long> g_group_hits, g_group_misses;
 
 // ---- device contexts (qfec_runtime.cpp)
 constexpr int kMaxDevices = 64;
+constexpr int kMaxHostLanes = 8;  // host-buffer chunk slots per device context
 
 struct DevCtx {
     int device = 0;
@@ -104,8 +105,9 @@ struct DevCtx {
         unsigned long long tr[7] = {0, 0, 0, 0, 0, 0, 0};
     } srv;
     int init_rc = QFEC_ENODEV;
-    // qfec_encode_host: two chunk slots, each with its own stream, event, device buffers
-    // and pinned staging (created on first use)
+    // host-buffer chunk slots, each with its own stream, event, device buffers and pinned staging
+    // (created on first use): qfec_encode_host / qfec_reconstruct_host alternate host[0] and host[1];
+    // module/rs.h's host-pointer pipelines take the first tuning "host_lanes" of them
     struct HostSlot {
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
@@ -113,7 +115,7 @@ struct DevCtx {
         uint8_t* h_in = nullptr;   // pinned
         uint8_t* h_out = nullptr;  // pinned
         size_t in_cap = 0, out_cap = 0;
-    } host[2];
+    } host[kMaxHostLanes];
     std::mutex host_mu;
 };
 

@@ -649,6 +649,7 @@ const std::vector<Knob>& knob_table() {
         {"wire_fused", &tuning().wire_fused, 0, 1},
         {"wire_rx", &tuning().wire_rx, 0, 5},
         {"host_zero_copy", &tuning().host_zero_copy, 0, 1},
+        {"host_lanes", &tuning().host_lanes, 2, 8},
         {"percall_fast", &g_percall_fast, 0, 1},
         {"percall_group", &g_percall_group, 0, 1},
         {"percall_fault", &g_percall_fault, 0, 2},
@@ -843,8 +844,8 @@ int qfec_encode_host(qfec_code* code, const unsigned char* h_data, unsigned char
         if (!rc && e != hipSuccess) rc = hip_fail(e, "qfec_encode_host: zero-copy encode");
         return rc;
     }
-    for (auto& h : ctx->host)
-        if ((rc = ensure_host_slot(h, (size_t)gc * in_g, (size_t)gc * out_g))) return rc;
+    for (int sl = 0; sl < 2; ++sl)
+        if ((rc = ensure_host_slot(ctx->host[sl], (size_t)gc * in_g, (size_t)gc * out_g))) return rc;
     long long pending[2] = {-1, -1};  // chunk whose parity sits in the slot's staging
     auto drain = [&](int sl) -> int {
         if (pending[sl] < 0) return QFEC_OK;
@@ -941,8 +942,8 @@ int qfec_reconstruct_host(qfec_code* code, unsigned char* h_data, const unsigned
         if (!rc && failed) *failed = *reinterpret_cast<const unsigned*>(h.h_out);
         return rc;
     }
-    for (auto& h : ctx->host)
-        if ((rc = ensure_host_slot(h, slot_bytes, slot_bytes))) return rc;
+    for (int sl = 0; sl < 2; ++sl)
+        if ((rc = ensure_host_slot(ctx->host[sl], slot_bytes, slot_bytes))) return rc;
     long long pending[2] = {-1, -1};
     long long nfail = 0;
     auto drain = [&](int sl) -> int {

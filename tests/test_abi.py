@@ -120,6 +120,8 @@ def test_no_gpu_fails_loudly():
     data = np.zeros((1, 4, 16), np.uint8)
     par = np.zeros((1, 2, 16), np.uint8)
     assert rs.encode(data, par, 16) != 0
+    arr = (C.c_int * 2)(0, 0)
+    assert L.qfec_rs_host_devices(arr, 2) == -2  # no device to list
 
 
 def test_net_layer_host_side():

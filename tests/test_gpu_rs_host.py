@@ -62,12 +62,14 @@ def mixed_marks(G, k, m, seed):
 
 
 @pytest.mark.parametrize("k,m,B", [(10, 3, 1000), (4, 2, 1024), (16, 4, 1400)])
-@pytest.mark.parametrize("chunk,threads", [(7, 4), (0, 0), (1, 1)])
-def test_rs_host_encode_pipeline_vs_oracle(oracle, knobs, k, m, B, chunk, threads):
+@pytest.mark.parametrize("chunk,threads,lanes", [(7, 4, 2), (0, 0, 4), (1, 1, 8)])
+def test_rs_host_encode_pipeline_vs_oracle(oracle, knobs, k, m, B, chunk, threads, lanes):
     """reed_solomon_encode on host pointers: many pipelined chunks (host_chunk groups each, two slots
     alternating), 1 to 4 copy threads; shard rows scattered in memory.  The encode leg always stages
     each chunk through the slot's device buffer (reading the pinned slot in place over PCIe measured
-    slower, profiles/r05af), so host_zero_copy does not apply to it and is not varied here."""
+    slower, profiles/r05af), so host_zero_copy does not apply to it and is not varied here.  2, 4 or 8
+    chunks in flight (host_lanes)."""
+    knobs("host_lanes", lanes)
     knobs("host_chunk", chunk)
     knobs("host_threads", threads)
     G, n = 61, k + m
@@ -87,12 +89,13 @@ def test_rs_host_encode_pipeline_vs_oracle(oracle, knobs, k, m, B, chunk, thread
 
 @pytest.mark.parametrize("k,m,B", [(10, 3, 1000), (4, 2, 1024), (16, 4, 1400)])
 @pytest.mark.parametrize("zero_copy", [1, 0])
-@pytest.mark.parametrize("chunk,threads", [(7, 4), (0, 0), (1, 1)])
-def test_rs_host_reconstruct_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_copy, chunk, threads):
+@pytest.mark.parametrize("chunk,threads,lanes", [(7, 4, 8), (0, 0, 4), (1, 1, 2)])
+def test_rs_host_reconstruct_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_copy, chunk, threads, lanes):
     """reed_solomon_reconstruct on host pointers: many pipelined chunks, 1 to 4 copy threads, the
     kernel reading the survivors and writing the erased rows in the pinned slot in place (zero copy)
     or through the slot's device buffer; inconsistent parity (pins the survivor rule byte for byte),
-    erased rows pre-filled with 0x5A, unrecoverable groups."""
+    erased rows pre-filled with 0x5A, unrecoverable groups; 2, 4 or 8 chunks in flight."""
+    knobs("host_lanes", lanes)
     knobs("host_zero_copy", zero_copy)
     knobs("host_chunk", chunk)
     knobs("host_threads", threads)
@@ -304,7 +307,7 @@ def test_rs_host_while_tuning(oracle):
     """Encodes and reconstructs on host pointers from two threads while a third flips the host
     knobs (chunking, copy threads, zero copy): every result still equals the oracle's."""
     import threading
-    keys = ("host_chunk", "host_threads", "host_zero_copy")
+    keys = ("host_chunk", "host_threads", "host_zero_copy", "host_lanes")
     before = {k: qa.tune_get(k) for k in keys}
     stop = threading.Event()
     errors = []
@@ -315,6 +318,7 @@ def test_rs_host_while_tuning(oracle):
             qa.tune("host_chunk", (0, 3, 17)[i % 3])
             qa.tune("host_threads", (0, 1, 3)[i % 3])
             qa.tune("host_zero_copy", i & 1)
+            qa.tune("host_lanes", (2, 4, 8)[i % 3])
             i += 1
 
     def coder(seed):
@@ -465,15 +469,26 @@ def _ref_codec():
     return RefCodec()
 
 
+@pytest.fixture
+def devlist():
+    """Set qfec_rs_host_devices for one test, back to the current device afterwards."""
+    yield qa.rs_host_devices
+    qa.rs_host_devices(None)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0], [0, 0, 0]])
 @pytest.mark.parametrize("k,m,B,G,edit", [(10, 3, 1000, 61, False), (10, 3, 1024, 40, True), (16, 4, 1400, 37, True),
                                           (4, 2, 37, 200, True), (20, 5, 256, 50, False), (3, 2, 33, 90, True)])
-def test_rs_host_pipeline_vs_reference_rs(knobs, k, m, B, G, edit):
+def test_rs_host_pipeline_vs_reference_rs(knobs, devlist, k, m, B, G, edit, devices):
     """The pipelined host path against the reference's own module/rs.c (oracle/_ref, compiled from
     /root/reference) on identical scattered rows: the same public-matrix edits on both handles
     (a zero column-0 coefficient, an edited row of rs->m), encode, then reconstruct with 0..m+1
-    erasures per group (unrecoverable groups included) -- bytes and return codes equal."""
+    erasures per group (unrecoverable groups included) -- bytes and return codes equal.  Chunks on
+    the current device's two slots, or spread over qfec_rs_host_devices' lanes (device 0 listed two
+    or three times: four or six chunks in flight, the multi-GPU path's control flow on one GPU)."""
     ref = _ref_codec()
     knobs("host_chunk", 9)
+    assert devlist(devices) == (devices or [])
     n = k + m
     rng = np.random.default_rng(k * 1000 + B)
     rows, _keep = scattered_rows(G, n, B, k + B)

@@ -7,13 +7,15 @@
 #   ab K M B G ONLY [ARGS...]
 #                         tools/ab.py interleaved A/B (ONLY: comma-separated variant prefixes)
 #   bench [ARGS...]       bench.py -> TAG/bench.json (stderr TAG/bench.err)
-#   kstats [ARGS...]      rocprofv3 --kernel-trace --stats over bench.py -> TAG/prof/, summary TAG/kernel_stats.csv
+#   kstats [ARGS...]      rocprofv3 --kernel-trace --stats over bench.py --no-cpu --no-host --no-side -> TAG/prof/,
+#                         summary TAG/kernel_stats.csv
 #   pmc NAME K M B G [ARGS...]
 #                         tools/pmc_traffic.py (separate --pmc passes per counter group) -> TAG/traffic_NAME.json
 #   sq NAME SCRIPT [ARGS...]
 #                         SQ counters per kernel (two --pmc passes over python SCRIPT) -> TAG/NAME_sq_summary.txt
 #   smoke                 __graft_entry__.smoke()
 #   py NAME SECS ARGS...  any python command (tools/*.py), log TAG/NAME.log
+#   pyenv NAME SECS VAR=VALUE ARGS...  the same with one environment variable set
 set -o pipefail
 TAG=${1:?tag}; shift
 OUT=gpurun_out/$TAG
@@ -44,7 +46,10 @@ for spec in "$@"; do
       if [ $rc -ne 0 ]; then tail -30 $OUT/bench.err; exit $rc; fi ;;
     kstats)
       echo "== rocprofv3 kernel stats"
-      timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --no-cpu "$@" > $OUT/kstats.log 2>&1
+      # only the timed step's launches and config 4's (the host / per-call / side legs launch the same
+      # kernels at other sizes), so each kernel's average is the one bench.py reports
+      timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+        python3 bench.py --no-cpu --no-host --no-side "$@" > $OUT/kstats.log 2>&1
       rc=$?; echo "   rc=$rc"; tail -3 $OUT/kstats.log
       if [ $rc -ne 0 ]; then exit $rc; fi
       f=$(find $OUT/prof -name '*kernel_stats.csv' | head -1)
@@ -75,6 +80,10 @@ for spec in "$@"; do
     py)
       name=$1 secs=$2; shift 2
       step $name $secs python -u "$@" ;;
+    pyenv)
+      # pyenv NAME SECS VAR=VALUE SCRIPT [ARGS...]: the same with one environment variable set
+      name=$1 secs=$2 var=$3; shift 3
+      step $name $secs env "$var" python -u "$@" ;;
     *)
       echo "unknown step '$what'"; exit 2 ;;
   esac

@@ -63,13 +63,17 @@ def main():
     p.add_argument("--erasures", type=int, default=3, help="erasures per group (bench.py --erasures); key suffix _eN "
                                                            "when not 3 (config 4: 4, read by bench.py's config4 field)")
     p.add_argument("--tag", default="PMC run", help="which run produced the numbers (recorded in the JSON)")
-    p.add_argument("--workload", choices=["headline", "wire"], default="headline")
+    p.add_argument("--workload", choices=["headline", "wire", "config4"], default="headline",
+                   help="headline: bench.py's timed step; config4: its RS(16,4) config 4 leg alone (key "
+                        "rs16_4_b1400_g<G>_e4, read by the line's config4 field); wire: the datagram leg")
     p.add_argument("--csv-home", default=None,
                    help="where the counter CSVs are kept in the repository (default profiles/<tag>/pmc): recorded "
                         "in the JSON so the bench line names tracked files whether or not they travel to the box")
     a = p.parse_args()
     if a.workload == "wire":
         return wire_main(a)
+    if a.workload == "config4":
+        return config4_main(a)
     bench_args = ["--steps", "5", "--warmup", "1", "--k", str(a.k), "--m", str(a.m), "--block", str(a.block),
                   "--groups", str(a.groups), "--erasures", str(a.erasures), "--no-side", "--no-config4", "--no-host"]
     fetch = run_pass("FETCH_SIZE", a.out, bench_args, a.k, a.m)
@@ -105,6 +109,41 @@ def main():
         "csv": a.csv_home or f"profiles/{a.tag}/pmc",
     }
     os.makedirs(os.path.dirname(a.json), exist_ok=True)
+    with open(a.json, "w") as fh:
+        json.dump(doc, fh, indent=1)
+    print(json.dumps(doc[key], indent=1))
+
+
+def config4_main(a):
+    """PMC bytes per launch of bench.py's config 4 leg (RS(16,4) 1400 B, 4 erasures, --config4-groups
+    groups on one rank): its encode (inputs in halves) and reconstruct (8-B lanes, one group per block)."""
+    G = a.groups
+    kernels = {"encode": "k_encode_perm_halves<16, 4>", "reconstruct": "k_reconstruct_perm<16, 4, 8>"}
+    args = ["--config4-only", "--config4-groups", str(G), "--steps", "5", "--warmup", "1"]
+    fetch = run_pass("FETCH_SIZE", a.out, args, 16, 4, kernels)
+    write = run_pass("WRITE_SIZE", a.out, args, 16, 4, kernels)
+    res = {}
+    for key in kernels:
+        if not fetch[key] or not write[key]:
+            print(f"no PMC rows for {kernels[key]}", file=sys.stderr)
+            return 1
+        f = sum(fetch[key]) / len(fetch[key])
+        w = sum(write[key]) / len(write[key])
+        res[key] = {"fetch_kib_raw": f, "write_kib_raw": w, "read_bytes": 2 * f * 1024, "write_bytes": w * 1024,
+                    "bytes_per_launch": 2 * f * 1024 + w * 1024, "launches": len(fetch[key])}
+    doc = {}
+    if os.path.exists(a.json):
+        with open(a.json) as fh:
+            doc = json.load(fh)
+    sys.path.insert(0, ROOT)
+    from bench import kernel_sources_hash
+    key = f"rs16_4_b1400_g{G}_e4"
+    doc[key] = {"kernel_sources_sha256": kernel_sources_hash(), "run": a.tag,
+                "encode_bytes_per_launch": res["encode"]["bytes_per_launch"],
+                "reconstruct_bytes_per_launch": res["reconstruct"]["bytes_per_launch"],
+                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py "
+                          "--config4-only; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 corrections)",
+                "raw": res, "csv": a.csv_home or f"profiles/{a.tag}/pmc"}
     with open(a.json, "w") as fh:
         json.dump(doc, fh, indent=1)
     print(json.dumps(doc[key], indent=1))

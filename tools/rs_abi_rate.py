@@ -3,7 +3,7 @@
 per-shard pointers into pageable host memory (RS(10,3) 1 KiB, config 2's shape).  For before/after
 A/B of libqfec builds (tools/ab_lib.sh with QFEC_LIB / QFEC_LIB_COMPAT) and knob sweeps.
 
-  python tools/rs_abi_rate.py [--groups 100000] [--reps 3] [--threads 0] [--chunk 0] [--zero-copy 1]
+  python tools/rs_abi_rate.py [--groups 100000] [--reps 3] [--threads 0] [--chunk 0] [--zero-copy 1] [--devices 0,0]
 """
 import argparse
 import json
@@ -26,6 +26,7 @@ def main():
     p.add_argument("--threads", type=int, default=None)
     p.add_argument("--chunk", type=int, default=None)
     p.add_argument("--zero-copy", type=int, default=None)
+    p.add_argument("--devices", default="", help="qfec_rs_host_devices list, e.g. 0,0 (default: the current device)")
     a = p.parse_args()
     torch.cuda.set_device(0)
     for key, v in (("host_threads", a.threads), ("host_chunk", a.chunk), ("host_zero_copy", a.zero_copy)):
@@ -34,6 +35,8 @@ def main():
                 qa.tune(key, v)
             except Exception as exc:
                 print(f"# {key}: {exc}", file=sys.stderr)
+    if a.devices:
+        print("# rs_host_devices", qa.rs_host_devices([int(x) for x in a.devices.split(",")]), file=sys.stderr)
     r = rs_abi_host_leg(G=a.groups, reps=a.reps)
     r.pop("_sample", None)
     print(json.dumps(r), flush=True)
