@@ -14,6 +14,12 @@
 #   sq NAME SCRIPT [ARGS...]
 #                         SQ counters per kernel (two --pmc passes over python SCRIPT) -> TAG/NAME_sq_summary.txt
 #   smoke                 __graft_entry__.smoke()
+#   bench2                bench.py --gpus 2 with gloo (the launcher's two ranks share the one GPU) -> TAG/bench_g2.json
+#   wirestats             rocprofv3 kernel stats of the datagram kernels at the wire leg's shapes -> TAG/wire_kernel_stats.csv
+#   merge_traffic         the TAG/traffic_*.json entries of earlier pmc steps into profiles/traffic.json (on the box,
+#                         so a later bench step reads them; copy it back from TAG/traffic.json)
+#   closing               the end-of-round pass: tests all, smoke, pmc h / c4 / wire, merge_traffic, bench, kstats,
+#                         wirestats, bench2 (the steps of the former tools/gpu_full.sh + gpu_final.sh)
 #   py NAME SECS ARGS...  any python command (tools/*.py), log TAG/NAME.log
 #   pyenv NAME SECS VAR=VALUE ARGS...  the same with one environment variable set
 set -o pipefail
@@ -23,7 +29,16 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 source tools/gpu_step.sh
 n=0
+specs=()
 for spec in "$@"; do
+  if [ "$spec" = closing ]; then
+    specs+=("tests all" smoke "pmc h 10 3 1024 100000" "pmc c4 16 4 1400 250000 --workload config4"
+            "pmc wire 10 3 1024 100000 --workload wire" merge_traffic bench kstats wirestats bench2)
+  else
+    specs+=("$spec")
+  fi
+done
+for spec in "${specs[@]}"; do
   n=$((n + 1))
   set -- $spec
   what=$1; shift
@@ -75,6 +90,35 @@ for spec in "$@"; do
       done
       python3 tools/sq_summary.py $OUT/${name}_sq1 $OUT/${name}_sq2 > $OUT/${name}_sq_summary.txt
       cat $OUT/${name}_sq_summary.txt ;;
+    bench2)
+      echo "== bench --gpus 2 (gloo)"
+      QFEC_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 20 --no-cpu > $OUT/bench_g2.json 2> $OUT/bench_g2.err
+      rc=$?; echo "   rc=$rc"; cut -c1-400 $OUT/bench_g2.json
+      if [ $rc -ne 0 ]; then tail -20 $OUT/bench_g2.err; exit $rc; fi ;;
+    wirestats)
+      echo "== rocprofv3 kernel stats, datagram kernels (tools/side_legs.py)"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_wire -o wire -- \
+        python3 tools/side_legs.py --steps 100 > $OUT/side_prof.json 2> $OUT/side_prof.err
+      rc=$?; echo "   rc=$rc"
+      if [ $rc -ne 0 ]; then tail -20 $OUT/side_prof.err; exit $rc; fi
+      f=$(find $OUT/prof_wire -name '*kernel_stats.csv' | head -1)
+      [ -n "$f" ] && cp "$f" $OUT/wire_kernel_stats.csv && cut -d, -f1-5 $OUT/wire_kernel_stats.csv | cut -c1-160 | head -10 ;;
+    merge_traffic)
+      python3 - "$OUT" <<'PY' || exit 11
+import glob, json, os, sys
+out = sys.argv[1]
+main = json.load(open("profiles/traffic.json"))
+for f in sorted(glob.glob(os.path.join(out, "traffic_*.json"))):
+    name = os.path.basename(f)[len("traffic_"):-len(".json")]
+    for key, ent in json.load(open(f)).items():
+        if ent.get("run") == os.path.basename(out):
+            ent["csv"] = f"profiles/{os.path.basename(out)}/pmc/{name}"
+            main[key] = ent
+            print("merged", key, "from", f)
+json.dump(main, open("profiles/traffic.json", "w"), indent=1)
+json.dump(main, open(os.path.join(out, "traffic.json"), "w"), indent=1)
+PY
+      ;;
     smoke)
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     py)
