@@ -178,8 +178,8 @@ uint8_t* rs_slot_dev(DevCtx::HostSlot& h, bool zc) {
 }
 
 // ---- where the host-pointer pipelines run their chunks: host_lanes slots on the calling thread's
-// device (its context's own host slots; 4 by default: at config 2's shape 2 -> 4 slots measured
-// 28.8 -> 33.6 GiB/s, 6 34.4, profiles/r06l), or two slots per entry of the list
+// device (its context's own host slots; 4 by default: at config 2's shape, interleaved in one
+// process, 2 / 4 / 6 / 8 slots 35.6 / 43.3 / 43.4 / 42.7 GiB/s, profiles/r06o), or two slots per entry of the list
 // qfec_rs_host_devices set (own slots per entry, so a device may be listed more than once).  Chunk i takes lane i % lanes; a lane
 // is one slot of one entry, with the entry's device, context and code tables.
 struct RsLane {

@@ -26,7 +26,6 @@ def main():
     p.add_argument("--threads", type=int, default=None)
     p.add_argument("--chunk", type=int, default=None)
     p.add_argument("--zero-copy", type=int, default=None)
-    p.add_argument("--prefetch", type=int, default=None)
     p.add_argument("--lanes", type=int, default=None)
     p.add_argument("--ab", default="", help="KNOB=V1,V2,...: interleaved in-process A/B of a host knob")
     p.add_argument("--rounds", type=int, default=8)
@@ -35,7 +34,7 @@ def main():
     a = p.parse_args()
     torch.cuda.set_device(0)
     for key, v in (("host_threads", a.threads), ("host_chunk", a.chunk), ("host_zero_copy", a.zero_copy),
-                   ("host_prefetch", a.prefetch), ("host_lanes", a.lanes)):
+                   ("host_lanes", a.lanes)):
         if v is not None:
             try:
                 qa.tune(key, v)
