@@ -18,9 +18,11 @@ from zfec_script import PAIRS, make_script, replay, run_oracle
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tests", "zfec_host", "_build", "libzfec_host.so")
-SRCS = [os.path.join(ROOT, "quicknet_amd", "csrc", "qfec_zfec.cpp"), os.path.join(ROOT, "tests", "zfec_host", "stubs.cpp"),
-        os.path.join(ROOT, "quicknet_amd", "csrc", "qfec_pool.cpp"), os.path.join(ROOT, "quicknet_amd", "csrc", "qfec_pool.hpp"),
-        os.path.join(ROOT, "include", "qfec_zfec.h"), os.path.join(ROOT, "include", "qfec.h")]
+CSRC = os.path.join(ROOT, "quicknet_amd", "csrc")
+SRCS = [os.path.join(CSRC, "qfec_zfec.cpp"), os.path.join(CSRC, "qfec_zfec_flush.cpp"),
+        os.path.join(ROOT, "tests", "zfec_host", "stubs.cpp"), os.path.join(CSRC, "qfec_pool.cpp")]
+DEPS = SRCS + [os.path.join(CSRC, "qfec_zfec_impl.hpp"), os.path.join(CSRC, "qfec_pool.hpp"),
+               os.path.join(ROOT, "include", "qfec_zfec.h"), os.path.join(ROOT, "include", "qfec.h")]
 ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
 
 pytestmark = pytest.mark.skipif(not (zfec_ref.available() and os.path.exists(ORACLE_LIB)),
@@ -29,10 +31,10 @@ pytestmark = pytest.mark.skipif(not (zfec_ref.available() and os.path.exists(ORA
 
 @pytest.fixture(scope="module")
 def host_layer():
-    if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(s) for s in SRCS):
+    if not os.path.exists(OUT) or os.path.getmtime(OUT) < max(os.path.getmtime(s) for s in DEPS):
         os.makedirs(os.path.dirname(OUT), exist_ok=True)
         subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-                        "-o", OUT, SRCS[0], SRCS[1], SRCS[2], "-lpthread", "-L" + os.path.dirname(ORACLE_LIB), "-loracle",
+                        "-o", OUT] + SRCS + ["-lpthread", "-L" + os.path.dirname(ORACLE_LIB), "-loracle",
                         "-Wl,-rpath," + os.path.dirname(ORACLE_LIB)], check=True)
     from quicknet_amd._lib import bind_zfec
     return bind_zfec(C.CDLL(OUT))
