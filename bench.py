@@ -63,7 +63,8 @@ GIB = float(1 << 30)
 KERNEL_SOURCES = ("quicknet_amd/csrc/qfec_kernels.hip", "quicknet_amd/csrc/qfec_internal.hpp",
                   "quicknet_amd/csrc/qfec_device.hpp")
 # ... and those of the datagram / framing legs (their own traffic.json entry)
-WIRE_KERNEL_SOURCES = KERNEL_SOURCES + ("quicknet_amd/csrc/qfec_wire.hip", "quicknet_amd/csrc/qfec_rx.hip")
+WIRE_KERNEL_SOURCES = KERNEL_SOURCES + ("quicknet_amd/csrc/qfec_wire.hip", "quicknet_amd/csrc/qfec_rx.hip",
+                                        "quicknet_amd/csrc/qfec_frame.hip", "quicknet_amd/csrc/qfec_wire_device.hpp")
 TRAFFIC_PATH = os.path.join(ROOT, "profiles", "traffic.json")
 
 
