@@ -256,6 +256,9 @@ int qfec_probe_reconstruct(unsigned char *d_data, const unsigned char *d_parity,
  *                      measured faster for a freshly gathered slot)
  *   "host_lanes"       4 (default) | 2 .. 8: module/rs.h on host pointers, chunk slots in flight on the
  *                      current device; qfec_rs_host_devices spreads them over listed devices instead
+ *   "host_nt"          2 (default) | 1 | 0: module/rs.h on host pointers, streaming (non-temporal) stores
+ *                      when gathering caller rows into a slot: 2 for rows that start where the previous
+ *                      row ended, 1 for every row, 0 never
  *   "host_chunk"       groups per staged host chunk (0: by bytes: ~32 MiB for qfec_*_host, ~16 MiB of
  *                      caller shards for module/rs.h on host pointers)
  *   "host_threads"     host threads that gather / scatter module/rs.h host shard pointers (0: the

@@ -153,6 +153,7 @@ struct Tuning {
     std::atomic<int> host_threads{0};   // host copy threads for module/rs.h on host pointers (0: usable CPUs, <= 32)
     std::atomic<int> host_zero_copy{1}; // pinned host batches: kernels read/write them directly (0: staged copies)
     std::atomic<int> host_lanes{4};     // module/rs.h on host pointers: chunk slots in flight on the device (2..8)
+    std::atomic<int> host_nt{2};        // module/rs.h on host pointers: streaming stores into the slots (0 / 1 / 2 sequential rows)
     std::atomic<int> encode_lds{-1};    // LDS bytes per encode block, capping waves per CU (-1 auto, 0 none)
 };
 Tuning& tuning();

@@ -4,6 +4,8 @@
 // mixes are staged row by row.
 #include "qfec_rt.hpp"
 
+#include <immintrin.h>
+
 using namespace qfec;
 
 // ====================================================================== host-buffer paths
@@ -177,6 +179,48 @@ uint8_t* rs_slot_dev(DevCtx::HostSlot& h, bool zc) {
     return nullptr;
 }
 
+// a caller row into a pinned slot with streaming stores (tuning "host_nt"): the slot is read next by
+// the device (DMA or zero-copy reads over PCIe), not by this CPU, so its lines need not be fetched
+// for ownership first; the caller's thread fences (sfence) before the slot is handed over
+inline void copy_row_nt(uint8_t* dst, const uint8_t* src, size_t len) {
+    if (((uintptr_t)dst & 15) || len < 64) {
+        memcpy(dst, src, len);
+        return;
+    }
+    size_t i = 0;
+    for (; i + 64 <= len; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    if (i < len) memcpy(dst + i, src + i, len - i);
+}
+
+// one thread's run of row copies into a slot.  Streaming stores pay when the caller's rows follow one
+// another in memory (the loads stream, and the stores' ownership reads are the traffic saved); on rows
+// at scattered places the loads are latency-bound and the streaming stores lose (profiles/r06r).  So
+// host_nt 2 (the default) streams a row only when it starts where the previous row of the same run
+// ended (up to 4 KiB on); 1 streams every row, 0 none.
+struct RowRun {
+    int mode;
+    size_t len;
+    uintptr_t next = 0;
+    void operator()(uint8_t* dst, const uint8_t* src) {
+        const bool seq = (uintptr_t)src - next <= 4096;
+        next = (uintptr_t)src + len;
+        if (mode == 1 || (mode == 2 && seq)) copy_row_nt(dst, src, len);
+        else memcpy(dst, src, len);
+    }
+    void fence() const {
+        if (mode) _mm_sfence();
+    }
+};
+
 // ---- where the host-pointer pipelines run their chunks: host_lanes slots on the calling thread's
 // device (its context's own host slots; 4 by default: at config 2's shape, interleaved in one
 // process, 2 / 4 / 6 / 8 slots 35.6 / 43.3 / 43.4 / 42.7 GiB/s, profiles/r06o), or two slots per entry of the list
@@ -348,10 +392,18 @@ int rs_encode_pipe(DevCtx& ctx, qfec_code* c, unsigned char** data, unsigned cha
         // data rows (and, when a parity row keeps its old bytes -- the rs.c quirk -- the parity rows)
         const size_t nd = (size_t)gn * k, np = any_stale ? (size_t)gn * m : 0;
         const auto tg = std::chrono::steady_clock::now();
-        rows_job(nd + np, [&](size_t r) {
-            if (r < nd) memcpy(hd + r * pitch, data[(size_t)g0 * k + r], (size_t)B);
-            else memcpy(hp + (r - nd) * pitch, par[(size_t)g0 * m + (r - nd)], (size_t)B);
-        });
+        const int nt = tuning().host_nt;
+        pool->run(
+            [&](int t, int nth) {
+                const size_t rows = nd + np, a = rows * t / nth, b = rows * (t + 1) / nth;
+                RowRun put{nt, (size_t)B};
+                for (size_t r = a; r < b; ++r) {
+                    if (r < nd) put(hd + r * pitch, data[(size_t)g0 * k + r]);
+                    else put(hp + (r - nd) * pitch, par[(size_t)g0 * m + (r - nd)]);
+                }
+                put.fence();
+            },
+            (int)std::max<size_t>(1, (nd + np) / 64));
         tr.gather += RsTrace::since(tg);
         if (hipSetDevice(L.device) != hipSuccess) { rc = hip_fail(hipGetLastError(), "reed_solomon_encode: device"); break; }
         uint8_t* z = rs_slot_dev(h, zc);
@@ -442,7 +494,9 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const uint8_t* seed, unsigned
         todo[ln].assign((size_t)gn, 0);
         uint8_t* todo_s = todo[ln].data();
         const auto tg = std::chrono::steady_clock::now();
+        const int nt = tuning().host_nt;
         groups_job(gn, [&](long long a, long long b) {
+            RowRun put_d{nt, (size_t)B}, put_p{nt, (size_t)B};  // data rows and parity rows: two runs
             long long nf = 0;
             for (long long g = a; g < b; ++g) {
                 const size_t gg = (size_t)(g0 + g);
@@ -460,7 +514,7 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const uint8_t* seed, unsigned
                 int got = 0;
                 for (int j = 0; j < m && got < e; ++j)
                     if (!pm[j]) {
-                        memcpy(hp + ((size_t)g * m + j) * pitch, par[gg * m + j], (size_t)B);
+                        put_p(hp + ((size_t)g * m + j) * pitch, par[gg * m + j]);
                         ++got;
                     }
                 if (got < e) {  // under-determined: left as it is (rs.c:630-634)
@@ -469,9 +523,10 @@ int rs_reconstruct_pipe(DevCtx& ctx, qfec_code* c, const uint8_t* seed, unsigned
                 }
                 const bool sd = seed[mask] != 0;
                 for (int x = 0; x < k; ++x)
-                    if (!dm[x] || sd) memcpy(hd + ((size_t)g * k + x) * pitch, data[gg * k + x], (size_t)B);
+                    if (!dm[x] || sd) put_d(hd + ((size_t)g * k + x) * pitch, data[gg * k + x]);
                 todo_s[g] = 1;
             }
+            put_d.fence();
             fails += nf;
         });
         tr.gather += RsTrace::since(tg);

@@ -650,6 +650,7 @@ const std::vector<Knob>& knob_table() {
         {"wire_rx", &tuning().wire_rx, 0, 5},
         {"host_zero_copy", &tuning().host_zero_copy, 0, 1},
         {"host_lanes", &tuning().host_lanes, 2, 8},
+        {"host_nt", &tuning().host_nt, 0, 2},
         {"percall_fast", &g_percall_fast, 0, 1},
         {"percall_group", &g_percall_group, 0, 1},
         {"percall_fault", &g_percall_fault, 0, 2},

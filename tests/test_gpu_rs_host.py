@@ -123,6 +123,49 @@ def test_rs_host_reconstruct_pipeline_vs_oracle(oracle, knobs, k, m, B, zero_cop
     rs.close()
 
 
+@pytest.mark.parametrize("B", [40, 1000, 1400])
+@pytest.mark.parametrize("layout", ["contiguous", "scattered"])
+@pytest.mark.parametrize("nt", [0, 1, 2])
+def test_rs_host_streaming_rows_vs_oracle(oracle, knobs, B, layout, nt):
+    """The slot gathers with streaming stores (host_nt 1: every row; 2, the default: rows that start
+    where the previous row of the run ended; 0: none), over rows that follow one another in memory
+    (data and parity each one batch at pitch B, so mode 2 streams them) and rows scattered at
+    misaligned places; B = 40 takes the short-row copy, 1000 a tail after the 64-B steps.  Encode,
+    then reconstruct, both equal to the oracle."""
+    knobs("host_nt", nt)
+    knobs("host_chunk", 13)
+    k, m, G = 10, 3, 97
+    n = k + m
+    if layout == "contiguous":
+        dbuf = np.zeros((G * k, B), np.uint8)
+        pbuf = np.zeros((G * m, B), np.uint8)
+        rows = list(dbuf) + list(pbuf)
+    else:
+        rows, _keep = scattered_rows(G, n, B, 9)
+    data0 = synth_bytes(0x57EA + B, G * k * B).reshape(G, k, B)
+    for i in range(G * k):
+        rows[i][:] = data0.reshape(G * k, B)[i]
+    ptrs = ptr_array(rows)
+    rs = qa.ReedSolomon(k, m)
+    L = qa.lib()
+    assert L.reed_solomon_encode(rs._h, ptrs, G * n, B) == 0
+    par = np.zeros((G, m, B), np.uint8)
+    oracle.rs_encode(oracle.cauchy(k, m), data0, par, B)
+    assert np.array_equal(np.stack(rows[G * k:]).reshape(G, m, B), par)
+    gm = mixed_marks(G, k, m, 23)
+    marks = marks_to_rs_layout(gm, k)
+    d = data0.copy()
+    d.reshape(G * k, B)[marks[:G * k] == 1] = 0x5A
+    for i in range(G * k):
+        rows[i][:] = d.reshape(G * k, B)[i]
+    rc = L.reed_solomon_reconstruct(rs._h, ptrs, C.c_void_p(marks.ctypes.data), G * n, B)
+    exp = d.copy()
+    rc_o = oracle.rs_reconstruct(oracle.cauchy(k, m), exp, par.copy(), marks, B)
+    assert rc == rc_o == -1
+    assert np.array_equal(np.stack(rows[:G * k]).reshape(G, k, B), exp)
+    rs.close()
+
+
 @pytest.mark.parametrize("layout", ["host", "mixed"])
 def test_rs_wide_code_host_pointers(oracle, capfd, monkeypatch, layout):
     """n = k + m > 24 (no pattern LUT: per-chunk decode records) on host shard pointers.
@@ -305,9 +348,9 @@ def test_rs_mixed_host_device_pointers(oracle, pattern):
 
 def test_rs_host_while_tuning(oracle):
     """Encodes and reconstructs on host pointers from two threads while a third flips the host
-    knobs (chunking, copy threads, zero copy): every result still equals the oracle's."""
+    knobs (chunking, copy threads, zero copy, lanes, streaming stores): every result still equals the oracle's."""
     import threading
-    keys = ("host_chunk", "host_threads", "host_zero_copy", "host_lanes")
+    keys = ("host_chunk", "host_threads", "host_zero_copy", "host_lanes", "host_nt")
     before = {k: qa.tune_get(k) for k in keys}
     stop = threading.Event()
     errors = []
@@ -319,6 +362,7 @@ def test_rs_host_while_tuning(oracle):
             qa.tune("host_threads", (0, 1, 3)[i % 3])
             qa.tune("host_zero_copy", i & 1)
             qa.tune("host_lanes", (2, 4, 8)[i % 3])
+            qa.tune("host_nt", (2, 0, 1, 2)[i % 4])
             i += 1
 
     def coder(seed):
