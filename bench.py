@@ -700,8 +700,17 @@ def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=2
         # PMC traffic of this rank's launches (tools/pmc_traffic.py --erasures 4, the same shape and
         # group count through bench.py's headline leg; keyed by the rank's group count)
         tr, src = load_traffic(TRAFFIC_PATH, f"rs{k}_{m}_b{B}_g{G}_e{E}")
+        scale = 1.0
+        if tr is None and G != Gt:
+            # N > 1 shards config 4's groups: the counters were taken on the whole batch in one launch
+            # (N = 1); a launch streams each group's rows once, so its bytes scale with the groups
+            tr, src0 = load_traffic(TRAFFIC_PATH, f"rs{k}_{m}_b{B}_g{Gt}_e{E}")
+            if isinstance(tr, dict):
+                scale = G / Gt
+                src = f"scaled by {G}/{Gt} groups from {src0}"
         if isinstance(tr, dict):
             et, dt = tr.get("encode_bytes_per_launch"), tr.get("reconstruct_bytes_per_launch")
+            et, dt = (et * scale if et else et), (dt * scale if dt else dt)
             out["rank0_traffic"] = {"encode_bytes_per_launch": et, "reconstruct_bytes_per_launch": dt,
                                     "encode_traffic_over_alg": round(et / enc_alg, 4) if et else None,
                                     "reconstruct_traffic_over_alg": round(dt / dec_alg, 4) if dt else None}
