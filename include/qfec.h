@@ -282,13 +282,16 @@ int qfec_probe_reconstruct(unsigned char *d_data, const unsigned char *d_parity,
  *                      is set to 1 again (the abandoned block's buffers stay allocated)
  *   "percall_fast"     1 per-packet calls on host packets through the server / one launch on mapped
  *                      pinned staging | 0 the staged DMA path (the one device-pointer packets take)
- *   "encode_lds"       -1 auto | 0 none | N: bytes of LDS each 256-thread encode block allocates (and
- *                      does not use), of the CU's 160 KiB: a cap on the encode's resident waves per CU.
- *                      Auto caps device-resident launches of >= 8 192 blocks at 16 waves per CU, 24
- *                      for the two-half inputs on rows <= 1 KiB, 8 for k = 10 from 16 384 blocks
+ *   "encode_lds"       -1 auto | 0 none | N: bytes of LDS each encode block allocates (and does not
+ *                      use), of the CU's 160 KiB: a cap on the encode's resident waves per CU.  Auto
+ *                      caps device-resident launches of >= 8 192 256-thread blocks at 16 waves per CU,
+ *                      24 for the two-half inputs on rows <= 1 KiB, and runs k = 10 (all rows in
+ *                      registers, rows >= 1 KiB, >= 2^21 lanes) as one-wave blocks held at 10 per CU
  *                      (fewer concurrent row streams move more bytes per second through HBM); k <= 2
  *                      and encodes of host memory are never capped.  The XOR probe follows the same
- *                      rule for its k
+ *                      rule for its k (on one-wave blocks at 6 per CU, where its stream runs best)
+ *   "encode_block"     -1 auto (64 where the rule above says so, else 256) | 64 | 256: threads per
+ *                      encode block
  * A/B, one per kernel family:
  *   "encode_impl"      -1 auto (2 for k >= 16, else 0) | 0 all rows | 2 all rows, the inputs loaded in
  *                      two halves (fewer registers, more waves per SIMD)

@@ -47,6 +47,7 @@ struct EncodeArgs {
     int vec16;
     int impl;               // tuning "encode_impl"
     int lds;                // dynamic LDS bytes per block, a residency cap: -1 auto, 0 none (tuning "encode_lds")
+    int block;              // threads per block: -1 auto, 64, 256 (tuning "encode_block")
 };
 
 struct ReconArgs {
@@ -154,6 +155,7 @@ struct Tuning {
     std::atomic<int> host_zero_copy{1}; // pinned host batches: kernels read/write them directly (0: staged copies)
     std::atomic<int> host_lanes{4};     // module/rs.h on host pointers: chunk slots in flight on the device (2..8)
     std::atomic<int> host_nt{2};        // module/rs.h on host pointers: streaming stores into the slots (0 / 1 / 2 sequential rows)
+    std::atomic<int> encode_block{-1};  // threads per encode block: -1 auto (64 for k = 10 all-rows), 64, 256
     std::atomic<int> encode_lds{-1};    // LDS bytes per encode block, capping waves per CU (-1 auto, 0 none)
 };
 Tuning& tuning();

@@ -42,9 +42,9 @@ namespace qfec {
 // tab layout: [rows][k][QFEC_TAB_STRIDE] dwords; dword 5 of (r, 0) = 1 if row r starts
 // from the destination's previous bytes (rs.c column-0 zero-coefficient quirk).
 
-template <int K, int M>
+template <int K, int M, int BS = 256>
 __global__ void __launch_bounds__(256) k_encode_perm(EncodeArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t t = (uint64_t)blockIdx.x * (uint64_t)BS + threadIdx.x;
     if (t >= a.work) return;
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
@@ -85,10 +85,10 @@ __global__ void __launch_bounds__(256) k_encode_perm(EncodeArgs a) {
 // only after the first half has been multiplied in -- half the input registers live at a time
 // (RS(16,4): 69 instead of 116 VGPRs, 7 waves per SIMD instead of 4; RS(10,3): 60 instead of 102),
 // so more waves share the memory latency; each wave has one round trip more.  Same VALU as impl 0.
-template <int K, int M>
+template <int K, int M, int BS = 256>
 __global__ void __launch_bounds__(256) k_encode_perm_halves(EncodeArgs a) {
     constexpr int H = (K + 1) / 2;
-    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t t = (uint64_t)blockIdx.x * (uint64_t)BS + threadIdx.x;
     if (t >= a.work) return;
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
@@ -558,8 +558,9 @@ __global__ void __launch_bounds__(256) k_synth_fill(uint8_t* p, uint64_t nbytes,
 
 // streaming probe with the encode's traffic shape (k rows in, m rows out, XOR only):
 // the memory-side ceiling the GF arithmetic is measured against.
+template <int BS = 256>
 __global__ void __launch_bounds__(256) k_probe_xor(EncodeArgs a) {
-    const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t t = (uint64_t)blockIdx.x * (uint64_t)BS + threadIdx.x;
     if (t >= a.work) return;
     const uint64_t g = fast_div(t, a.cols_div);
     const uint32_t col = (uint32_t)(t - g * (uint64_t)a.cols);
@@ -663,8 +664,22 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
 // Launches under 8 192 blocks keep every slot (RS(16,4) B=1400 at 31 250 groups, config 4's share
 // of 8 ranks, 10 742 blocks: +4 %, profiles/r05ap).  The reconstruct and the
 // datagram kernels lose with any cap (profiles/r05ak, r05al) and have none.
-static inline size_t enc_lds(const EncodeArgs& a, int K, int im, unsigned grid) {
+// One-wave blocks (tuning "encode_block" -1 auto, 64, 256; round 6): the all-rows body of k = 10
+// on rows of at least 1 KiB (64 16-B columns) in launches of >= 2^21 lanes runs 64-thread blocks
+// held at 10 per CU (16 KiB of LDS each): RS(10,3) B=1024 100 000 groups 200.1 / 201.4 against
+// 209.2 / 210.4 us, B=1400 276.6 against 292.0, 50 000 groups 102.1 against 109.5; equal at 25 000
+// and 17 000 groups; B=512 not better (108-111 against 108), so left out (interleaved,
+// profiles/r06_enc/).  Blocks of one wave leave a CU's slots one wave at a time and can hold 10
+// waves, which 4-wave blocks cannot (8 or 12).  RS(16,4) (the two-half body), RS(4,2), RS(16,4)
+// B=1024 and every reconstruct body measured no gain from them (r06z_*): 256-thread blocks there.
+static inline unsigned enc_block(const EncodeArgs& a, int K, int im) {
+    if (a.block == 64 || a.block == 256) return (unsigned)a.block;
+    return im == 0 && K == 10 && a.cols >= 64 && a.work >= (8192ull << 8) ? 64u : 256u;
+}
+
+static inline size_t enc_lds(const EncodeArgs& a, int K, int im, unsigned grid, unsigned bs = 256) {
     if (a.lds >= 0) return (size_t)a.lds;
+    if (bs == 64) return 16384;
     if (grid < 8192 || K <= 2) return 0;
     if (im == 0 && K == 10) return a.cols >= 32 && grid >= 16384 ? 65536 : 40960;
     if (im == 2 && a.cols <= 64) return 27000;
@@ -674,9 +689,14 @@ static inline size_t enc_lds(const EncodeArgs& a, int K, int im, unsigned grid) 
 #define QFEC_ENC_CASE(KK, MM)                                                                 \
     if (a.k == KK && a.m == MM) {                                                             \
         const int im = a.impl < 0 ? (KK >= 16 ? 2 : 0) : a.impl;                              \
-        const size_t lds = enc_lds(a, KK, im, grid);                                          \
-        if (im == 2)                                                                          \
+        const unsigned bs = enc_block(a, KK, im);                                             \
+        const size_t lds = enc_lds(a, KK, im, grid, bs);                                      \
+        if (im == 2 && bs == 64)                                                              \
+            hipLaunchKernelGGL((k_encode_perm_halves<KK, MM, 64>), dim3(grid_for(a.work, 64)), dim3(64), lds, stream, a); \
+        else if (im == 2)                                                                     \
             hipLaunchKernelGGL((k_encode_perm_halves<KK, MM>), dim3(grid), dim3(256), lds, stream, a); \
+        else if (bs == 64)                                                                    \
+            hipLaunchKernelGGL((k_encode_perm<KK, MM, 64>), dim3(grid_for(a.work, 64)), dim3(64), lds, stream, a); \
         else                                                                                  \
             hipLaunchKernelGGL((k_encode_perm<KK, MM>), dim3(grid), dim3(256), lds, stream, a);  \
         return hipGetLastError();                                                             \
@@ -795,10 +815,16 @@ hipError_t launch_synth_fill(uint8_t* p, uint64_t nbytes, uint64_t seed, hipStre
 
 hipError_t launch_probe_xor(const EncodeArgs& a, hipStream_t stream) {
     if (a.work == 0) return hipSuccess;
-    // the ceiling of the shape, so at the residency the encode of that k runs with
+    // the ceiling of the shape: the encode's block rule for that k; on one-wave blocks the stream
+    // runs best at 6 per CU (27 000 B of LDS: 199.8 us against 218.5 at the encode's 10, 211.5 at
+    // 4-wave blocks x 2, RS(10,3) B=1024, profiles/r06_enc/r06ab_g100.log)
     const unsigned grid = grid_for(a.work, 256);
-    const size_t lds = enc_lds(a, a.k, 0, grid);
-    hipLaunchKernelGGL(k_probe_xor, dim3(grid), dim3(256), lds, stream, a);
+    const unsigned bs = enc_block(a, a.k, 0);
+    const size_t lds = bs == 64 && a.lds < 0 ? 27000 : enc_lds(a, a.k, 0, grid, bs);
+    if (bs == 64)
+        hipLaunchKernelGGL(k_probe_xor<64>, dim3(grid_for(a.work, 64)), dim3(64), lds, stream, a);
+    else
+        hipLaunchKernelGGL(k_probe_xor<>, dim3(grid), dim3(256), lds, stream, a);
     return hipGetLastError();
 }
 

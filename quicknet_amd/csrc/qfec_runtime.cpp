@@ -433,9 +433,10 @@ int run_encode(DevCtx& ctx, const qfec_code* c, const uint32_t* tab, int m, cons
     a.pitch = (uint64_t)pitch;
     a.vec16 = vec16_ok(d_data, d_par, block, pitch) ? 1 : 0;
     a.impl = tuning().encode_impl;
-    // a cap on resident waves pays in HBM (qfec_kernels.hip launch_encode), not over PCIe, where
-    // latency wants every wave the registers allow
+    // a cap on resident waves (and the one-wave blocks held to 10 per CU) pays in HBM
+    // (qfec_kernels.hip launch_encode), not over PCIe, where latency wants every wave the registers allow
     a.lds = host_mem ? 0 : tuning().encode_lds.load();
+    a.block = host_mem ? 256 : tuning().encode_block.load();
     a.cols = a.vec16 ? (uint32_t)((block + 15) / 16) : (uint32_t)block;
     a.cols_div = make_div_magic(a.cols);
     a.dgs = dgs >= 0 ? (uint64_t)dgs : (uint64_t)c->k * pitch;
@@ -659,6 +660,7 @@ const std::vector<Knob>& knob_table() {
         {"percall_idle_us", &g_percall_idle_us, 0, 1000000},
         {"percall_resident", &g_percall_resident, 0, 1},
         {"encode_lds", &tuning().encode_lds, -1, 163840},
+        {"encode_block", &tuning().encode_block, -1, 256},
     };
     return t;
 }
@@ -695,6 +697,7 @@ int qfec_tune(const char* key, int value) {
         if (strcmp(key, kn.key)) continue;
         if (value < kn.lo || value > kn.hi) break;
         if (!strcmp(key, "recon_impl") && value != -1 && value != 2 && value != 3 && value != 4 && value != 8) break;
+        if (!strcmp(key, "encode_block") && value != -1 && value != 64 && value != 256) break;
         if (!strcmp(key, "encode_impl") && value == 1) break;
         kn.v->store(value);
         if (!strcmp(key, "percall_idle_us") || (!strcmp(key, "percall_resident") && !value)) stop_percall_servers();
@@ -1078,6 +1081,7 @@ int qfec_probe_stream(const unsigned char* d_data, unsigned char* d_parity, long
     a.dgs = (uint64_t)k * pitch;
     a.pgs = (uint64_t)m * pitch;
     a.lds = tuning().encode_lds.load();
+    a.block = tuning().encode_block.load();
     if (a.work >= 0x80000000ull) return QFEC_EINVAL;
     hipError_t e = launch_probe_xor(a, (hipStream_t)stream);
     return e == hipSuccess ? QFEC_OK : hip_fail(e, "probe launch");

@@ -344,14 +344,16 @@ def test_encode_impls_vs_oracle(oracle, impl, flavour, k, m, B):
 _RESID_EXPECT = {}
 
 
-@pytest.mark.parametrize("lds", [-1, 0, 40960, 65536, 163840])
+@pytest.mark.parametrize("block", [-1, 64, 256])
+@pytest.mark.parametrize("lds", [-1, 0, 16384, 40960, 65536, 163840])
 @pytest.mark.parametrize("k,m,B,G", [(10, 3, 1024, 70000), (16, 4, 1400, 24000), (16, 4, 1024, 33000),
                                      (4, 2, 1024, 33000), (3, 2, 512, 66000)])
-def test_encode_residency_caps_vs_oracle(oracle, lds, k, m, B, G):
+def test_encode_residency_caps_vs_oracle(oracle, block, lds, k, m, B, G):
     """The encode's residency cap (tuning "encode_lds": -1 auto, 0 none, else LDS bytes per block)
-    changes only how many waves share a CU: outputs equal the oracle's at every setting, on
-    launches large enough (>= 8 192 blocks) for the auto rule to apply (RS(10,3) at 100 000 groups,
-    the 8-wave rule, is test_large_batch_roundtrip)."""
+    and block size (tuning "encode_block": -1 auto -- one-wave blocks for k = 10 --, 64, 256)
+    change only how many waves share a CU: outputs equal the oracle's at every setting, on
+    launches large enough (>= 8 192 blocks) for the auto rule to apply (RS(10,3) at 100 000 groups
+    is test_large_batch_roundtrip)."""
     assert G * round16(B) // 16 >= 8192 * 256
     code = qa.Code.cauchy(k, m)
     key = (k, m, B, G)
@@ -364,11 +366,13 @@ def test_encode_residency_caps_vs_oracle(oracle, lds, k, m, B, G):
     d, expect = _RESID_EXPECT[key]
     p = torch.full((G, m, round16(B)), 0x5A, dtype=torch.uint8, device=DEV)
     qa.tune("encode_lds", lds)
+    qa.tune("encode_block", block)
     try:
         code.encode(d, p, B)
         torch.cuda.synchronize()
     finally:
         qa.tune("encode_lds", -1)
+        qa.tune("encode_block", -1)
     assert np.array_equal(p.cpu().numpy()[..., :B], expect)
 
 

@@ -46,6 +46,8 @@ def main():
     p.add_argument("--patterns", type=int, default=0, help="draw each group's erasures from this many masks")
     p.add_argument("--pairs", action="store_true", help="time reconstruct right after encode, as bench.py does")
     p.add_argument("--probe-lds", default="0", help="reconstruct skeleton probe: LDS bytes per block to try")
+    p.add_argument("--probe-sweep", default="", help="XOR probe block:lds pairs")
+    p.add_argument("--enc-sweep", default="", help="encode block:lds[:impl] triples, e.g. 64:16384,256:65536:2")
     a = p.parse_args()
     k, m, B, G = a.k, a.m, a.block, a.groups
     dev = torch.device("cuda:0")
@@ -99,6 +101,16 @@ def main():
         ("recon impl8 (impl3, one group per block)", lambda: qa.tune("recon_impl", 8), rec, dec_bytes),
     ]
 
+    for spec in [x for x in a.enc_sweep.split(",") if x]:
+        f = [int(v) for v in spec.split(":")]
+        bs, lds, im = f[0], f[1], (f[2] if len(f) > 2 else 0)
+        variants.append((f"encode bs{bs} lds{lds} impl{im}",
+                         lambda bs=bs, lds=lds, im=im: (qa.tune("encode_impl", im), qa.tune("encode_block", bs),
+                                                        qa.tune("encode_lds", lds)), enc, enc_bytes))
+    for spec in [x for x in a.probe_sweep.split(",") if x]:
+        bs, lds = (int(v) for v in spec.split(":"))
+        variants.append((f"probe xor bs{bs} lds{lds}", lambda bs=bs, lds=lds: (qa.tune("encode_block", bs),
+                                                                             qa.tune("encode_lds", lds)), probe, enc_bytes))
     skel = data.clone()
 
     # the reconstruct's memory skeleton (XOR, garbage into skel's erased rows) at LDS residency caps
@@ -122,6 +134,8 @@ def main():
     for r in range(a.rounds):
         for name, setup, fn, _ in variants:
             qa.set_kernel_variant(0)
+            qa.tune("encode_lds", -1)
+            qa.tune("encode_block", -1)
             setup()
             if r == 0 and fn is rec:
                 work.copy_(damaged)
@@ -130,6 +144,10 @@ def main():
                 torch.cuda.synchronize()
                 assert torch.equal(work[..., :B], data[..., :B]), f"{name}: wrong output"
                 print(f"  {name}: output checked", flush=True)
+            if r == 0 and fn is enc:
+                torch.cuda.synchronize()
+                assert torch.equal(par[..., :B], ref_par[..., :B]), f"{name}: wrong parity"
+                print(f"  {name}: parity checked", flush=True)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(a.reps):
@@ -171,6 +189,8 @@ def main():
     qa.set_kernel_variant(0)
     qa.tune("encode_impl", -1)
     qa.tune("recon_impl", -1)
+    qa.tune("encode_lds", -1)
+    qa.tune("encode_block", -1)
     code.encode(data, par, B)
     torch.cuda.synchronize()
     assert torch.equal(par, ref_par)

@@ -21,7 +21,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"encode": "k_encode_perm<{k}, {m}>", "reconstruct": "k_reconstruct_perm<{k}, {m},", "probe": "k_probe_xor"}
+KERNELS = {"encode": "k_encode_perm<{k}, {m},", "reconstruct": "k_reconstruct_perm<{k}, {m},", "probe": "k_probe_xor"}
 # --workload wire: bench.py's `wire` leg (tools/side_legs.py), RS(10,13) 1 KiB payloads
 WIRE_KERNELS = {"pack": "k_pack_wave64<10, 3, 1, 0, 1, 16, 0>", "unpack": "k_rx<10, 3, 4, false, true>",
                 "pack_frames": "k_pack_wave64<10, 3, 1, 4, 1, 16, 0>", "unpack_frames": "k_rx<10, 3, 4, true, true>"}
@@ -118,7 +118,7 @@ def config4_main(a):
     """PMC bytes per launch of bench.py's config 4 leg (RS(16,4) 1400 B, 4 erasures, --config4-groups
     groups on one rank): its encode (inputs in halves) and reconstruct (8-B lanes, one group per block)."""
     G = a.groups
-    kernels = {"encode": "k_encode_perm_halves<16, 4>", "reconstruct": "k_reconstruct_perm<16, 4, 8>"}
+    kernels = {"encode": "k_encode_perm_halves<16, 4,", "reconstruct": "k_reconstruct_perm<16, 4, 8>"}
     args = ["--config4-only", "--config4-groups", str(G), "--steps", "5", "--warmup", "1"]
     fetch = run_pass("FETCH_SIZE", a.out, args, 16, 4, kernels)
     write = run_pass("WRITE_SIZE", a.out, args, 16, 4, kernels)
