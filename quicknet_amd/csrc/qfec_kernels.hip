@@ -672,9 +672,11 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
 // profiles/r06_enc/).  Blocks of one wave leave a CU's slots one wave at a time and can hold 10
 // waves, which 4-wave blocks cannot (8 or 12).  RS(16,4) (the two-half body), RS(4,2), RS(16,4)
 // B=1024 and every reconstruct body measured no gain from them (r06z_*): 256-thread blocks there.
+// Over the other templated shapes (r06ak): RS(8,2) 172.5 -> 156.2 us and RS(6,2) 132.6 -> 124.6 at
+// 10 per CU; RS(8,4), RS(12,4) and RS(5,3) within 1.3 %: the rule takes 6 <= k <= 10 with m <= 3.
 static inline unsigned enc_block(const EncodeArgs& a, int K, int im) {
     if (a.block == 64 || a.block == 256) return (unsigned)a.block;
-    return im == 0 && K == 10 && a.cols >= 64 && a.work >= (8192ull << 8) ? 64u : 256u;
+    return im == 0 && K >= 6 && K <= 10 && a.m <= 3 && a.cols >= 64 && a.work >= (8192ull << 8) ? 64u : 256u;
 }
 
 static inline size_t enc_lds(const EncodeArgs& a, int K, int im, unsigned grid, unsigned bs = 256) {

@@ -347,7 +347,8 @@ _RESID_EXPECT = {}
 @pytest.mark.parametrize("block", [-1, 64, 256])
 @pytest.mark.parametrize("lds", [-1, 0, 16384, 40960, 65536, 163840])
 @pytest.mark.parametrize("k,m,B,G", [(10, 3, 1024, 70000), (16, 4, 1400, 24000), (16, 4, 1024, 33000),
-                                     (4, 2, 1024, 33000), (3, 2, 512, 66000)])
+                                     (4, 2, 1024, 33000), (3, 2, 512, 66000), (8, 2, 1024, 40000),
+                                     (6, 2, 1400, 40000)])
 def test_encode_residency_caps_vs_oracle(oracle, block, lds, k, m, B, G):
     """The encode's residency cap (tuning "encode_lds": -1 auto, 0 none, else LDS bytes per block)
     and block size (tuning "encode_block": -1 auto -- one-wave blocks for k = 10 --, 64, 256)
