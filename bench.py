@@ -699,18 +699,9 @@ def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=2
         out["rank0_reconstruct_skeleton"] = skel
         # PMC traffic of this rank's launches (tools/pmc_traffic.py --erasures 4, the same shape and
         # group count through bench.py's headline leg; keyed by the rank's group count)
-        tr, src = load_traffic(TRAFFIC_PATH, f"rs{k}_{m}_b{B}_g{G}_e{E}")
-        scale = 1.0
-        if tr is None and G != Gt:
-            # N > 1 shards config 4's groups: the counters were taken on the whole batch in one launch
-            # (N = 1); a launch streams each group's rows once, so its bytes scale with the groups
-            tr, src0 = load_traffic(TRAFFIC_PATH, f"rs{k}_{m}_b{B}_g{Gt}_e{E}")
-            if isinstance(tr, dict):
-                scale = G / Gt
-                src = f"scaled by {G}/{Gt} groups from {src0}"
+        tr, src = config4_traffic(TRAFFIC_PATH, k, m, B, G, Gt, E)
         if isinstance(tr, dict):
             et, dt = tr.get("encode_bytes_per_launch"), tr.get("reconstruct_bytes_per_launch")
-            et, dt = (et * scale if et else et), (dt * scale if dt else dt)
             out["rank0_traffic"] = {"encode_bytes_per_launch": et, "reconstruct_bytes_per_launch": dt,
                                     "encode_traffic_over_alg": round(et / enc_alg, 4) if et else None,
                                     "reconstruct_traffic_over_alg": round(dt / dec_alg, 4) if dt else None}
@@ -718,6 +709,25 @@ def config4_sharded(rank, world, groups=250_000, steps=20, warmup=5, spinup_ms=2
     del data, parity, work, marks
     torch.cuda.empty_cache()
     return out
+
+
+def config4_traffic(path, k, m, B, G, Gt, E):
+    """PMC bytes per launch of config 4's encode and reconstruct at this rank's G groups: the entry
+    for G itself, else (N > 1 shards the Gt groups) the whole batch's entry, taken at N = 1 in one
+    launch, scaled by G / Gt -- a launch streams each group's rows once, so its bytes scale with
+    the groups.  Returns (dict or None, source text)."""
+    tr, src = load_traffic(path, f"rs{k}_{m}_b{B}_g{G}_e{E}")
+    if tr is not None or G == Gt:
+        return tr, src
+    full, src0 = load_traffic(path, f"rs{k}_{m}_b{B}_g{Gt}_e{E}")
+    if not isinstance(full, dict):
+        return None, src
+    f = G / Gt
+    scaled = dict(full)
+    for key in ("encode_bytes_per_launch", "reconstruct_bytes_per_launch"):
+        if full.get(key):
+            scaled[key] = full[key] * f
+    return scaled, f"scaled by {G}/{Gt} groups from {src0}"
 
 
 def wire_leg(rank, G=100_000, k=10, m=3, S=1024, steps=20, warmup=10, spinup_ms=25.0):
