@@ -318,14 +318,17 @@ def test_probe_reconstruct_writes_only_erased_rows(k, m, B, lds):
                              to_dev(np.zeros(24, np.uint8)), 64)
 
 
+@pytest.mark.parametrize("block", [-1, 64])
 @pytest.mark.parametrize("impl", [-1, 0, 2])
 @pytest.mark.parametrize("flavour", ["cauchy", "vandermonde"])
-@pytest.mark.parametrize("k,m,B", [(10, 3, 1024), (16, 4, 1400), (10, 3, 100), (16, 4, 8)])
-def test_encode_impls_vs_oracle(oracle, impl, flavour, k, m, B):
+@pytest.mark.parametrize("k,m,B,G", [(10, 3, 1024, 300), (16, 4, 1400, 300), (10, 3, 100, 300), (16, 4, 8, 300),
+                                     (8, 2, 1400, 7), (6, 2, 1008, 13), (10, 3, 1400, 1)])
+def test_encode_impls_vs_oracle(oracle, block, impl, flavour, k, m, B, G):
     """The encode bodies (-1 auto, 0 all rows at once, 2 all rows with the inputs
-    loaded in halves) against the oracle's restatement of rs.c's code_some_shards on 300 random
-    groups (the rs.c quirk included: parity pre-filled with 0x5A)."""
-    G = 300
+    loaded in halves) against the oracle's restatement of rs.c's code_some_shards on random
+    groups (the rs.c quirk included: parity pre-filled with 0x5A), on the auto blocks and forced
+    onto one-wave blocks (tuning "encode_block" 64), group counts that leave the last block part
+    empty and lanes that straddle groups (B = 1400: 88 columns)."""
     code = qa.Code.cauchy(k, m) if flavour == "cauchy" else qa.Code.vandermonde(k, m)
     data = synth_bytes(k * 13 + B, G * k * B).reshape(G, k, B)
     expect = np.zeros((G, m, B), np.uint8)
@@ -333,11 +336,13 @@ def test_encode_impls_vs_oracle(oracle, impl, flavour, k, m, B):
     pitch = round16(B)
     p = to_dev(np.full((G, m, pitch), 0x5A, np.uint8))
     qa.tune("encode_impl", impl)
+    qa.tune("encode_block", block)
     try:
         code.encode(to_dev(padded(data, pitch, 0xC3)), p, B)
         torch.cuda.synchronize()
     finally:
         qa.tune("encode_impl", -1)
+        qa.tune("encode_block", -1)
     assert np.array_equal(p.cpu().numpy()[..., :B], expect)
 
 
