@@ -286,7 +286,8 @@ int qfec_probe_reconstruct(unsigned char *d_data, const unsigned char *d_parity,
  *                      use), of the CU's 160 KiB: a cap on the encode's resident waves per CU.  Auto
  *                      caps device-resident launches of >= 8 192 256-thread blocks at 16 waves per CU,
  *                      24 for the two-half inputs on rows <= 1 KiB, and runs 6 <= k <= 10 with m <= 3
- *                      (all rows in registers, rows >= 1 KiB, >= 2^21 lanes) as one-wave blocks held
+ *                      (all rows in registers, rows >= 1 KiB with 128-B-aligned pitch, strides and
+ *                      bases, >= 2^21 lanes) as one-wave blocks held
  *                      at 10 per CU (fewer concurrent row streams move more bytes per second through
  *                      HBM); k <= 2
  *                      and encodes of host memory are never capped.  The XOR probe follows the same

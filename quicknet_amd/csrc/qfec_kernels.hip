@@ -674,9 +674,15 @@ static inline unsigned grid_for(uint64_t work, unsigned block) {
 // B=1024 and every reconstruct body measured no gain from them (r06z_*): 256-thread blocks there.
 // Over the other templated shapes (r06ak): RS(8,2) 172.5 -> 156.2 us and RS(6,2) 132.6 -> 124.6 at
 // 10 per CU; RS(8,4), RS(12,4) and RS(5,3) within 1.3 %: the rule takes 6 <= k <= 10 with m <= 3.
+// Only where every wave starts on a 128-B line (pitch, group strides and bases multiples of 128 B):
+// one-wave blocks are dealt round-robin over the XCDs, and a line two waves share is then fetched
+// and written from two L2s -- RS(10,3) B=1500 (1 504-B pitch) ran 253.8 against 227.3 us on them,
+// while B=1400 (1 408 = 11 x 128) and B=2048 / 4096 gain 5.4 / 2.4 / 3.4 % (r06av).
 static inline unsigned enc_block(const EncodeArgs& a, int K, int im) {
     if (a.block == 64 || a.block == 256) return (unsigned)a.block;
-    return im == 0 && K >= 6 && K <= 10 && a.m <= 3 && a.cols >= 64 && a.work >= (8192ull << 8) ? 64u : 256u;
+    const bool lines = (a.pitch % 128 == 0) && (a.dgs % 128 == 0) && (a.pgs % 128 == 0) &&
+                       ((reinterpret_cast<uintptr_t>(a.data) | reinterpret_cast<uintptr_t>(a.parity)) % 128 == 0);
+    return im == 0 && K >= 6 && K <= 10 && a.m <= 3 && a.cols >= 64 && lines && a.work >= (8192ull << 8) ? 64u : 256u;
 }
 
 static inline size_t enc_lds(const EncodeArgs& a, int K, int im, unsigned grid, unsigned bs = 256) {
